@@ -1,0 +1,45 @@
+// Host-side launcher declarations shared by csrc/kernels/*.hip and csrc/bindings/*.cpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+void nf_throw_hip_error(hipError_t e, const char* expr, const char* file, int line);
+
+// coupling.hip
+void nf_launch_coupling_fwd(const void* st, int st_is_bf16, long ld_st_, const float* x, long ld_x,
+                            float* y, long ld_y, void* ybf, long ld_yb, float* ssav, long ld_s,
+                            float* ldj, int B, int Dh, float scale, int inverse, int ldj_init,
+                            int yb_width, hipStream_t stream);
+void nf_launch_coupling_bwd(const float* gy, long ld_gy, const float* s, long ld_s, const float* x,
+                            long ld_x, float c_scalar, const float* c_row, void* dst, long ld_dst,
+                            float* gx, long ld_gx, int B, int Dh, float scale, int gx_accumulate,
+                            int dst_pad_to, hipStream_t stream);
+
+// elbo.hip
+void nf_launch_target_logp_grad(int kind, const float* A, long lda, const float* Bh, long ldb,
+                                float* gA, long ldga, float* gB, long ldgb, int grad_accumulate,
+                                const float* params, float p0, float p1, float p2, float cst,
+                                const float* beta_ptr, float beta_host, float row_weight,
+                                const float* logq0, const float* ldj, float* logp_out,
+                                float* frow_out, int B, int Dh, hipStream_t stream);
+void nf_launch_bernoulli_logits(const void* logits, int is_bf16, long ldl_, const float* x, long ldx,
+                                void* dlogits, long ldd, const float* coef_ptr, float coef_host,
+                                float* logpx, int B, int P, hipStream_t stream);
+
+// sampling.hip
+void nf_launch_reparam_sample(const float* mu, const float* logvar, uint64_t seed,
+                              const int64_t* offset_ptr, int64_t offset_host, uint32_t stream_id,
+                              float* z, long ldz, float* eps, long lde, void* zbf, long ldzb,
+                              int nbf, float* logq0, int B, int D, hipStream_t stream);
+void nf_launch_normal_fill(float* out, long n, uint64_t seed, const int64_t* offset_ptr,
+                           int64_t offset_host, uint32_t stream_id, hipStream_t stream);
+
+// optim.hip
+void nf_launch_flat_optimizer(int kind, float* p, const float* g, float* m, float* v, void* pbf,
+                              long n, float lr, float b1, float b2, float eps, float wd,
+                              const float* step_ptr, float step_host, const float* gscale_ptr,
+                              float gscale_host, const float* skip_ptr, hipStream_t stream);
+void nf_launch_sumsq_guard(const float* x, long n, float* partial, int npartial, float* out_sumsq,
+                           float* out_skip, float* out_scale, float max_norm, float base_scale,
+                           hipStream_t stream);

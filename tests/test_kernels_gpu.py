@@ -1,0 +1,203 @@
+"""HIP kernels vs the fp32 PyTorch composites in ops/reference.py (MI355X only)."""
+import math
+
+import pytest
+import torch
+
+from vi_normflows_amd.ops import fused
+from vi_normflows_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, tol):
+    err = (a.float() - b.float()).abs().max().item()
+    scale = 1.0 + b.float().abs().max().item()
+    assert err <= tol * scale, (err, scale)
+
+
+@pytest.mark.parametrize("B,Dh", [(1, 2), (7, 392), (33, 130), (256, 392)])
+@pytest.mark.parametrize("st_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("inverse", [False, True])
+def test_coupling_fwd(gpu, B, Dh, st_dtype, inverse):
+    torch.manual_seed(0)
+    st = torch.randn(B, 2 * Dh + 5, device=gpu).to(st_dtype)[:, :2 * Dh + 3]
+    x = torch.randn(B, 2 * Dh, device=gpu)[:, Dh:]          # strided half view
+    outs = []
+    for impl in ("native", "ref"):
+        y = torch.empty(B, Dh, device=gpu)
+        ybf = torch.full((B, Dh + 6), 7.0, device=gpu, dtype=torch.bfloat16)
+        ss = torch.empty(B, Dh, device=gpu)
+        ldj = torch.full((B,), 0.5, device=gpu)
+        f = (lambda *a: torch.ops.vinf.coupling_fwd(*a)) if impl == "native" else ref.coupling_fwd
+        f(st, x, y, ybf, ss, ldj, 1.7, inverse, False)
+        outs.append((y, ybf, ss, ldj))
+    for a, b in zip(*outs):
+        _close(a, b, 2e-5 if a.dtype == torch.float32 else 1e-2)
+    assert (outs[0][1][:, Dh:] == 0).all()
+
+
+@pytest.mark.parametrize("B,Dh", [(3, 2), (64, 392), (5, 100)])
+@pytest.mark.parametrize("acc", [False, True])
+@pytest.mark.parametrize("use_row", [False, True])
+def test_coupling_bwd(gpu, B, Dh, acc, use_row):
+    torch.manual_seed(1)
+    gy = torch.randn(B, Dh, device=gpu)
+    s = torch.tanh(torch.randn(B, Dh, device=gpu)) * 1.3
+    x = torch.randn(B, Dh, device=gpu)
+    c_row = torch.randn(B, device=gpu) if use_row else None
+    res = []
+    for impl in ("native", "ref"):
+        dst = torch.full((B, 2 * Dh + 4), 3.0, device=gpu, dtype=torch.bfloat16)
+        gx = torch.ones(B, Dh, device=gpu)
+        f = torch.ops.vinf.coupling_bwd if impl == "native" else ref.coupling_bwd
+        f(gy, s, x, -0.25, c_row, dst, gx, 1.3, acc)
+        res.append((dst, gx))
+    _close(res[0][0], res[1][0], 1e-2)
+    _close(res[0][1], res[1][1], 2e-5)
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("B,Dh", [(5, 2), (40, 392)])
+def test_target_logp_grad(gpu, kind, B, Dh):
+    torch.manual_seed(2)
+    A = torch.randn(B, Dh, device=gpu)
+    Bh = torch.randn(B, 2 * Dh, device=gpu)[:, :Dh]
+    D = 2 * Dh
+    params = torch.cat([torch.randn(D, device=gpu) * 0.1, torch.rand(D, device=gpu) + 0.5])
+    beta = torch.tensor(0.7, device=gpu)
+    lq, lj = torch.randn(B, device=gpu), torch.randn(B, device=gpu)
+    res = []
+    for impl in ("native", "ref"):
+        gA, gB = torch.ones(B, Dh, device=gpu), torch.ones(B, Dh, device=gpu)
+        lp, fr = torch.empty(B, device=gpu), torch.empty(B, device=gpu)
+        f = torch.ops.vinf.target_logp_grad if impl == "native" else ref.target_logp_grad
+        f(kind, A, Bh, gA, gB, True, params if kind == 0 else None, 1.1, 0.6, 0.4, -3.0, beta,
+          1.0, 1.0 / B, lq, lj, lp, fr)
+        res.append((gA, gB, lp, fr))
+    for a, b in zip(*res):
+        _close(a, b, 2e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bernoulli_logits(gpu, dtype):
+    torch.manual_seed(3)
+    B, P = 37, 784
+    l = (torch.randn(B, P, device=gpu) * 3).to(dtype)
+    x = (torch.rand(B, P, device=gpu) > 0.5).float()
+    res = []
+    for impl in ("native", "ref"):
+        d = torch.empty(B, P, device=gpu, dtype=dtype)
+        lp = torch.empty(B, device=gpu)
+        f = torch.ops.vinf.bernoulli_logits if impl == "native" else ref.bernoulli_logits
+        f(l, x, d, None, -0.5, lp)
+        res.append((d, lp))
+    _close(res[0][0], res[1][0], 1e-2 if dtype == torch.bfloat16 else 1e-5)
+    _close(res[0][1], res[1][1], 1e-5)
+
+
+def test_reparam_sample_statistics_and_logq0(gpu):
+    B, D = 4096, 784
+    mu = torch.linspace(-1, 1, D, device=gpu)
+    lv = torch.linspace(-1, 0.5, D, device=gpu)
+    off = torch.tensor(5, dtype=torch.int64, device=gpu)
+    z = torch.empty(B, D, device=gpu)
+    e = torch.empty(B, D, device=gpu)
+    zb = torch.empty(B, 400, device=gpu, dtype=torch.bfloat16)
+    lq = torch.empty(B, device=gpu)
+    torch.ops.vinf.reparam_sample(mu, lv, 123, off, 0, 0, z, e, zb, 392, lq)
+    assert abs(e.mean().item()) < 5e-3
+    assert abs(e.std().item() - 1.0) < 5e-3
+    assert torch.allclose(z, mu + torch.exp(0.5 * lv) * e, atol=1e-5)
+    exp_lq = -0.5 * D * math.log(2 * math.pi) - 0.5 * lv.sum() - 0.5 * (e * e).sum(1)
+    assert torch.allclose(lq, exp_lq, rtol=1e-5, atol=1e-3)
+    assert torch.equal(zb[:, :392], z[:, :392].to(torch.bfloat16))
+    assert (zb[:, 392:] == 0).all()
+    # determinism and stream separation
+    z2 = torch.empty_like(z)
+    torch.ops.vinf.reparam_sample(mu, lv, 123, off, 0, 0, z2, None, None, 0, None)
+    assert torch.equal(z, z2)
+    torch.ops.vinf.reparam_sample(mu, lv, 123, off, 0, 1, z2, None, None, 0, None)
+    assert not torch.allclose(z, z2)
+    off.add_(1)
+    torch.ops.vinf.reparam_sample(mu, lv, 123, off, 0, 0, z2, None, None, 0, None)
+    assert not torch.allclose(z, z2)
+
+
+def test_normal_fill(gpu):
+    out = torch.empty(1_000_003, device=gpu)
+    torch.ops.vinf.normal_fill(out, 7, None, 3, 0)
+    assert abs(out.mean().item()) < 5e-3 and abs(out.std().item() - 1) < 5e-3
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+@pytest.mark.parametrize("n", [1, 4099, 100_000])
+def test_flat_optimizer(gpu, kind, n):
+    torch.manual_seed(4)
+    p0 = torch.randn(n, device=gpu)
+    g = torch.randn(n, device=gpu)
+    res = []
+    for impl in ("native", "ref"):
+        p, m, v = p0.clone(), torch.rand(n, device=gpu) * 0.1, torch.rand(n, device=gpu) * 0.1
+        pbf = torch.empty(n, device=gpu, dtype=torch.bfloat16)
+        step = torch.tensor(3.0, device=gpu)
+        gs = torch.tensor(0.5, device=gpu)
+        f = torch.ops.vinf.flat_optimizer if impl == "native" else ref.flat_optimizer
+        f(kind, p, g, m, v, pbf, 1e-2, 0.9, 0.99, 1e-8, 0.01, step, 1.0, gs, 1.0, None)
+        res.append((p, m, v, pbf))
+    for a, b in zip(*res):
+        _close(a, b, 1e-5 if a.dtype == torch.float32 else 1e-2)
+
+
+def test_sumsq_guard(gpu):
+    x = torch.randn(1_000_000, device=gpu)
+    part = torch.empty(512, device=gpu)
+    s, sk, sc = (torch.empty((), device=gpu) for _ in range(3))
+    torch.ops.vinf.sumsq_guard(x, part, s, sk, sc, 10.0, 0.5)
+    exp = (x.double() ** 2).sum().item() * 0.25
+    assert abs(s.item() - exp) / exp < 1e-4
+    assert sk.item() == 0.0
+    assert abs(sc.item() - 0.5 * 10.0 / math.sqrt(exp)) < 1e-3
+    x[123] = float("nan")
+    torch.ops.vinf.sumsq_guard(x, part, s, sk, sc, 0.0, 1.0)
+    assert sk.item() == 1.0
+
+
+def test_engine_gpu_fp32_matches_autograd(gpu):
+    from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI
+    from test_realnvp_engine import autograd_free_energy
+
+    cfg = RealNVPConfig(dim=10, n_layers=3, hidden=16, target="banana", anneal="none",
+                        init_out_std=0.3)
+    eng = RealNVPVI(cfg, batch=9, device=gpu, compute_dtype=torch.float32, seed=5)
+    eng._update_schedule()
+    eng.forward()
+    eng.backward()
+    params = {n: v.detach().cpu().clone().requires_grad_(True)
+              for n, v in eng.params.named_views().items()}
+    F, _ = autograd_free_energy(eng, params, eng.eps0.cpu().clone(), 1.0)
+    F.backward()
+    assert abs(eng.loss.item() - F.item()) < 1e-3 * (1 + abs(F.item()))
+    for n, p in params.items():
+        err = (eng.params.g(n).cpu() - p.grad).abs().max()
+        assert err <= 1e-3 * (1.0 + p.grad.abs().max()), n
+
+
+def test_engine_gpu_bf16_trains_and_graph_replays(gpu):
+    from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI
+    from vi_normflows_amd.parallel.dist import DistInfo
+    from vi_normflows_amd.parallel.runner import DataParallelRunner
+
+    cfg = RealNVPConfig(dim=64, n_layers=4, hidden=128, target="gaussian", anneal="none")
+    eng = RealNVPVI(cfg, batch=1024, device=gpu, lr=2e-3, seed=0)
+    run = DataParallelRunner(eng, DistInfo(device=gpu))
+    run.step()
+    first = eng.loss.item()
+    assert run.capture(warmup=2)
+    s0 = eng.step_t.item()
+    for _ in range(100):
+        run.step()
+    torch.cuda.synchronize()
+    assert eng.step_t.item() == s0 + 100
+    assert eng.loss.item() < first
+    assert math.isfinite(eng.loss.item())

@@ -1,0 +1,342 @@
+"""RealNVP variational inference engine (north-star flagship).
+
+q_K(z) is a diagonal Gaussian base pushed through ``n_layers`` affine coupling
+layers (Dinh et al. 2017); the objective is the reparameterised free energy
+
+    F = E_eps[ log q0(z0) - sum_l log|det J_l| - beta_t * log p(z_K) ],
+    z0 = mu + exp(logvar / 2) * eps,
+
+i.e. the estimator of the reference's ``optimization.optimize`` F
+(``normflows/normflows/optimization.py:66-92``) with the biases of SURVEY
+§2.6 Q1/Q7 removed (log-det of the *actual* transform, entropy term of the
+learnable base kept) and the planar flow replaced by coupling layers.
+
+MI355X-first structure (no autograd tape on the hot path):
+
+* State lives as a chain of fp32 half-vectors h_0..h_{L+1}: layer l
+  conditions on h_{l+1}, transforms h_l and writes h_{l+2}. Alternating
+  halves therefore costs no permutation/copy, and the coupling epilogue writes
+  the bf16 copy of its output that the *next* layer's conditioner GEMM reads.
+* Conditioner GEMMs are bf16 with fp32 accumulation (``ops.gemm``);
+  log-dets, the state and every reduction stay fp32.
+* Backward is explicit and per layer, so each layer's gradient slice in the
+  flat gradient buffer is final the moment its backward ends: the DP reducer
+  all-reduces those slices on a separate HIP stream while earlier layers are
+  still differentiating.
+* Every op is allocation-free on fixed buffers and all schedule state (step,
+  beta_t, RNG offset) lives on the device, so ``train_step`` can be captured
+  once into a hipGraph and replayed.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from ..ops import fused
+from ..ops import gemm
+from ..utils.flat import FlatLayout, FlatParams
+
+
+@dataclass
+class RealNVPConfig:
+    dim: int = 784
+    n_layers: int = 32
+    hidden: int = 1024
+    n_hidden: int = 2              # hidden layers per conditioner: Dh -> H (-> H)*(n-1) -> 2*Dh
+    scale_bound: float = 1.0       # s = scale_bound * tanh(s_hat)
+    target: str = "banana"         # "banana" (twisted Gaussian, log Z = 0) | "gaussian"
+    banana_sigma1: float = 1.0
+    banana_sigma2: float = 0.5
+    banana_bend: float = 0.5
+    gaussian_scale: float = 0.7
+    learn_base: bool = True
+    init_out_std: float = 1e-3     # small *random* output init (not zeros: see bench notes)
+    anneal: str = "reference"      # "reference" | "none" (beta_t schedule)
+    anneal_iters: int = 10000      # max_iter for the reference schedule
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def half(self) -> int:
+        assert self.dim % 2 == 0, "RealNVP needs an even dimension"
+        return self.dim // 2
+
+    def n_params(self) -> int:
+        Dh, H = self.half, self.hidden
+        per = Dh * H + H + (self.n_hidden - 1) * (H * H + H) + H * 2 * Dh + 2 * Dh
+        return self.n_layers * per + 2 * self.dim
+
+    def flops_per_sample(self) -> float:
+        """Forward+backward GEMM FLOPs per sample (dgrad of the first layer included)."""
+        Dh, H = self.half, self.hidden
+        macs = Dh * H + (self.n_hidden - 1) * H * H + H * 2 * Dh
+        return 6.0 * macs * self.n_layers
+
+
+def _layer_shapes(cfg: RealNVPConfig):
+    Dh, H = cfg.half, cfg.hidden
+    dims = [Dh] + [H] * cfg.n_hidden + [2 * Dh]
+    return [(dims[i + 1], dims[i]) for i in range(len(dims) - 1)]
+
+
+class RealNVPVI:
+    """Explicit-backward RealNVP VI engine over flat parameter buffers."""
+
+    def __init__(self, cfg: RealNVPConfig, batch: int, device="cuda",
+                 compute_dtype: torch.dtype | None = None, seed: int = 0, rank: int = 0,
+                 lr: float = 1e-4, optimizer: int = fused.OPT_ADAM, betas=(0.9, 0.999),
+                 eps: float = 1e-8, weight_decay: float = 0.0, max_grad_norm: float = 0.0):
+        self.cfg = cfg
+        self.B = int(batch)
+        self.device = torch.device(device)
+        if compute_dtype is None:
+            compute_dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        self.cdt = compute_dtype
+        self.seed = int(seed)
+        self.rank = int(rank)
+        self.lr, self.opt_kind, self.betas, self.eps, self.wd = lr, optimizer, betas, eps, weight_decay
+        self.max_grad_norm = float(max_grad_norm)
+        self.grad_scale_host = 1.0
+        self.unit_ready_hook = None   # callable(unit_idx) after a unit's grads are final
+
+        L = cfg.n_layers
+        layout = FlatLayout()
+        layout.add_unit([("base.mu", (cfg.dim,)), ("base.logvar", (cfg.dim,))])
+        self.shapes = _layer_shapes(cfg)
+        for l in range(L):
+            ts = []
+            for i, (o, inp) in enumerate(self.shapes):
+                ts += [(f"l{l}.W{i}", (o, inp)), (f"l{l}.b{i}", (o,))]
+            layout.add_unit(ts)
+        self.layout = layout
+        self.params = FlatParams(layout, self.device, self.cdt)
+        self._alloc_state()
+        self._alloc_workspace()
+        self.init_params(seed)
+
+    # ------------------------------------------------------------------ setup
+    def _alloc_state(self):
+        dev = self.device
+        self.step_t = torch.zeros((), dtype=torch.float32, device=dev)
+        self.rng_offset = torch.zeros((), dtype=torch.int64, device=dev)
+        self.beta = torch.ones((), dtype=torch.float32, device=dev)
+        self.loss = torch.zeros((), dtype=torch.float32, device=dev)
+        self.gnorm2 = torch.zeros((), dtype=torch.float32, device=dev)
+        self.skip = torch.zeros((), dtype=torch.float32, device=dev)
+        self.gscale = torch.ones((), dtype=torch.float32, device=dev)
+        self.n_skipped = torch.zeros((), dtype=torch.float32, device=dev)
+        self._partials = torch.zeros(512, dtype=torch.float32, device=dev)
+
+    def _alloc_workspace(self):
+        cfg, B, dev = self.cfg, self.B, self.device
+        L, Dh, H, D = cfg.n_layers, cfg.half, cfg.hidden, cfg.dim
+        f32 = torch.float32
+        self.z0 = torch.empty(B, D, dtype=f32, device=dev)
+        self.eps0 = torch.empty(B, D, dtype=f32, device=dev)
+        self.Hs = torch.empty(L, B, Dh, dtype=f32, device=dev)          # h_2 .. h_{L+1}
+        self.Hbf = torch.empty(L, B, Dh, dtype=self.cdt, device=dev)    # bf16(h_1 .. h_L)
+        self.Act = torch.empty(L, cfg.n_hidden, B, H, dtype=self.cdt, device=dev)
+        self.S = torch.empty(L, B, Dh, dtype=f32, device=dev)
+        self.st = torch.empty(B, 2 * Dh, dtype=self.cdt, device=dev)
+        self.dst = torch.empty(B, 2 * Dh, dtype=self.cdt, device=dev)
+        self.dH = [torch.empty(B, H, dtype=self.cdt, device=dev) for _ in range(2)]
+        self.G = torch.empty(L + 2, B, Dh, dtype=f32, device=dev)
+        self.logq0 = torch.empty(B, dtype=f32, device=dev)
+        self.ldj = torch.empty(B, dtype=f32, device=dev)
+        self.logp = torch.empty(B, dtype=f32, device=dev)
+        self.frow = torch.empty(B, dtype=f32, device=dev)
+        self._target_params = None
+        if cfg.target == "gaussian":
+            m = torch.zeros(D, device=dev)
+            iv = torch.full((D,), 1.0 / cfg.gaussian_scale ** 2, device=dev)
+            self._target_params = torch.cat([m, iv]).contiguous()
+
+    def h(self, i: int) -> torch.Tensor:
+        """Half-state h_i: h_0 = z0[:, Dh:], h_1 = z0[:, :Dh], h_{i>=2} = Hs[i-2]."""
+        Dh = self.cfg.half
+        if i == 0:
+            return self.z0[:, Dh:]
+        if i == 1:
+            return self.z0[:, :Dh]
+        return self.Hs[i - 2]
+
+    def zK_halves(self):
+        """(first-half, second-half) of z_K as fp32 views."""
+        L = self.cfg.n_layers
+        a, b = (L + 1, L) if (L + 1) % 2 == 1 else (L, L + 1)
+        return self.h(a), self.h(b), a, b
+
+    def init_params(self, seed: int = 0):
+        g = torch.Generator(device="cpu").manual_seed(int(seed))
+        P = self.params
+        n_lin = len(self.shapes)
+        for l in range(self.cfg.n_layers):
+            for i, (o, inp) in enumerate(self.shapes):
+                std = math.sqrt(2.0 / inp) if i < n_lin - 1 else self.cfg.init_out_std
+                P.p(f"l{l}.W{i}").copy_(torch.randn(o, inp, generator=g) * std)
+                P.p(f"l{l}.b{i}").copy_(torch.randn(o, generator=g) * (0.01 if i < n_lin - 1 else
+                                                                       self.cfg.init_out_std))
+        P.p("base.mu").zero_()
+        P.p("base.logvar").zero_()
+        P.sync_compute()
+        P.m.zero_()
+        P.v.zero_()
+        self.step_t.zero_()
+        self.rng_offset.zero_()
+
+    # ------------------------------------------------------------------ target
+    def _target_args(self):
+        cfg = self.cfg
+        if cfg.target == "banana":
+            s1, s2 = cfg.banana_sigma1, cfg.banana_sigma2
+            pairs = cfg.dim // 2
+            cst = -pairs * (math.log(2 * math.pi) + math.log(s1) + math.log(s2))
+            return dict(kind=fused.TARGET_BANANA, params=None, p0=s1, p1=s2, p2=cfg.banana_bend,
+                        cst=cst)
+        if cfg.target == "gaussian":
+            D, s = cfg.dim, cfg.gaussian_scale
+            cst = -0.5 * D * math.log(2 * math.pi) - D * math.log(s)
+            return dict(kind=fused.TARGET_GAUSSIAN, params=self._target_params, cst=cst)
+        raise ValueError(cfg.target)
+
+    def log_normalizer(self) -> float:
+        """log Z of the target (both shipped targets are normalised: 0)."""
+        return 0.0
+
+    # ------------------------------------------------------------------ schedule
+    def _update_schedule(self):
+        """Device-side step/beta update (captured into the graph)."""
+        self.step_t.add_(1.0)
+        self.rng_offset.add_(1)
+        if self.cfg.anneal == "reference":
+            # beta_t = min(1, 0.001 + t / min(max_iter/4, 1e4))   (optimization.py:71-72)
+            cool = min(self.cfg.anneal_iters / 4.0, 1e4)
+            torch.clamp((self.step_t - 1.0) * (1.0 / cool) + 0.001, max=1.0, out=self.beta)
+        else:
+            self.beta.fill_(1.0)
+
+    # ------------------------------------------------------------------ forward
+    def _conditioner_fwd(self, l: int, inp: torch.Tensor) -> torch.Tensor:
+        P = self.params
+        a = inp
+        nh = self.cfg.n_hidden
+        for i in range(nh):
+            out = self.Act[l, i]
+            gemm.linear_fwd(a, P.c(f"l{l}.W{i}"), P.c(f"l{l}.b{i}"), out, relu=True)
+            a = out
+        gemm.linear_fwd(a, P.c(f"l{l}.W{nh}"), P.c(f"l{l}.b{nh}"), self.st, relu=False)
+        return self.st
+
+    def forward(self):
+        cfg, P = self.cfg, self.params
+        L, Dh = cfg.n_layers, cfg.half
+        fused.reparam_sample(self.z0, mu=P.p("base.mu"), logvar=P.p("base.logvar"),
+                             seed=self.seed, offset=self.rng_offset, stream_id=self.rank,
+                             eps=self.eps0, zbf=self.Hbf[0], nbf=Dh, logq0=self.logq0)
+        for l in range(L):
+            st = self._conditioner_fwd(l, self.Hbf[l])
+            ybf = self.Hbf[l + 1] if l + 1 < L else None
+            fused.coupling_fwd(st, self.h(l), self.h(l + 2), ybf=ybf, ssav=self.S[l],
+                               ldj=self.ldj, scale=cfg.scale_bound, inverse=False,
+                               ldj_init=(l == 0))
+        A, Bh, ia, ib = self.zK_halves()
+        ta = self._target_args()
+        fused.target_logp_grad(ta["kind"], A, Bh, gA=self.G[ia], gB=self.G[ib],
+                               grad_accumulate=False, params=ta.get("params"), p0=ta.get("p0", 1.0),
+                               p1=ta.get("p1", 1.0), p2=ta.get("p2", 0.0), cst=ta["cst"],
+                               beta=self.beta, row_weight=1.0 / self.B, logq0=self.logq0,
+                               ldj=self.ldj, logp_out=self.logp, frow_out=self.frow)
+        torch.mean(self.frow, 0, out=self.loss)
+
+    # ------------------------------------------------------------------ backward
+    def backward(self):
+        cfg, P = self.cfg, self.params
+        L, nh = cfg.n_layers, cfg.n_hidden
+        c = -1.0 / self.B
+        for l in range(L - 1, -1, -1):
+            fused.coupling_bwd(self.G[l + 2], self.S[l], self.h(l), self.dst, self.G[l], c=c,
+                               scale=cfg.scale_bound, gx_accumulate=False)
+            d = self.dst
+            for i in range(nh, -1, -1):
+                inp = self.Act[l, i - 1] if i > 0 else self.Hbf[l]
+                gemm.linear_wgrad(d, inp, P.g(f"l{l}.W{i}"), P.g(f"l{l}.b{i}"))
+                if i > 0:
+                    nd = self.dH[i % 2]
+                    gemm.linear_dgrad(d, P.c(f"l{l}.W{i}"), nd, relu_of=self.Act[l, i - 1])
+                    d = nd
+                else:
+                    gemm.linear_dgrad(d, P.c(f"l{l}.W0"), self.G[l + 1], accumulate=True)
+            if self.unit_ready_hook is not None:
+                self.unit_ready_hook(l + 1)
+        self._base_backward()
+        if self.unit_ready_hook is not None:
+            self.unit_ready_hook(0)
+
+    def _base_backward(self):
+        cfg, P = self.cfg, self.params
+        gmu, glv = P.g("base.mu"), P.g("base.logvar")
+        if not cfg.learn_base:
+            gmu.zero_()
+            glv.zero_()
+            return
+        # z0 = [h_1 | h_0]: dL/dz0 = [G1 | G0]
+        g0 = torch.cat([self.G[1], self.G[0]], 1)
+        torch.sum(g0, 0, out=gmu)
+        sig = torch.exp(0.5 * P.p("base.logvar"))
+        torch.sum(g0 * self.eps0, 0, out=glv)
+        glv.mul_(0.5 * sig).sub_(0.5)
+
+    # ------------------------------------------------------------------ optimizer
+    def optimizer_step(self):
+        P = self.params
+        # non-finite guard (+ optional clipping); folds 1/world averaging into gscale
+        fused.sumsq_guard(P.grad, self._partials, out_sumsq=self.gnorm2, skip=self.skip,
+                          scale=self.gscale, max_norm=self.max_grad_norm,
+                          base_scale=self.grad_scale_host)
+        b1, b2 = self.betas
+        fused.flat_optimizer(self.opt_kind, P.master, P.grad, P.m, P.v,
+                             pbf=None if P.compute is P.master else P.compute, lr=self.lr,
+                             b1=b1, b2=b2, eps=self.eps, wd=self.wd, step=self.step_t,
+                             gscale=self.gscale, skip=self.skip)
+        self.n_skipped.add_(self.skip)
+
+    # ------------------------------------------------------------------ step
+    def train_step(self, reduce_fn=None):
+        """One full ELBO step: sample, flow fwd, target, bwd, [grad all-reduce], optimizer."""
+        self._update_schedule()
+        self.forward()
+        self.backward()
+        if reduce_fn is not None:
+            reduce_fn()
+        self.optimizer_step()
+
+    # ------------------------------------------------------------------ inference
+    @torch.no_grad()
+    def sample(self, n: int | None = None, offset: int = 10**9):
+        """Draw z_K ~ q_K with log q_K(z_K); uses the workspace (n <= batch)."""
+        n = n or self.B
+        assert n <= self.B
+        cfg, P = self.cfg, self.params
+        Dh, L = cfg.half, cfg.n_layers
+        fused.reparam_sample(self.z0, mu=P.p("base.mu"), logvar=P.p("base.logvar"),
+                             seed=self.seed + 1, offset_host=offset, stream_id=self.rank,
+                             eps=self.eps0, zbf=self.Hbf[0], nbf=Dh, logq0=self.logq0)
+        for l in range(L):
+            st = self._conditioner_fwd(l, self.Hbf[l])
+            ybf = self.Hbf[l + 1] if l + 1 < L else None
+            fused.coupling_fwd(st, self.h(l), self.h(l + 2), ybf=ybf, ssav=None, ldj=self.ldj,
+                               scale=cfg.scale_bound, ldj_init=(l == 0))
+        A, Bh, _, _ = self.zK_halves()
+        z = torch.cat([A, Bh], 1)[:n].clone()
+        logq = (self.logq0 - self.ldj)[:n].clone()
+        return z, logq
+
+    def state_dict(self) -> dict:
+        return {"params": self.params.state_dict(), "step": self.step_t.detach().cpu(),
+                "rng_offset": self.rng_offset.detach().cpu(), "cfg": self.cfg.__dict__}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.params.load_state_dict(sd["params"])
+        self.step_t.copy_(sd["step"])
+        self.rng_offset.copy_(sd["rng_offset"])

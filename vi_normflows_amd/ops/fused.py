@@ -1,0 +1,98 @@
+"""Device-routed entry points for the fused kernels.
+
+GPU tensors -> ``torch.ops.vinf.*`` (hand-written CDNA4 HIP kernels, required);
+CPU tensors -> the composites in :mod:`vi_normflows_amd.ops.reference`.
+All functions mutate their output arguments and return nothing, so a whole
+training step built from them is allocation-free and hipGraph-capturable.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import reference as ref
+from ._ext import native
+
+TARGET_GAUSSIAN = 0
+TARGET_BANANA = 1
+
+OPT_ADAM = 0
+OPT_RMSPROP = 1
+OPT_SGD_MOMENTUM = 2
+OPT_RMSPROP_MOMENTUM = 3
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def coupling_fwd(st, x, y, ybf=None, ssav=None, ldj=None, scale=1.0, inverse=False,
+                 ldj_init=False):
+    """y = x*exp(s)+t (or inverse), s = scale*tanh(st[:, :Dh]); ldj (+)= sum(s)."""
+    if _gpu(x):
+        native().coupling_fwd(st, x, y, ybf, ssav, ldj, float(scale), bool(inverse),
+                              bool(ldj_init))
+    else:
+        ref.coupling_fwd(st, x, y, ybf, ssav, ldj, float(scale), bool(inverse), bool(ldj_init))
+
+
+def coupling_bwd(gy, s, x, dst, gx, c=0.0, c_row=None, scale=1.0, gx_accumulate=False):
+    if _gpu(x):
+        native().coupling_bwd(gy, s, x, float(c), c_row, dst, gx, float(scale),
+                              bool(gx_accumulate))
+    else:
+        ref.coupling_bwd(gy, s, x, float(c), c_row, dst, gx, float(scale), bool(gx_accumulate))
+
+
+def target_logp_grad(kind, A, Bh, gA=None, gB=None, grad_accumulate=False, params=None, p0=1.0,
+                     p1=1.0, p2=0.0, cst=0.0, beta=None, beta_host=1.0, row_weight=1.0,
+                     logq0=None, ldj=None, logp_out=None, frow_out=None):
+    args = (int(kind), A, Bh, gA, gB, bool(grad_accumulate), params, float(p0), float(p1),
+            float(p2), float(cst), beta, float(beta_host), float(row_weight), logq0, ldj,
+            logp_out, frow_out)
+    if _gpu(A):
+        native().target_logp_grad(*args)
+    else:
+        ref.target_logp_grad(*args)
+
+
+def bernoulli_logits(logits, x, dlogits=None, coef=None, coef_host=1.0, logpx=None):
+    if _gpu(logits):
+        native().bernoulli_logits(logits, x, dlogits, coef, float(coef_host), logpx)
+    else:
+        ref.bernoulli_logits(logits, x, dlogits, coef, float(coef_host), logpx)
+
+
+def reparam_sample(z, mu=None, logvar=None, seed=0, offset=None, offset_host=0, stream_id=0,
+                   eps=None, zbf=None, nbf=0, logq0=None):
+    if _gpu(z):
+        native().reparam_sample(mu, logvar, int(seed), offset, int(offset_host), int(stream_id),
+                                z, eps, zbf, int(nbf), logq0)
+    else:
+        ref.reparam_sample(mu, logvar, int(seed), offset, int(offset_host), int(stream_id), z,
+                           eps, zbf, int(nbf), logq0)
+
+
+def normal_fill(out, seed=0, offset=None, offset_host=0, stream_id=0):
+    if _gpu(out):
+        native().normal_fill(out, int(seed), offset, int(offset_host), int(stream_id))
+    else:
+        g = torch.Generator().manual_seed(int(seed) * 31 + int(offset_host) + 7 * int(stream_id))
+        out.copy_(torch.randn(out.shape, generator=g))
+
+
+def flat_optimizer(kind, p, g, m=None, v=None, pbf=None, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8,
+                   wd=0.0, step=None, step_host=1.0, gscale=None, gscale_host=1.0, skip=None):
+    args = (int(kind), p, g, m, v, pbf, float(lr), float(b1), float(b2), float(eps), float(wd),
+            step, float(step_host), gscale, float(gscale_host), skip)
+    if _gpu(p):
+        native().flat_optimizer(*args)
+    else:
+        ref.flat_optimizer(*args)
+
+
+def sumsq_guard(x, partial, out_sumsq=None, skip=None, scale=None, max_norm=0.0, base_scale=1.0):
+    if _gpu(x):
+        native().sumsq_guard(x, partial, out_sumsq, skip, scale, float(max_norm),
+                             float(base_scale))
+    else:
+        ref.sumsq_guard(x, partial, out_sumsq, skip, scale, float(max_norm), float(base_scale))

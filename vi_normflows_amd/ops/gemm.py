@@ -1,0 +1,90 @@
+"""Dense-layer GEMM entry points used by the explicit-backward engines.
+
+Three GEMM flavours cover an MLP layer ``y = act(x W^T + b)`` (W is [out, in],
+nn.Linear convention):
+
+* ``linear_fwd``   y = act(x W^T + b)                    (fused bias [+ ReLU])
+* ``linear_dgrad`` dx = (dy W) [* 1(h > 0)]              (fused ReLU-mask; fp32 accumulate option)
+* ``linear_wgrad`` dW = dy^T x (fp32), db = colsum(dy)   (fp32 outputs into the flat grad buffer)
+
+Backends (selected per call by :func:`set_backend` / ``VINF_GEMM``):
+``"mfma"`` - the hand-written gfx950 MFMA kernels in ``csrc/kernels/gemm.hip``
+(bf16 in, fp32 accumulate, fused epilogues); ``"blas"`` - hipBLASLt through
+``torch.mm`` for plain library GEMMs (used to A/B the MFMA kernels). CPU tensors
+always use torch in their own dtype.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+_BACKEND = os.environ.get("VINF_GEMM", "blas")
+
+
+def set_backend(name: str) -> None:
+    global _BACKEND
+    if name not in ("mfma", "blas"):
+        raise ValueError(name)
+    _BACKEND = name
+
+
+def backend() -> str:
+    return _BACKEND
+
+
+def _mfma_ok(*ts) -> bool:
+    return _BACKEND == "mfma" and all(t is None or t.is_cuda for t in ts)
+
+
+def linear_fwd(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, out: torch.Tensor,
+               relu: bool = False) -> torch.Tensor:
+    if _mfma_ok(x) and x.is_cuda:
+        from ._ext import native
+
+        native().gemm_nt(x, W, b, out, 1 if relu else 0)
+        return out
+    if b is not None:
+        torch.addmm(b, x, W.t(), out=out)
+    else:
+        torch.mm(x, W.t(), out=out)
+    if relu:
+        out.relu_()
+    return out
+
+
+def linear_dgrad(dy: torch.Tensor, W: torch.Tensor, out: torch.Tensor,
+                 relu_of: torch.Tensor | None = None, accumulate: bool = False) -> torch.Tensor:
+    """out (+)= (dy @ W) * 1(relu_of > 0). ``out`` may be fp32 while dy/W are bf16."""
+    if _mfma_ok(dy) and dy.is_cuda:
+        from ._ext import native
+
+        native().gemm_nn(dy, W, relu_of, out, bool(accumulate))
+        return out
+    if dy.is_cuda and out.dtype != dy.dtype:
+        r = torch.mm(dy, W, out_dtype=out.dtype)
+    else:
+        r = torch.mm(dy, W)
+    if relu_of is not None:
+        r = r * (relu_of > 0)
+    if accumulate:
+        out.add_(r)
+    else:
+        out.copy_(r)
+    return out
+
+
+def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dW: torch.Tensor,
+                 db: torch.Tensor | None) -> None:
+    """dW = dy^T x and db = sum_rows(dy), both written in dW/db's dtype (fp32)."""
+    if _mfma_ok(dy) and dy.is_cuda:
+        from ._ext import native
+
+        native().gemm_tn(dy, x, dW, db)
+        return
+    if dy.is_cuda and dW.dtype != dy.dtype:
+        dW.copy_(torch.mm(dy.t(), x, out_dtype=dW.dtype))
+    else:
+        torch.mm(dy.t(), x, out=dW)
+    if db is not None:
+        torch.sum(dy, 0, dtype=db.dtype, out=db)

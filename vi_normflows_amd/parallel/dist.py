@@ -1,0 +1,102 @@
+"""Process-group setup: one process per GPU, RCCL over xGMI (backend "nccl" on ROCm).
+
+Gloo is used only for CPU tests/plumbing. Rendezvous is env:// (torchrun sets
+RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT); MASTER_ADDR defaults to
+127.0.0.1 because the container hostname may not resolve.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    local_rank: int = 0
+    world: int = 1
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+
+_INFO = DistInfo()
+
+
+def env_world() -> int:
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def init(backend: str | None = None, device_type: str | None = None) -> DistInfo:
+    """Initialise the default process group if WORLD_SIZE > 1 and pick this rank's device."""
+    global _INFO
+    world = env_world()
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if device_type is None:
+        device_type = "cuda" if torch.cuda.is_available() else "cpu"
+    if device_type == "cuda":
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if backend is None:
+        backend = "nccl" if device_type == "cuda" else "gloo"
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+    _INFO = DistInfo(rank=rank, local_rank=local, world=world,
+                     backend=backend if world > 1 else "none", device=device)
+    return _INFO
+
+
+def info() -> DistInfo:
+    return _INFO
+
+
+def barrier() -> None:
+    if dist.is_initialized():
+        if _INFO.backend == "nccl":
+            dist.barrier(device_ids=[_INFO.local_rank])
+        else:
+            dist.barrier()
+
+
+def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.broadcast(t, src)
+    return t
+
+
+def all_reduce_max(x: float, device=None) -> float:
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device or _INFO.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_reduce_mean_(t: torch.Tensor) -> torch.Tensor:
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t)
+        t.div_(dist.get_world_size())
+    return t
+
+
+def shutdown() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()

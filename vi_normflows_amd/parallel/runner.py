@@ -1,0 +1,77 @@
+"""Data-parallel step runner with optional hipGraph capture.
+
+* rank 0's parameters are broadcast at start (same init everywhere);
+* each rank draws rank-distinct Philox noise (engine ``rank`` -> RNG stream id);
+* per-layer gradient slices are all-reduced in buckets during backward
+  (``BucketedAllReduce``), the 1/world average is folded into the optimizer;
+* ``capture()`` records one whole training step (sample, forward, target,
+  backward, collectives, guard, optimizer) into a hipGraph; ``step()`` then
+  replays it, removing all host launch overhead. Schedule state (step, beta,
+  RNG offset) is updated on the device inside the graph.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+from .dist import DistInfo
+from .reducer import BucketedAllReduce
+
+
+class DataParallelRunner:
+    def __init__(self, engine, info: DistInfo, bucket_cap_mb: float = 32.0,
+                 compress_bf16: bool = False):
+        self.engine = engine
+        self.info = info
+        self.graph = None
+        self.reducer = None
+        if info.world > 1:
+            P = engine.params
+            dist.broadcast(P.master, 0)
+            P.sync_compute()
+            engine.grad_scale_host = 1.0 / info.world
+            self.reducer = BucketedAllReduce(P.grad, engine.layout.unit_ranges,
+                                             bucket_cap_mb=bucket_cap_mb,
+                                             compress_bf16=compress_bf16)
+            engine.unit_ready_hook = self.reducer.mark_ready
+
+    def _eager_step(self):
+        if self.reducer is not None:
+            self.reducer.start_step()
+            self.engine.train_step(reduce_fn=self.reducer.finish)
+        else:
+            self.engine.train_step()
+
+    def capture(self, warmup: int = 2) -> bool:
+        """Capture one training step into a hipGraph. Returns False if capture is unsupported."""
+        if self.engine.device.type != "cuda":
+            return False
+        if self.reducer is not None and os.environ.get("VINF_GRAPH_COLLECTIVES", "0") != "1":
+            # collectives inside a captured graph need RCCL graph support; opt-in
+            return False
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._eager_step()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        # the warmup advanced the schedule; keep the step count honest for replay
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g):
+                self._eager_step()
+        except Exception:
+            self.graph = None
+            torch.cuda.synchronize()
+            return False
+        self.graph = g
+        return True
+
+    def step(self):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._eager_step()
