@@ -64,7 +64,7 @@ void coupling_fwd(const at::Tensor& st, const at::Tensor& x, const at::Tensor& y
   long ld_yb = 0, ld_s = 0;
   if (ybf && ybf->defined()) {
     check_2d(*ybf, "ybf");
-    check_dtype(*ybf, at::kBFloat16, "ybf");
+    TORCH_CHECK(ybf->scalar_type() == at::kBFloat16 || ybf->scalar_type() == at::kFloat, "ybf dtype");
     TORCH_CHECK(ybf->size(0) == B && ybf->size(1) >= Dh, "ybf shape");
     ld_yb = ld_of(*ybf);
   }
@@ -78,7 +78,9 @@ void coupling_fwd(const at::Tensor& st, const at::Tensor& x, const at::Tensor& y
   // the kernel pads ybf up to its logical width, not its stride
   nf_launch_coupling_fwd(st.data_ptr(), st.scalar_type() == at::kBFloat16, ld_of(st),
                          x.data_ptr<float>(), ld_of(x), y.data_ptr<float>(), ld_of(y),
-                         opt_ptr<void>(ybf), ld_yb, opt_ptr<float>(ssav), ld_s,
+                         opt_ptr<void>(ybf),
+                         ybf && ybf->defined() && ybf->scalar_type() == at::kBFloat16, ld_yb,
+                         opt_ptr<float>(ssav), ld_s,
                          ldj.data_ptr<float>(), B, Dh, (float)scale, inverse, ldj_init, yb_cols,
                          cur_stream());
 }
@@ -95,7 +97,7 @@ void coupling_bwd(const at::Tensor& gy, const at::Tensor& s, const at::Tensor& x
   check_dtype(s, at::kFloat, "s");
   check_dtype(x, at::kFloat, "x");
   check_dtype(gx, at::kFloat, "gx");
-  check_dtype(dst, at::kBFloat16, "dst");
+  TORCH_CHECK(dst.scalar_type() == at::kBFloat16 || dst.scalar_type() == at::kFloat, "dst dtype");
   const int B = x.size(0), Dh = x.size(1);
   TORCH_CHECK(gy.size(0) == B && gy.size(1) == Dh && s.size(0) == B && s.size(1) == Dh, "shape");
   TORCH_CHECK(gx.size(0) == B && gx.size(1) == Dh, "gx shape");
@@ -106,7 +108,8 @@ void coupling_bwd(const at::Tensor& gy, const at::Tensor& s, const at::Tensor& x
   }
   nf_launch_coupling_bwd(gy.data_ptr<float>(), ld_of(gy), s.data_ptr<float>(), ld_of(s),
                          x.data_ptr<float>(), ld_of(x), (float)c, opt_ptr<float>(c_row),
-                         dst.data_ptr(), ld_of(dst), gx.data_ptr<float>(), ld_of(gx), B, Dh,
+                         dst.data_ptr(), dst.scalar_type() == at::kBFloat16, ld_of(dst),
+                         gx.data_ptr<float>(), ld_of(gx), B, Dh,
                          (float)scale, gx_accumulate, (int)dst.size(1), cur_stream());
 }
 
@@ -125,7 +128,6 @@ void target_logp_grad(int64_t kind, const at::Tensor& A, const at::Tensor& Bh,
   const int B = A.size(0), Dh = A.size(1);
   TORCH_CHECK(Bh.size(0) == B && Bh.size(1) == Dh, "halves must match");
   TORCH_CHECK(kind == 0 || kind == 1, "unknown target kind");
-  TORCH_CHECK(kind != 1 || Dh % 2 == 0, "banana target needs an even half width");
   if (kind == 0) {
     TORCH_CHECK(params && params->defined() && params->numel() == 4 * Dh, "gaussian params [2D]");
   }
@@ -184,7 +186,7 @@ void reparam_sample(const c10::optional<at::Tensor>& mu, const c10::optional<at:
   }
   if (zbf && zbf->defined()) {
     check_2d(*zbf, "zbf");
-    check_dtype(*zbf, at::kBFloat16, "zbf");
+    TORCH_CHECK(zbf->scalar_type() == at::kBFloat16 || zbf->scalar_type() == at::kFloat, "zbf dtype");
     TORCH_CHECK(zbf->size(0) == B && zbf->size(1) >= nbf && nbf <= D, "zbf shape");
     ldzb = ld_of(*zbf);
   }
@@ -197,7 +199,9 @@ void reparam_sample(const c10::optional<at::Tensor>& mu, const c10::optional<at:
   nf_launch_reparam_sample(opt_ptr<float>(mu), opt_ptr<float>(logvar), (uint64_t)seed,
                            opt_ptr<int64_t>(offset), offset_host, (uint32_t)stream_id,
                            z.data_ptr<float>(), ld_of(z), opt_ptr<float>(eps), lde,
-                           opt_ptr<void>(zbf), ldzb, (int)nbf, opt_ptr<float>(logq0), B, D,
+                           opt_ptr<void>(zbf),
+                           zbf && zbf->defined() && zbf->scalar_type() == at::kBFloat16, ldzb,
+                           (int)nbf, opt_ptr<float>(logq0), B, D,
                            cur_stream());
 }
 

@@ -8,13 +8,13 @@ void nf_throw_hip_error(hipError_t e, const char* expr, const char* file, int li
 
 // coupling.hip
 void nf_launch_coupling_fwd(const void* st, int st_is_bf16, long ld_st_, const float* x, long ld_x,
-                            float* y, long ld_y, void* ybf, long ld_yb, float* ssav, long ld_s,
-                            float* ldj, int B, int Dh, float scale, int inverse, int ldj_init,
-                            int yb_width, hipStream_t stream);
+                            float* y, long ld_y, void* ybf, int ybf_is_bf16, long ld_yb,
+                            float* ssav, long ld_s, float* ldj, int B, int Dh, float scale,
+                            int inverse, int ldj_init, int yb_width, hipStream_t stream);
 void nf_launch_coupling_bwd(const float* gy, long ld_gy, const float* s, long ld_s, const float* x,
-                            long ld_x, float c_scalar, const float* c_row, void* dst, long ld_dst,
-                            float* gx, long ld_gx, int B, int Dh, float scale, int gx_accumulate,
-                            int dst_pad_to, hipStream_t stream);
+                            long ld_x, float c_scalar, const float* c_row, void* dst,
+                            int dst_is_bf16, long ld_dst, float* gx, long ld_gx, int B, int Dh,
+                            float scale, int gx_accumulate, int dst_pad_to, hipStream_t stream);
 
 // elbo.hip
 void nf_launch_target_logp_grad(int kind, const float* A, long lda, const float* Bh, long ldb,
@@ -30,8 +30,8 @@ void nf_launch_bernoulli_logits(const void* logits, int is_bf16, long ldl_, cons
 // sampling.hip
 void nf_launch_reparam_sample(const float* mu, const float* logvar, uint64_t seed,
                               const int64_t* offset_ptr, int64_t offset_host, uint32_t stream_id,
-                              float* z, long ldz, float* eps, long lde, void* zbf, long ldzb,
-                              int nbf, float* logq0, int B, int D, hipStream_t stream);
+                              float* z, long ldz, float* eps, long lde, void* zbf, int zbf_is_bf16,
+                              long ldzb, int nbf, float* logq0, int B, int D, hipStream_t stream);
 void nf_launch_normal_fill(float* out, long n, uint64_t seed, const int64_t* offset_ptr,
                            int64_t offset_host, uint32_t stream_id, hipStream_t stream);
 

@@ -37,6 +37,14 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return *reinterpret_cast<bf16_t*>(&h);
 }
 
+// Store a float into a bf16 or fp32 "compute copy" buffer.
+template <typename T>
+__device__ __forceinline__ void st_cv(T* p, float v);
+template <>
+__device__ __forceinline__ void st_cv<float>(float* p, float v) { *p = v; }
+template <>
+__device__ __forceinline__ void st_cv<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

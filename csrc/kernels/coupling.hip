@@ -22,10 +22,10 @@ __device__ __forceinline__ float ld_st<float>(const float* p, long i) { return p
 template <>
 __device__ __forceinline__ float ld_st<bf16_t>(const bf16_t* p, long i) { return bf2f(p[i]); }
 
-template <typename TS, bool INVERSE>
+template <typename TS, bool INVERSE, typename TY>
 __global__ void __launch_bounds__(256) coupling_fwd_kernel(
     const TS* __restrict__ st, long ld_st_, const float* __restrict__ x, long ld_x,
-    float* __restrict__ y, long ld_y, bf16_t* __restrict__ ybf, long ld_yb,
+    float* __restrict__ y, long ld_y, TY* __restrict__ ybf, long ld_yb,
     float* __restrict__ ssav, long ld_s, float* __restrict__ ldj, int B, int Dh, float scale,
     int ldj_init, int yb_width) {
   const int lane = threadIdx.x & 63;
@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(256) coupling_fwd_kernel(
       yv = fmaf(xv, __expf(s), t);
     }
     y_r[j] = yv;
-    if (ybf) ybf[row * ld_yb + j] = f2bf(yv);
+    if (ybf) st_cv<TY>(ybf + row * ld_yb + j, yv);
     if (ssav) ssav[row * ld_s + j] = s;
     acc += s;
   }
@@ -69,10 +69,11 @@ __global__ void __launch_bounds__(256) coupling_fwd_kernel(
 // Outputs:
 //   dst [B, ld_dst] bf16: cols [0,Dh) = dL/ds_hat, cols [Dh,2Dh) = dL/dt, pad cols zeroed
 //   gx  [B, ld_gx]  dL/dx = gy * exp(s)   (gx_accumulate: +=)
+template <typename TD>
 __global__ void __launch_bounds__(256) coupling_bwd_kernel(
     const float* __restrict__ gy, long ld_gy, const float* __restrict__ s, long ld_s,
     const float* __restrict__ x, long ld_x, float c_scalar, const float* __restrict__ c_row,
-    bf16_t* __restrict__ dst, long ld_dst, float* __restrict__ gx, long ld_gx, int B, int Dh,
+    TD* __restrict__ dst, long ld_dst, float* __restrict__ gx, long ld_gx, int B, int Dh,
     float scale, int gx_accumulate, int dst_pad_to) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -86,55 +87,70 @@ __global__ void __launch_bounds__(256) coupling_bwd_kernel(
     const float xv = x[row * ld_x + j];
     const float ds = fmaf(g * xv, es, c);            // dL/ds
     const float dsh = ds * (scale - sv * sv * inv_scale);  // ds/dshat = scale*(1 - tanh^2)
-    dst[row * ld_dst + j] = f2bf(dsh);
-    dst[row * ld_dst + Dh + j] = f2bf(g);
+    st_cv<TD>(dst + row * ld_dst + j, dsh);
+    st_cv<TD>(dst + row * ld_dst + Dh + j, g);
     const float gxv = g * es;
     float* gp = gx + row * ld_gx + j;
     *gp = gx_accumulate ? (*gp + gxv) : gxv;
   }
-  for (int j = 2 * Dh + lane; j < dst_pad_to; j += 64) dst[row * ld_dst + j] = 0;
+  for (int j = 2 * Dh + lane; j < dst_pad_to; j += 64) st_cv<TD>(dst + row * ld_dst + j, 0.f);
 }
 
 }  // namespace nf
 
 using namespace nf;
 
-void nf_launch_coupling_fwd(const void* st, int st_is_bf16, long ld_st_, const float* x, long ld_x,
-                            float* y, long ld_y, void* ybf, long ld_yb, float* ssav, long ld_s,
-                            float* ldj, int B, int Dh, float scale, int inverse, int ldj_init,
-                            int yb_width, hipStream_t stream) {
-  if (B <= 0) return;
+template <typename TS, bool INV>
+static void launch_cf(const void* st, long ld_st_, const float* x, long ld_x, float* y, long ld_y,
+                      void* ybf, int ybf_is_bf16, long ld_yb, float* ssav, long ld_s, float* ldj,
+                      int B, int Dh, float scale, int ldj_init, int yb_width, hipStream_t stream) {
   dim3 grid((B + 3) / 4), block(256);
+  if (ybf_is_bf16)
+    hipLaunchKernelGGL((coupling_fwd_kernel<TS, INV, bf16_t>), grid, block, 0, stream,
+                       (const TS*)st, ld_st_, x, ld_x, y, ld_y, (bf16_t*)ybf, ld_yb, ssav, ld_s,
+                       ldj, B, Dh, scale, ldj_init, yb_width);
+  else
+    hipLaunchKernelGGL((coupling_fwd_kernel<TS, INV, float>), grid, block, 0, stream,
+                       (const TS*)st, ld_st_, x, ld_x, y, ld_y, (float*)ybf, ld_yb, ssav, ld_s,
+                       ldj, B, Dh, scale, ldj_init, yb_width);
+}
+
+void nf_launch_coupling_fwd(const void* st, int st_is_bf16, long ld_st_, const float* x, long ld_x,
+                            float* y, long ld_y, void* ybf, int ybf_is_bf16, long ld_yb,
+                            float* ssav, long ld_s, float* ldj, int B, int Dh, float scale,
+                            int inverse, int ldj_init, int yb_width, hipStream_t stream) {
+  if (B <= 0) return;
   if (st_is_bf16) {
     if (inverse)
-      hipLaunchKernelGGL((coupling_fwd_kernel<bf16_t, true>), grid, block, 0, stream,
-                         (const bf16_t*)st, ld_st_, x, ld_x, y, ld_y, (bf16_t*)ybf, ld_yb, ssav,
-                         ld_s, ldj, B, Dh, scale, ldj_init, yb_width);
+      launch_cf<bf16_t, true>(st, ld_st_, x, ld_x, y, ld_y, ybf, ybf_is_bf16, ld_yb, ssav, ld_s,
+                              ldj, B, Dh, scale, ldj_init, yb_width, stream);
     else
-      hipLaunchKernelGGL((coupling_fwd_kernel<bf16_t, false>), grid, block, 0, stream,
-                         (const bf16_t*)st, ld_st_, x, ld_x, y, ld_y, (bf16_t*)ybf, ld_yb, ssav,
-                         ld_s, ldj, B, Dh, scale, ldj_init, yb_width);
+      launch_cf<bf16_t, false>(st, ld_st_, x, ld_x, y, ld_y, ybf, ybf_is_bf16, ld_yb, ssav, ld_s,
+                               ldj, B, Dh, scale, ldj_init, yb_width, stream);
   } else {
     if (inverse)
-      hipLaunchKernelGGL((coupling_fwd_kernel<float, true>), grid, block, 0, stream,
-                         (const float*)st, ld_st_, x, ld_x, y, ld_y, (bf16_t*)ybf, ld_yb, ssav,
-                         ld_s, ldj, B, Dh, scale, ldj_init, yb_width);
+      launch_cf<float, true>(st, ld_st_, x, ld_x, y, ld_y, ybf, ybf_is_bf16, ld_yb, ssav, ld_s,
+                             ldj, B, Dh, scale, ldj_init, yb_width, stream);
     else
-      hipLaunchKernelGGL((coupling_fwd_kernel<float, false>), grid, block, 0, stream,
-                         (const float*)st, ld_st_, x, ld_x, y, ld_y, (bf16_t*)ybf, ld_yb, ssav,
-                         ld_s, ldj, B, Dh, scale, ldj_init, yb_width);
+      launch_cf<float, false>(st, ld_st_, x, ld_x, y, ld_y, ybf, ybf_is_bf16, ld_yb, ssav, ld_s,
+                              ldj, B, Dh, scale, ldj_init, yb_width, stream);
   }
   NF_HIP_CHECK(hipGetLastError());
 }
 
 void nf_launch_coupling_bwd(const float* gy, long ld_gy, const float* s, long ld_s, const float* x,
-                            long ld_x, float c_scalar, const float* c_row, void* dst, long ld_dst,
-                            float* gx, long ld_gx, int B, int Dh, float scale, int gx_accumulate,
-                            int dst_pad_to, hipStream_t stream) {
+                            long ld_x, float c_scalar, const float* c_row, void* dst,
+                            int dst_is_bf16, long ld_dst, float* gx, long ld_gx, int B, int Dh,
+                            float scale, int gx_accumulate, int dst_pad_to, hipStream_t stream) {
   if (B <= 0) return;
   dim3 grid((B + 3) / 4), block(256);
-  hipLaunchKernelGGL(coupling_bwd_kernel, grid, block, 0, stream, gy, ld_gy, s, ld_s, x, ld_x,
-                     c_scalar, c_row, (bf16_t*)dst, ld_dst, gx, ld_gx, B, Dh, scale,
-                     gx_accumulate, dst_pad_to);
+  if (dst_is_bf16)
+    hipLaunchKernelGGL(coupling_bwd_kernel<bf16_t>, grid, block, 0, stream, gy, ld_gy, s, ld_s, x,
+                       ld_x, c_scalar, c_row, (bf16_t*)dst, ld_dst, gx, ld_gx, B, Dh, scale,
+                       gx_accumulate, dst_pad_to);
+  else
+    hipLaunchKernelGGL(coupling_bwd_kernel<float>, grid, block, 0, stream, gy, ld_gy, s, ld_s, x,
+                       ld_x, c_scalar, c_row, (float*)dst, ld_dst, gx, ld_gx, B, Dh, scale,
+                       gx_accumulate, dst_pad_to);
   NF_HIP_CHECK(hipGetLastError());
 }

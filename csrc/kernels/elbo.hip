@@ -54,7 +54,7 @@ __global__ void __launch_bounds__(256) target_logp_grad_kernel(
     const float s1 = p0, s2 = p1, bend = p2;
     const float is1 = 1.f / (s1 * s1), is2 = 1.f / (s2 * s2);
     for (int i = lane; i < Dh; i += 64) {
-      // pair (2i, 2i+1) lives entirely in one half because Dh is even
+      // pair (2i, 2i+1); straddles the two halves only when Dh is odd
       const int j = 2 * i;
       const float x = zval(A, lda, Bh, ldb, row, j, Dh);
       const float y = zval(A, lda, Bh, ldb, row, j + 1, Dh);
@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(256) target_logp_grad_kernel(
         const float dy = -r * is2;
         const float dx = -x * is1 + r * is2 * 2.f * bend * x;
         float* gp0 = j < Dh ? (gA + row * ldga + j) : (gB + row * ldgb + (j - Dh));
-        float* gp1 = gp0 + 1;
+        float* gp1 = (j + 1) < Dh ? (gA + row * ldga + j + 1) : (gB + row * ldgb + (j + 1 - Dh));
         const float g0 = coef * dx, g1 = coef * dy;
         if (grad_accumulate) {
           *gp0 += g0;

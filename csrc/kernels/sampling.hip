@@ -10,10 +10,11 @@
 
 namespace nf {
 
+template <typename TZ>
 __global__ void __launch_bounds__(256) reparam_sample_kernel(
     const float* __restrict__ mu, const float* __restrict__ logvar, uint32_t seed_lo,
     uint32_t seed_hi, const int64_t* __restrict__ offset_ptr, int64_t offset_host, uint32_t stream,
-    float* __restrict__ z, long ldz, float* __restrict__ eps_out, long lde, bf16_t* __restrict__ zbf,
+    float* __restrict__ z, long ldz, float* __restrict__ eps_out, long lde, TZ* __restrict__ zbf,
     long ldzb, int nbf, float* __restrict__ logq0, int B, int D) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -37,14 +38,14 @@ __global__ void __launch_bounds__(256) reparam_sample_kernel(
         const float zv = fmaf(__expf(0.5f * lv), e, m);
         z[row * ldz + j] = zv;
         if (eps_out) eps_out[row * lde + j] = e;
-        if (zbf && j < nbf) zbf[row * ldzb + j] = f2bf(zv);
+        if (zbf && j < nbf) st_cv<TZ>(zbf + row * ldzb + j, zv);
         sq += e * e;
         slv += lv;
       }
     }
   }
   if (zbf) {
-    for (int j = nbf + lane; j < ldzb; j += 64) zbf[row * ldzb + j] = 0;
+    for (int j = nbf + lane; j < ldzb; j += 64) st_cv<TZ>(zbf + row * ldzb + j, 0.f);
   }
   sq = wave_sum(sq);
   slv = wave_sum(slv);
@@ -81,14 +82,20 @@ using namespace nf;
 
 void nf_launch_reparam_sample(const float* mu, const float* logvar, uint64_t seed,
                               const int64_t* offset_ptr, int64_t offset_host, uint32_t stream_id,
-                              float* z, long ldz, float* eps, long lde, void* zbf, long ldzb,
-                              int nbf, float* logq0, int B, int D, hipStream_t stream) {
+                              float* z, long ldz, float* eps, long lde, void* zbf, int zbf_is_bf16,
+                              long ldzb, int nbf, float* logq0, int B, int D, hipStream_t stream) {
   if (B <= 0) return;
   dim3 grid((B + 3) / 4), block(256);
-  hipLaunchKernelGGL(reparam_sample_kernel, grid, block, 0, stream, mu, logvar,
-                     (uint32_t)(seed & 0xffffffffu), (uint32_t)(seed >> 32), offset_ptr,
-                     offset_host, stream_id, z, ldz, eps, lde, (bf16_t*)zbf, ldzb, nbf, logq0, B,
-                     D);
+  if (zbf_is_bf16 || zbf == nullptr)
+    hipLaunchKernelGGL(reparam_sample_kernel<bf16_t>, grid, block, 0, stream, mu, logvar,
+                       (uint32_t)(seed & 0xffffffffu), (uint32_t)(seed >> 32), offset_ptr,
+                       offset_host, stream_id, z, ldz, eps, lde, (bf16_t*)zbf, ldzb, nbf, logq0, B,
+                       D);
+  else
+    hipLaunchKernelGGL(reparam_sample_kernel<float>, grid, block, 0, stream, mu, logvar,
+                       (uint32_t)(seed & 0xffffffffu), (uint32_t)(seed >> 32), offset_ptr,
+                       offset_host, stream_id, z, ldz, eps, lde, (float*)zbf, ldzb, nbf, logq0, B,
+                       D);
   NF_HIP_CHECK(hipGetLastError());
 }
 

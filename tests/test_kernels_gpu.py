@@ -136,9 +136,10 @@ def test_flat_optimizer(gpu, kind, n):
     torch.manual_seed(4)
     p0 = torch.randn(n, device=gpu)
     g = torch.randn(n, device=gpu)
+    m0, v0 = torch.rand(n, device=gpu) * 0.1, torch.rand(n, device=gpu) * 0.1
     res = []
     for impl in ("native", "ref"):
-        p, m, v = p0.clone(), torch.rand(n, device=gpu) * 0.1, torch.rand(n, device=gpu) * 0.1
+        p, m, v = p0.clone(), m0.clone(), v0.clone()
         pbf = torch.empty(n, device=gpu, dtype=torch.bfloat16)
         step = torch.tensor(3.0, device=gpu)
         gs = torch.tensor(0.5, device=gpu)

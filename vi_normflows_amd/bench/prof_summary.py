@@ -1,0 +1,67 @@
+"""Summarise a rocprofv3 kernel trace (SQLite ``*_results.db`` or ``kernel_stats.csv``).
+
+    python -m vi_normflows_amd.bench.prof_summary gpurun_out/prof1 [--steps N] [--top 30]
+
+Prints per-kernel total / per-call time, share of the total and (with --steps)
+time per training step; the text goes into ``profiles/`` for the record.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import os
+import sqlite3
+from collections import defaultdict
+
+
+def _from_db(path):
+    con = sqlite3.connect(path)
+    rows = con.execute("select name, count(*), sum(end-start) from kernels group by name").fetchall()
+    return [(n, c, t / 1e3) for n, c, t in rows]  # us
+
+
+def _from_csv(path):
+    acc = defaultdict(lambda: [0, 0.0])
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            name = r.get("Kernel_Name") or r.get("KernelName") or r.get("Name")
+            if "TotalDurationNs" in r:
+                acc[name][0] += int(r.get("Calls", 1))
+                acc[name][1] += float(r["TotalDurationNs"]) / 1e3
+            else:
+                acc[name][0] += 1
+                acc[name][1] += (float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) / 1e3
+    return [(n, c, t) for n, (c, t) in acc.items()]
+
+
+def summarize(root: str, steps: int | None = None, top: int = 30) -> str:
+    dbs = glob.glob(os.path.join(root, "**", "*.db"), recursive=True)
+    csvs = glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), recursive=True) or \
+        glob.glob(os.path.join(root, "**", "*kernel_trace.csv"), recursive=True)
+    rows = _from_db(dbs[0]) if dbs else _from_csv(csvs[0])
+    rows.sort(key=lambda r: -r[2])
+    total = sum(r[2] for r in rows)
+    out = [f"total kernel time {total / 1e3:.2f} ms" +
+           (f" over {steps} steps = {total / 1e3 / steps:.3f} ms/step" if steps else "")]
+    out.append(f"{'ms':>9} {'share':>6} {'calls':>6} {'us/call':>9}" +
+               (f" {'ms/step':>8}" if steps else "") + "  kernel")
+    for n, c, t in rows[:top]:
+        line = f"{t / 1e3:9.2f} {100 * t / total:5.1f}% {c:6d} {t / c:9.1f}"
+        if steps:
+            line += f" {t / 1e3 / steps:8.3f}"
+        out.append(line + "  " + n[:120])
+    return "\n".join(out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--top", type=int, default=30)
+    a = ap.parse_args()
+    print(summarize(a.root, a.steps, a.top))
+
+
+if __name__ == "__main__":
+    main()
