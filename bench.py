@@ -47,7 +47,7 @@ def main() -> None:
     ap.add_argument("--dim", type=int, default=784)
     ap.add_argument("--hidden", type=int, default=1024)
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto")
-    ap.add_argument("--gemm", choices=["mfma", "blas"], default=os.environ.get("VINF_GEMM", "blas"))
+    ap.add_argument("--gemm", choices=["mfma", "blas"], default=os.environ.get("VINF_GEMM", "mfma"))
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--cpu", action="store_true", help="plumbing run on CPU (tiny sizes)")
     ap.add_argument("--verbose", action="store_true")

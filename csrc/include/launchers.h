@@ -43,3 +43,13 @@ void nf_launch_flat_optimizer(int kind, float* p, const float* g, float* m, floa
 void nf_launch_sumsq_guard(const float* x, long n, float* partial, int npartial, float* out_sumsq,
                            float* out_skip, float* out_scale, float max_norm, float base_scale,
                            hipStream_t stream);
+
+// gemm.hip (bf16 MFMA, fp32 accumulate)
+void nf_launch_gemm_nt(const void* x, long ldx, const void* W, long ldw, const void* bias, void* y,
+                       long ldy, int M, int N, int K, int relu, hipStream_t stream);
+void nf_launch_gemm_nn(const void* dy, long lddy, const void* W, long ldw, const void* aux,
+                       long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
+                       int N, int K, hipStream_t stream);
+void nf_launch_gemm_tn(const void* dy, long lddy, const void* x, long ldx, float* dW, long lddw,
+                       float* db, int M, int N, int K, int splits, float* work,
+                       hipStream_t stream);

@@ -19,8 +19,13 @@ def autograd_free_energy(eng: RealNVPVI, params: dict, eps: torch.Tensor, beta: 
     for l in range(L):
         a = h[l + 1]
         for i in range(nh):
-            a = torch.relu(a @ params[f"l{l}.W{i}"].t() + params[f"l{l}.b{i}"])
-        st = a @ params[f"l{l}.W{nh}"].t() + params[f"l{l}.b{nh}"]
+            W = params[f"l{l}.W{i}"]
+            W = W[:, :Dh] if i == 0 else W
+            a = torch.relu(a @ W.t() + params[f"l{l}.b{i}"])
+        Wo = params[f"l{l}.W{nh}"][:2 * Dh]
+        if nh == 0:
+            Wo = Wo[:, :Dh]
+        st = a @ Wo.t() + params[f"l{l}.b{nh}"][:2 * Dh]
         s = cfg.scale_bound * torch.tanh(st[:, :Dh])
         t = st[:, Dh:]
         h.append(h[l] * torch.exp(s) + t)
@@ -34,10 +39,10 @@ def autograd_free_energy(eng: RealNVPVI, params: dict, eps: torch.Tensor, beta: 
 
 
 @pytest.mark.parametrize("target", ["banana", "gaussian"])
-@pytest.mark.parametrize("layers,n_hidden", [(3, 2), (4, 1)])
-def test_engine_grads_match_autograd(target, layers, n_hidden):
+@pytest.mark.parametrize("layers,n_hidden,k_align", [(3, 2, 1), (4, 1, 1), (3, 2, 8)])
+def test_engine_grads_match_autograd(target, layers, n_hidden, k_align):
     cfg = RealNVPConfig(dim=6, n_layers=layers, hidden=8, n_hidden=n_hidden, target=target,
-                        anneal="none", scale_bound=1.5, init_out_std=0.3)
+                        anneal="none", scale_bound=1.5, init_out_std=0.3, k_align=k_align)
     eng = RealNVPVI(cfg, batch=5, device="cpu", seed=3)
     eng._update_schedule()
     eng.forward()

@@ -1,0 +1,90 @@
+"""Micro-benchmark: MFMA GEMM family vs hipBLASLt (torch.mm) on the RealNVP layer shapes.
+
+    python -m vi_normflows_amd.bench.gemm_bench [--batch 16384] [--iters 50]
+
+Interleaves the two implementations per shape in one process (guide §5.4 rule 24),
+random bf16 operands (rule 25), and prints one JSON line per shape with TFLOP/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+
+import torch
+
+from vi_normflows_amd.ops._ext import native
+
+
+def _time(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=16384)
+    ap.add_argument("--iters", type=int, default=50)
+    a = ap.parse_args()
+    ops = native()
+    dev = torch.device("cuda")
+    B = a.batch
+    bf = torch.bfloat16
+    shapes = [("fwd_l1", "nt", B, 1024, 416), ("fwd_l2", "nt", B, 1024, 1024),
+              ("fwd_l3", "nt", B, 800, 1024),
+              ("dgrad_l3", "nn_mask", B, 1024, 800), ("dgrad_l2", "nn_mask", B, 1024, 1024),
+              ("dgrad_l1", "nn_f32acc", B, 416, 1024),
+              ("wgrad_l3", "tn", 800, 1024, B), ("wgrad_l2", "tn", 1024, 1024, B),
+              ("wgrad_l1", "tn", 1024, 416, B)]
+    for name, kind, M, N, K in shapes:
+        torch.manual_seed(0)
+        if kind == "nt":
+            x = torch.randn(M, K, device=dev).to(bf)
+            W = (torch.randn(N, K, device=dev) * 0.05).to(bf)
+            b = torch.randn(N, device=dev).to(bf)
+            y = torch.empty(M, N, device=dev, dtype=bf)
+            mine = lambda: ops.gemm_nt(x, W, b, y, 1)
+            ref = lambda: torch.relu_(torch.addmm(b, x, W.t(), out=y))
+        elif kind.startswith("nn"):
+            dy = torch.randn(M, K, device=dev).to(bf)
+            W = (torch.randn(K, N, device=dev) * 0.05).to(bf)
+            if kind == "nn_mask":
+                h = torch.randn(M, N, device=dev).to(bf)
+                y = torch.empty(M, N, device=dev, dtype=bf)
+                mine = lambda: ops.gemm_nn(dy, W, h, y, False)
+                ref = lambda: y.copy_(torch.mm(dy, W) * (h > 0))
+            else:
+                y = torch.zeros(M, N, device=dev)
+                mine = lambda: ops.gemm_nn(dy, W, None, y, True)
+                ref = lambda: y.add_(torch.mm(dy, W, out_dtype=torch.float32))
+        else:
+            dy = torch.randn(K, M, device=dev).to(bf)
+            x = torch.randn(K, N, device=dev).to(bf)
+            dW = torch.empty(M, N, device=dev)
+            db = torch.empty(M, device=dev)
+            mine = lambda: ops.gemm_tn(dy, x, dW, db)
+
+            def ref():
+                dW.copy_(torch.mm(dy.t(), x, out_dtype=torch.float32))
+                torch.sum(dy, 0, dtype=torch.float32, out=db)
+        flops = 2.0 * M * N * K
+        tm, tr = [], []
+        for _ in range(3):
+            tm.append(_time(mine, a.iters))
+            tr.append(_time(ref, a.iters))
+        t_m, t_r = min(tm), min(tr)
+        print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "mfma_us": round(t_m * 1e6, 1),
+                          "blas_us": round(t_r * 1e6, 1),
+                          "mfma_tflops": round(flops / t_m / 1e12, 1),
+                          "blas_tflops": round(flops / t_r / 1e12, 1),
+                          "speedup": round(t_r / t_m, 2)}))
+
+
+if __name__ == "__main__":
+    main()

@@ -55,6 +55,7 @@ class RealNVPConfig:
     init_out_std: float = 1e-3     # small *random* output init (not zeros: see bench notes)
     anneal: str = "reference"      # "reference" | "none" (beta_t schedule)
     anneal_iters: int = 10000      # max_iter for the reference schedule
+    k_align: int = 32              # pad GEMM K/N dims (392 -> 416, 784 -> 800) for MFMA tiles
     extra: dict = field(default_factory=dict)
 
     @property
@@ -62,21 +63,32 @@ class RealNVPConfig:
         assert self.dim % 2 == 0, "RealNVP needs an even dimension"
         return self.dim // 2
 
+    @property
+    def half_pad(self) -> int:
+        a = max(1, self.k_align)
+        return (self.half + a - 1) // a * a
+
+    @property
+    def out_pad(self) -> int:
+        a = max(1, self.k_align)
+        return (2 * self.half + a - 1) // a * a
+
     def n_params(self) -> int:
         Dh, H = self.half, self.hidden
         per = Dh * H + H + (self.n_hidden - 1) * (H * H + H) + H * 2 * Dh + 2 * Dh
         return self.n_layers * per + 2 * self.dim
 
     def flops_per_sample(self) -> float:
-        """Forward+backward GEMM FLOPs per sample (dgrad of the first layer included)."""
+        """Forward+backward GEMM FLOPs per sample of the *unpadded* model (useful work)."""
         Dh, H = self.half, self.hidden
         macs = Dh * H + (self.n_hidden - 1) * H * H + H * 2 * Dh
         return 6.0 * macs * self.n_layers
 
 
 def _layer_shapes(cfg: RealNVPConfig):
-    Dh, H = cfg.half, cfg.hidden
-    dims = [Dh] + [H] * cfg.n_hidden + [2 * Dh]
+    """(out, in) of each conditioner linear, padded: in0 = half_pad, out_last = out_pad."""
+    H = cfg.hidden
+    dims = [cfg.half_pad] + [H] * cfg.n_hidden + [cfg.out_pad]
     return [(dims[i + 1], dims[i]) for i in range(len(dims) - 1)]
 
 
@@ -135,13 +147,15 @@ class RealNVPVI:
         self.z0 = torch.empty(B, D, dtype=f32, device=dev)
         self.eps0 = torch.empty(B, D, dtype=f32, device=dev)
         self.Hs = torch.empty(L, B, Dh, dtype=f32, device=dev)          # h_2 .. h_{L+1}
-        self.Hbf = torch.empty(L, B, Dh, dtype=self.cdt, device=dev)    # bf16(h_1 .. h_L)
+        Dp, Np = cfg.half_pad, cfg.out_pad
+        self.Hbf = torch.empty(L, B, Dp, dtype=self.cdt, device=dev)    # bf16(h_1 .. h_L), 0-padded
         self.Act = torch.empty(L, cfg.n_hidden, B, H, dtype=self.cdt, device=dev)
         self.S = torch.empty(L, B, Dh, dtype=f32, device=dev)
-        self.st = torch.empty(B, 2 * Dh, dtype=self.cdt, device=dev)
-        self.dst = torch.empty(B, 2 * Dh, dtype=self.cdt, device=dev)
+        self.st = torch.empty(B, Np, dtype=self.cdt, device=dev)
+        self.dst = torch.empty(B, Np, dtype=self.cdt, device=dev)
         self.dH = [torch.empty(B, H, dtype=self.cdt, device=dev) for _ in range(2)]
-        self.G = torch.empty(L + 2, B, Dh, dtype=f32, device=dev)
+        self._G = torch.zeros(L + 2, B, Dp, dtype=f32, device=dev)   # dL/dh_i, 0-padded rows
+        self.G = self._G[:, :, :Dh]
         self.logq0 = torch.empty(B, dtype=f32, device=dev)
         self.ldj = torch.empty(B, dtype=f32, device=dev)
         self.logp = torch.empty(B, dtype=f32, device=dev)
@@ -171,12 +185,20 @@ class RealNVPVI:
         g = torch.Generator(device="cpu").manual_seed(int(seed))
         P = self.params
         n_lin = len(self.shapes)
+        Dh, No = self.cfg.half, 2 * self.cfg.half
         for l in range(self.cfg.n_layers):
             for i, (o, inp) in enumerate(self.shapes):
-                std = math.sqrt(2.0 / inp) if i < n_lin - 1 else self.cfg.init_out_std
-                P.p(f"l{l}.W{i}").copy_(torch.randn(o, inp, generator=g) * std)
-                P.p(f"l{l}.b{i}").copy_(torch.randn(o, generator=g) * (0.01 if i < n_lin - 1 else
-                                                                       self.cfg.init_out_std))
+                fan_in = Dh if i == 0 else inp
+                std = math.sqrt(2.0 / fan_in) if i < n_lin - 1 else self.cfg.init_out_std
+                W = torch.randn(o, inp, generator=g) * std
+                b = torch.randn(o, generator=g) * (0.01 if i < n_lin - 1 else self.cfg.init_out_std)
+                if i == 0:
+                    W[:, Dh:] = 0.0          # padded input columns
+                if i == n_lin - 1:
+                    W[No:, :] = 0.0          # padded output rows
+                    b[No:] = 0.0
+                P.p(f"l{l}.W{i}").copy_(W)
+                P.p(f"l{l}.b{i}").copy_(b)
         P.p("base.mu").zero_()
         P.p("base.logvar").zero_()
         P.sync_compute()
@@ -266,7 +288,7 @@ class RealNVPVI:
                     gemm.linear_dgrad(d, P.c(f"l{l}.W{i}"), nd, relu_of=self.Act[l, i - 1])
                     d = nd
                 else:
-                    gemm.linear_dgrad(d, P.c(f"l{l}.W0"), self.G[l + 1], accumulate=True)
+                    gemm.linear_dgrad(d, P.c(f"l{l}.W0"), self._G[l + 1], accumulate=True)
             if self.unit_ready_hook is not None:
                 self.unit_ready_hook(l + 1)
         self._base_backward()

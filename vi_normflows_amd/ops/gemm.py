@@ -19,7 +19,7 @@ import os
 
 import torch
 
-_BACKEND = os.environ.get("VINF_GEMM", "blas")
+_BACKEND = os.environ.get("VINF_GEMM", "mfma")
 
 
 def set_backend(name: str) -> None:
