@@ -53,3 +53,18 @@ void nf_launch_gemm_nn(const void* dy, long lddy, const void* W, long ldw, const
 void nf_launch_gemm_tn(const void* dy, long lddy, const void* x, long ldx, float* dW, long lddw,
                        float* db, int M, int N, int K, int splits, float* work,
                        hipStream_t stream);
+
+// planar.hip / radial.hip (fused K-layer stacks; per-row parameter gradients)
+void nf_launch_planar_fwd(const float* z, const float* W, const float* U, const float* B, float* zK,
+                          float* ldj, float* saved, int N, int D, int K, int per_sample,
+                          int broadcast, hipStream_t stream);
+void nf_launch_planar_bwd(const float* saved, const float* W, const float* U, const float* B,
+                          const float* gz, const float* gl, float* dz, float* dW, float* dU,
+                          float* dB, int N, int D, int K, int per_sample, int broadcast,
+                          hipStream_t stream);
+void nf_launch_radial_fwd(const float* z, const float* Z0, const float* AL, const float* BE,
+                          float* zK, float* ldj, float* saved, int N, int D, int K,
+                          int per_sample, hipStream_t stream);
+void nf_launch_radial_bwd(const float* saved, const float* Z0, const float* AL, const float* BE,
+                          const float* gz, const float* gl, float* dz, float* dZ0, float* dA,
+                          float* dBe, int N, int D, int K, int per_sample, hipStream_t stream);
