@@ -59,3 +59,32 @@ def load_reference(root):
 def ref_module(root, name):
     load_reference(root)
     return importlib.import_module(f"ref_normflows.{name}")
+
+
+def load_defs(path, names=None):
+    """Execute only the top-level function/lambda/import definitions of a reference *script*
+    (e.g. get_data.py parses sys.argv at import time, so it cannot be imported)."""
+    import ast
+
+    _install_autograd_shim()
+    src = open(path).read()
+    tree = ast.parse(src)
+    keep = []
+    for node in tree.body:
+        if isinstance(node, (ast.FunctionDef, ast.Import, ast.ImportFrom)):
+            keep.append(node)
+        elif isinstance(node, ast.Assign) and isinstance(node.value, ast.Lambda):
+            keep.append(node)
+    mod = ast.Module(body=[n for n in keep if not (isinstance(n, (ast.Import, ast.ImportFrom))
+                                                 and any(a.name.startswith(("pandas", "statsmodels",
+                                                                            "normflows", "tqdm",
+                                                                            "matplotlib"))
+                                                         for a in n.names if hasattr(a, "name"))
+                                                 or (isinstance(n, ast.ImportFrom) and
+                                                     (n.module or "").startswith(
+                                                         ("normflows", "matplotlib", "tqdm",
+                                                          "statsmodels", "pandas"))))],
+                     type_ignores=[])
+    ns: dict = {}
+    exec(compile(mod, path, "exec"), ns)
+    return ns if names is None else {k: ns[k] for k in names}
