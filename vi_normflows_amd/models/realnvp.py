@@ -111,6 +111,7 @@ class RealNVPVI:
         self.max_grad_norm = float(max_grad_norm)
         self.grad_scale_host = 1.0
         self.unit_ready_hook = None   # callable(unit_idx) after a unit's grads are final
+        self.eps_override = None      # fixed base noise [B, D] (tests); None -> Philox sampler
 
         L = cfg.n_layers
         layout = FlatLayout()
@@ -253,9 +254,12 @@ class RealNVPVI:
     def forward(self):
         cfg, P = self.cfg, self.params
         L, Dh = cfg.n_layers, cfg.half
-        fused.reparam_sample(self.z0, mu=P.p("base.mu"), logvar=P.p("base.logvar"),
-                             seed=self.seed, offset=self.rng_offset, stream_id=self.rank,
-                             eps=self.eps0, zbf=self.Hbf[0], nbf=Dh, logq0=self.logq0)
+        if self.eps_override is None:
+            fused.reparam_sample(self.z0, mu=P.p("base.mu"), logvar=P.p("base.logvar"),
+                                 seed=self.seed, offset=self.rng_offset, stream_id=self.rank,
+                                 eps=self.eps0, zbf=self.Hbf[0], nbf=Dh, logq0=self.logq0)
+        else:
+            self._base_from_eps(self.eps_override)
         for l in range(L):
             st = self._conditioner_fwd(l, self.Hbf[l])
             ybf = self.Hbf[l + 1] if l + 1 < L else None
@@ -270,6 +274,17 @@ class RealNVPVI:
                                beta=self.beta, row_weight=1.0 / self.B, logq0=self.logq0,
                                ldj=self.ldj, logp_out=self.logp, frow_out=self.frow)
         torch.mean(self.frow, 0, out=self.loss)
+
+    def _base_from_eps(self, eps: torch.Tensor):
+        """Deterministic base sample from given noise (tests / replaying a noise stream)."""
+        P, cfg = self.params, self.cfg
+        lv = P.p("base.logvar")
+        self.eps0.copy_(eps)
+        self.z0.copy_(P.p("base.mu") + torch.exp(0.5 * lv) * eps)
+        self.Hbf[0][:, :cfg.half].copy_(self.z0[:, :cfg.half].to(self.cdt))
+        self.Hbf[0][:, cfg.half:].zero_()
+        self.logq0.copy_(-0.5 * cfg.dim * math.log(2 * math.pi) - 0.5 * lv.sum()
+                         - 0.5 * (eps * eps).sum(1))
 
     # ------------------------------------------------------------------ backward
     def backward(self):
