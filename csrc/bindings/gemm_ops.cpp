@@ -82,27 +82,12 @@ void gemm_tn(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dW,
     TORCH_CHECK(db->scalar_type() == at::kFloat && db->numel() == M && db->is_contiguous(), "db");
     dbp = db->data_ptr<float>();
   }
-  // One wave of co-resident blocks (2 per CU) is the sweet spot: a partial second wave of
-  // split-K blocks costs more than the extra parallelism buys (measured, profiles/r1_*).
-  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus <= 0)
-      cus = 256;
-  }
-  int target = 2 * cus;
-  if (const char* e = std::getenv("VINF_TN_TARGET_BLOCKS")) target = std::atoi(e);
-  int splits = target / tiles;
-  const int nkt = (K + 63) / 64;
-  if (splits > nkt / 4) splits = nkt / 4 > 0 ? nkt / 4 : 1;
-  if (splits < 1) splits = 1;
+  const int splits = nf_gemm_tn_splits(M, N, K);
   at::Tensor work;
   float* wp = nullptr;
-  if (splits > 1) {
-    work = at::empty({(long)splits * M * N + (long)splits * M}, dW.options());
+  const long ws = nf_gemm_tn_workspace(M, N, splits);
+  if (ws > 0) {
+    work = at::empty({ws}, dW.options());
     wp = work.data_ptr<float>();
   }
   nf_launch_gemm_tn(dy.data_ptr(), ld2(dy), x.data_ptr(), ld2(x), dW.data_ptr<float>(), ld2(dW), dbp,

@@ -53,6 +53,8 @@ void nf_launch_gemm_nn(const void* dy, long lddy, const void* W, long ldw, const
 void nf_launch_gemm_tn(const void* dy, long lddy, const void* x, long ldx, float* dW, long lddw,
                        float* db, int M, int N, int K, int splits, float* work,
                        hipStream_t stream);
+long nf_gemm_tn_workspace(int M, int N, int splits);
+int nf_gemm_tn_splits(int M, int N, int K);
 
 // planar.hip / radial.hip (fused K-layer stacks; per-row parameter gradients)
 void nf_launch_planar_fwd(const float* z, const float* W, const float* U, const float* B, float* zK,

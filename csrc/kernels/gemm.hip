@@ -28,6 +28,8 @@
 // 16-byte aligned rows (ld % 8 == 0).
 #include "nf_common.h"
 
+#include <cstdlib>
+
 namespace nf {
 namespace gemm {
 
@@ -260,37 +262,36 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(GemmArgs a) {
   }
 }
 
-// out[r][c] (+)= sum_s slab[s][r][c]   (rows x cols, slabs dense with stride rows*cols... of ld_in)
+// One launch for the split-K epilogue of a weight-gradient GEMM:
+//   items [0, rows*cols/4)          : dW[r][c..c+3] = sum_s slab[s][r][c..c+3]
+//   items [rows*cols/4, + rows)     : db[r]         = sum_s part[s][r]
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slabs,
-                                                             long slab_stride, long ld_in, int splits,
+                                                             long slab_stride, int splits,
                                                              float* __restrict__ out, long ld_out,
-                                                             int rows, int cols, int accumulate) {
+                                                             int rows, int cols,
+                                                             const float* __restrict__ dpart,
+                                                             float* __restrict__ db) {
   const int c4 = cols >> 2;
-  const long total = (long)rows * c4;
+  const long n_w = (long)rows * c4;
+  const long total = n_w + (db ? rows : 0);
   for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long)gridDim.x * blockDim.x) {
-    const int r = (int)(idx / c4), q = (int)(idx % c4);
-    float4 s = *reinterpret_cast<const float4*>(slabs + (long)r * ld_in + 4 * q);
-    for (int k = 1; k < splits; ++k) {
-      const float4 t = *reinterpret_cast<const float4*>(slabs + k * slab_stride + (long)r * ld_in + 4 * q);
-      s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    if (idx < n_w) {
+      const int r = (int)(idx / c4), q = (int)(idx % c4);
+      const float* sp = slabs + (long)r * cols + 4 * q;
+      float4 acc = *reinterpret_cast<const float4*>(sp);
+      for (int k = 1; k < splits; ++k) {
+        const float4 t = *reinterpret_cast<const float4*>(sp + k * slab_stride);
+        acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+      }
+      *reinterpret_cast<float4*>(out + (long)r * ld_out + 4 * q) = acc;
+    } else {
+      const int m = (int)(idx - n_w);
+      float acc = 0.f;
+      for (int k = 0; k < splits; ++k) acc += dpart[(long)k * rows + m];
+      db[m] = acc;
     }
-    float4* op = reinterpret_cast<float4*>(out + (long)r * ld_out + 4 * q);
-    if (accumulate) {
-      const float4 o = *op;
-      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
-    }
-    *op = s;
   }
-}
-
-__global__ void __launch_bounds__(256) dbias_reduce_kernel(const float* __restrict__ part, int splits,
-                                                            int M, float* __restrict__ out) {
-  const int m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
-  float s = 0.f;
-  for (int k = 0; k < splits; ++k) s += part[(long)k * M + m];
-  out[m] = s;
 }
 
 template <bool AK, bool BK_, int EPI>
@@ -306,6 +307,18 @@ static void launch(const GemmArgs& a, int splits, hipStream_t stream) {
 
 using namespace nf;
 using namespace nf::gemm;
+
+static int device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
 
 // y[M][N] = act(x[M][K] W[N][K]^T + bias)   -> bf16
 void nf_launch_gemm_nt(const void* x, long ldx, const void* W, long ldw, const void* bias, void* y,
@@ -341,8 +354,24 @@ void nf_launch_gemm_nn(const void* dy, long lddy, const void* W, long ldw, const
   }
 }
 
+long nf_gemm_tn_workspace(int M, int N, int splits) {
+  return splits > 1 ? (long)splits * M * N + (long)splits * M : 0;
+}
+
+// Split-K count for the weight-gradient GEMM: fill exactly one wave of resident blocks
+// (2 per CU); a partial second wave costs more than it buys (profiles/r1_wgrad_splitk_sweep.txt).
+int nf_gemm_tn_splits(int M, int N, int K) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  int target = 2 * device_cus();
+  if (const char* e = getenv("VINF_TN_TARGET_BLOCKS")) target = atoi(e);
+  int splits = target / tiles;
+  const int nkt = (K + BK - 1) / BK;
+  if (splits > nkt / 4) splits = nkt / 4;
+  return splits < 1 ? 1 : splits;
+}
+
 // dW[M][N] = dy[K][M]^T x[K][N] (fp32), db[M] = sum_k dy[k][M]; split-K slabs in `work`
-// (>= splits*M*N + splits*M floats) reduced into dW/db.
+// (nf_gemm_tn_workspace floats) reduced into dW/db by one extra launch.
 void nf_launch_gemm_tn(const void* dy, long lddy, const void* x, long ldx, float* dW, long lddw,
                        float* db, int M, int N, int K, int splits, float* work,
                        hipStream_t stream) {
@@ -351,12 +380,12 @@ void nf_launch_gemm_tn(const void* dy, long lddy, const void* x, long ldx, float
   if (splits < 1) splits = 1;
   if (splits > nkt) splits = nkt;
   const int kts = (nkt + splits - 1) / splits;
-  splits = (nkt + kts - 1) / kts;
+  const int used = (nkt + kts - 1) / kts;
   GemmArgs a{};
   a.A = (const bf16_t*)dy; a.lda = lddy;
   a.B = (const bf16_t*)x; a.ldb = ldx;
   a.M = M; a.N = N; a.K = K; a.k_per_split = kts * BK;
-  if (splits == 1) {
+  if (used == 1) {
     a.C = dW; a.ldc = lddw; a.c_split_stride = 0;
     a.dbias = db;
     launch<false, false, EPI_F32>(a, 1, stream);
@@ -364,17 +393,12 @@ void nf_launch_gemm_tn(const void* dy, long lddy, const void* x, long ldx, float
   }
   const long slab = (long)M * N;
   a.C = work; a.ldc = N; a.c_split_stride = slab;
-  a.dbias = db ? work + splits * slab : nullptr;
-  launch<false, false, EPI_F32>(a, splits, stream);
-  const long total = (long)M * (N / 4);
+  a.dbias = db ? work + (long)used * slab : nullptr;
+  launch<false, false, EPI_F32>(a, used, stream);
+  const long total = (long)M * (N / 4) + (db ? M : 0);
   long blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, work,
-                     slab, (long)N, splits, dW, lddw, M, N, 0);
+                     slab, used, dW, lddw, M, N, a.dbias, db);
   NF_HIP_CHECK(hipGetLastError());
-  if (db) {
-    hipLaunchKernelGGL(dbias_reduce_kernel, dim3((M + 255) / 256), dim3(256), 0, stream,
-                       work + splits * slab, splits, M, db);
-    NF_HIP_CHECK(hipGetLastError());
-  }
 }

@@ -31,6 +31,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=16384)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--only", default=None, help="comma-separated shape names")
+    ap.add_argument("--mine-only", action="store_true", help="skip the hipBLASLt reference")
     a = ap.parse_args()
     ops = native()
     dev = torch.device("cuda")
@@ -41,7 +43,12 @@ def main():
               ("dgrad_l3", "nn_mask", B, 1024, 800), ("dgrad_l2", "nn_mask", B, 1024, 1024),
               ("dgrad_l1", "nn_f32acc", B, 416, 1024),
               ("wgrad_l3", "tn", 800, 1024, B), ("wgrad_l2", "tn", 1024, 1024, B),
-              ("wgrad_l1", "tn", 1024, 416, B)]
+              ("wgrad_l1", "tn", 1024, 416, B),
+              ("sq4096", "nt", 4096, 4096, 4096), ("fwd_k4096", "nt", B, 1024, 4096),
+              ("fwd_k2048", "nt", B, 1024, 2048), ("fwd_m64k", "nt", 65536, 1024, 1024)]
+    if a.only:
+        keep = set(a.only.split(","))
+        shapes = [s for s in shapes if s[0] in keep]
     for name, kind, M, N, K in shapes:
         torch.manual_seed(0)
         if kind == "nt":
@@ -77,7 +84,7 @@ def main():
         tm, tr = [], []
         for _ in range(3):
             tm.append(_time(mine, a.iters))
-            tr.append(_time(ref, a.iters))
+            tr.append(_time(ref, a.iters) if not a.mine_only else float("nan"))
         t_m, t_r = min(tm), min(tr)
         print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "mfma_us": round(t_m * 1e6, 1),
                           "blas_us": round(t_r * 1e6, 1),
