@@ -94,15 +94,87 @@ void gemm_tn(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dW,
                     M, N, K, splits, wp, cur_stream());
 }
 
+// ----------------------------------------------------------------- masked (MADE) variants
+void chk_ranges(const at::Tensor& r, long ntiles, const char* n) {
+  TORCH_CHECK(r.is_cuda() && r.scalar_type() == at::kInt && r.is_contiguous() && r.numel() == 2 * ntiles,
+              n, " must be an int32 GPU tensor [n_tiles, 2]");
+}
+
+void masked_gemm_nt(const at::Tensor& x, const at::Tensor& W, const c10::optional<at::Tensor>& b,
+                    const at::Tensor& y, int64_t relu, const at::Tensor& krange) {
+  chk_mat(x, "x", at::kBFloat16);
+  chk_mat(W, "W", at::kBFloat16);
+  chk_mat(y, "y", at::kBFloat16);
+  const int M = x.size(0), K = x.size(1), N = W.size(0);
+  TORCH_CHECK(W.size(1) == K && y.size(0) == M && y.size(1) == N, "shapes");
+  TORCH_CHECK(K % 32 == 0 && N % 8 == 0, "K % 32 and N % 8 required");
+  chk_ranges(krange, (N + 127) / 128, "krange");
+  const void* bp = (b && b->defined()) ? b->data_ptr() : nullptr;
+  nf_launch_gemm_nt_masked(x.data_ptr(), ld2(x), W.data_ptr(), ld2(W), bp, y.data_ptr(), ld2(y), M,
+                           N, K, (int)relu, krange.data_ptr<int>(), cur_stream());
+}
+
+void masked_gemm_nn(const at::Tensor& dy, const at::Tensor& W, const c10::optional<at::Tensor>& h,
+                    const at::Tensor& dx, const at::Tensor& krange) {
+  chk_mat(dy, "dy", at::kBFloat16);
+  chk_mat(W, "W", at::kBFloat16);
+  const bool f32 = dx.scalar_type() == at::kFloat;
+  chk_mat(dx, "dx", f32 ? at::kFloat : at::kBFloat16);
+  const int M = dy.size(0), K = dy.size(1), N = W.size(1);
+  TORCH_CHECK(W.size(0) == K && dx.size(0) == M && dx.size(1) == N, "shapes");
+  TORCH_CHECK(K % 32 == 0 && N % 8 == 0, "K % 32 and N % 8 required");
+  chk_ranges(krange, (N + 127) / 128, "krange");
+  const void* hp = nullptr;
+  long ldh = 0;
+  if (h && h->defined()) {
+    chk_mat(*h, "h", at::kBFloat16);
+    hp = h->data_ptr();
+    ldh = ld2(*h);
+  }
+  nf_launch_gemm_nn_masked(dy.data_ptr(), ld2(dy), W.data_ptr(), ld2(W), hp, ldh, dx.data_ptr(),
+                           ld2(dx), f32, M, N, K, krange.data_ptr<int>(), cur_stream());
+}
+
+void masked_gemm_tn(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dW,
+                    const c10::optional<at::Tensor>& db, const at::Tensor& skip) {
+  chk_mat(dy, "dy", at::kBFloat16);
+  chk_mat(x, "x", at::kBFloat16);
+  chk_mat(dW, "dW", at::kFloat);
+  const int K = dy.size(0), M = dy.size(1), N = x.size(1);
+  TORCH_CHECK(x.size(0) == K && dW.size(0) == M && dW.size(1) == N, "shapes");
+  TORCH_CHECK(K % 32 == 0 && M % 8 == 0 && N % 8 == 0, "K % 32, M % 8, N % 8 required");
+  TORCH_CHECK(skip.is_cuda() && skip.scalar_type() == at::kByte && skip.is_contiguous() &&
+                  skip.numel() == (long)((M + 127) / 128) * ((N + 127) / 128),
+              "skip must be a uint8 GPU tensor [tiles]");
+  float* dbp = (db && db->defined()) ? db->data_ptr<float>() : nullptr;
+  const int splits = nf_gemm_tn_splits(M, N, K);
+  at::Tensor work;
+  float* wp = nullptr;
+  const long ws = nf_gemm_tn_workspace(M, N, splits);
+  if (ws > 0) {
+    work = at::empty({ws}, dW.options());
+    wp = work.data_ptr<float>();
+  }
+  nf_launch_gemm_tn_masked(dy.data_ptr(), ld2(dy), x.data_ptr(), ld2(x), dW.data_ptr<float>(),
+                           ld2(dW), dbp, M, N, K, splits, wp, skip.data_ptr<unsigned char>(),
+                           cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(vinf, m) {
+  m.def("masked_gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu, Tensor krange) -> ()");
+  m.def("masked_gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, Tensor krange) -> ()");
+  m.def("masked_gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db, Tensor skip) -> ()");
   m.def("gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu) -> ()");
   m.def("gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, bool accumulate) -> ()");
   m.def("gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
+  m.impl("masked_gemm_nt", &masked_gemm_nt);
+  m.impl("masked_gemm_nn", &masked_gemm_nn);
+  m.impl("masked_gemm_tn", &masked_gemm_tn);
   m.impl("gemm_nt", &gemm_nt);
   m.impl("gemm_nn", &gemm_nn);
   m.impl("gemm_tn", &gemm_tn);

@@ -70,3 +70,14 @@ void nf_launch_radial_fwd(const float* z, const float* Z0, const float* AL, cons
 void nf_launch_radial_bwd(const float* saved, const float* Z0, const float* AL, const float* BE,
                           const float* gz, const float* gl, float* dz, float* dZ0, float* dA,
                           float* dBe, int N, int D, int K, int per_sample, hipStream_t stream);
+
+// masked (MADE) GEMMs: per-N-tile K ranges [ntn][2] / per-tile skip flags [ntm*ntn] (128x128 tiles)
+void nf_launch_gemm_nt_masked(const void* x, long ldx, const void* W, long ldw, const void* bias,
+                              void* y, long ldy, int M, int N, int K, int relu, const int* krange,
+                              hipStream_t stream);
+void nf_launch_gemm_nn_masked(const void* dy, long lddy, const void* W, long ldw, const void* aux,
+                              long ld_aux, void* dx, long lddx, int dx_is_f32, int M, int N, int K,
+                              const int* krange, hipStream_t stream);
+void nf_launch_gemm_tn_masked(const void* dy, long lddy, const void* x, long ldx, float* dW,
+                              long lddw, float* db, int M, int N, int K, int splits, float* work,
+                              const unsigned char* skip, hipStream_t stream);

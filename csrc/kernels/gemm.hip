@@ -65,6 +65,9 @@ struct GemmArgs {
   int M, N, K;
   int k_per_split;       // multiple of BK
   int relu;
+  // Masked (MADE) GEMMs - structural sparsity of the weight mask:
+  const int* krange;           // [ntn][2] per output N-tile K range [lo, hi) (multiples of 64), or null
+  const unsigned char* skip;   // [ntm*ntn] 1 -> tile entirely masked: write zeros, no MFMA, or null
 };
 
 __device__ __forceinline__ int mn_swz(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
@@ -150,10 +153,17 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(GemmArgs a) {
   const int tm = wg / ntn, tn = wg % ntn;
   const int m0 = tm * BM, n0 = tn * BN;
   const int split = blockIdx.y;
-  const int kbeg = split * a.k_per_split;
+  int kbeg = split * a.k_per_split;
   int kend = kbeg + a.k_per_split;
   kend = kend < a.K ? kend : a.K;
-  const int nkt = (kend - kbeg + BK - 1) / BK;
+  if (a.krange) {  // skip K-tiles whose weight block is entirely masked
+    const int lo = a.krange[2 * tn], hi = a.krange[2 * tn + 1];
+    kbeg = kbeg > lo ? kbeg : lo;
+    kend = kend < hi ? kend : hi;
+    if (kend < kbeg) kend = kbeg;
+  }
+  int nkt = (kend - kbeg + BK - 1) / BK;
+  if (a.skip && a.skip[tm * ntn + tn] && !(a.dbias != nullptr && tn == 0)) nkt = 0;
 
   const bool do_db = (a.dbias != nullptr) && tn == 0 && wn == 0;
   v4f acc[4][4];
@@ -385,6 +395,69 @@ void nf_launch_gemm_tn(const void* dy, long lddy, const void* x, long ldx, float
   a.A = (const bf16_t*)dy; a.lda = lddy;
   a.B = (const bf16_t*)x; a.ldb = ldx;
   a.M = M; a.N = N; a.K = K; a.k_per_split = kts * BK;
+  if (used == 1) {
+    a.C = dW; a.ldc = lddw; a.c_split_stride = 0;
+    a.dbias = db;
+    launch<false, false, EPI_F32>(a, 1, stream);
+    return;
+  }
+  const long slab = (long)M * N;
+  a.C = work; a.ldc = N; a.c_split_stride = slab;
+  a.dbias = db ? work + (long)used * slab : nullptr;
+  launch<false, false, EPI_F32>(a, used, stream);
+  const long total = (long)M * (N / 4) + (db ? M : 0);
+  long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, work,
+                     slab, used, dW, lddw, M, N, a.dbias, db);
+  NF_HIP_CHECK(hipGetLastError());
+}
+
+// Masked variants (MADE): same kernels, with per-N-tile K ranges / per-tile skip flags.
+void nf_launch_gemm_nt_masked(const void* x, long ldx, const void* W, long ldw, const void* bias,
+                              void* y, long ldy, int M, int N, int K, int relu, const int* krange,
+                              hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  GemmArgs a{};
+  a.A = (const bf16_t*)x; a.lda = ldx;
+  a.B = (const bf16_t*)W; a.ldb = ldw;
+  a.C = y; a.ldc = ldy;
+  a.bias = (const bf16_t*)bias;
+  a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + BK - 1) / BK) * BK; a.relu = relu;
+  a.krange = krange;
+  launch<true, true, EPI_BF16>(a, 1, stream);
+}
+
+void nf_launch_gemm_nn_masked(const void* dy, long lddy, const void* W, long ldw, const void* aux,
+                              long ld_aux, void* dx, long lddx, int dx_is_f32, int M, int N, int K,
+                              const int* krange, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  GemmArgs a{};
+  a.A = (const bf16_t*)dy; a.lda = lddy;
+  a.B = (const bf16_t*)W; a.ldb = ldw;
+  a.C = dx; a.ldc = lddx;
+  a.aux = (const bf16_t*)aux; a.ld_aux = ld_aux;
+  a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + BK - 1) / BK) * BK;
+  a.krange = krange;
+  if (dx_is_f32) launch<true, false, EPI_F32>(a, 1, stream);
+  else if (aux) launch<true, false, EPI_BF16_RELUMASK>(a, 1, stream);
+  else launch<true, false, EPI_BF16>(a, 1, stream);
+}
+
+void nf_launch_gemm_tn_masked(const void* dy, long lddy, const void* x, long ldx, float* dW,
+                              long lddw, float* db, int M, int N, int K, int splits, float* work,
+                              const unsigned char* skip, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  const int nkt = (K + BK - 1) / BK;
+  if (splits < 1) splits = 1;
+  if (splits > nkt) splits = nkt;
+  const int kts = (nkt + splits - 1) / splits;
+  const int used = (nkt + kts - 1) / kts;
+  GemmArgs a{};
+  a.A = (const bf16_t*)dy; a.lda = lddy;
+  a.B = (const bf16_t*)x; a.ldb = ldx;
+  a.M = M; a.N = N; a.K = K; a.k_per_split = kts * BK;
+  a.skip = skip;
   if (used == 1) {
     a.C = dW; a.ldc = lddw; a.c_split_stride = 0;
     a.dbias = db;

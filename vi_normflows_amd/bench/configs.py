@@ -1,0 +1,162 @@
+"""Throughput harness for the north-star configurations (BASELINE.json ``configs``).
+
+    python -m vi_normflows_amd.bench.configs --config 4 [--steps 20 --warmup 5 --batch B]
+    torchrun --nproc-per-node N -m vi_normflows_amd.bench.configs --config 5
+
+Prints one JSON line: samples/s for the whole job (max step time over ranks), timed exactly
+like bench.py (barrier + device sync on both sides of the timed steps). Config 3 (the
+headline) is ``bench.py`` itself.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import time
+
+import torch
+
+from ..parallel import dist as vdist
+
+NAMES = {1: "2D two-moons planar-flow VI on CPU (plumbing, no GPU)",
+         2: "8-layer RealNVP on 784-dim synthetic (MNIST-shape), bf16, 1xMI355X",
+         3: "32-layer RealNVP on 784-dim synthetic, DP over xGMI (see bench.py)",
+         4: "IAF-10 amortized VI (VAE encoder) on 3x32x32 synthetic",
+         5: "MAF-64 density estimation on 1024-dim synthetic"}
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+
+
+def build(cfg_id: int, info, batch: int | None):
+    dev = info.device
+    if cfg_id == 1:
+        from ..distributions.base import StdNormal
+        from ..distributions.energies import get_target
+        from ..flows.planar import PlanarStack
+        from ..inference.elbo import free_energy
+
+        dev = torch.device("cpu")
+        tgt = get_target("U1")
+        flow = PlanarStack(2, 16, init="reference")
+        base = StdNormal(2)
+        B = batch or 256
+        opt = torch.optim.Adam(flow.parameters(), lr=1e-2)
+
+        def step():
+            r = free_energy(base, flow, tgt.log_prob, B, with_stats=False)
+            opt.zero_grad()
+            r.F.backward()
+            opt.step()
+        return step, B, dev, "fp32"
+    if cfg_id in (2, 3):
+        from ..models.realnvp import RealNVPConfig, RealNVPVI
+        from ..parallel.runner import DataParallelRunner
+
+        B = batch or 16384
+        eng = RealNVPVI(RealNVPConfig(n_layers=8 if cfg_id == 2 else 32), batch=B, device=dev,
+                        rank=info.rank)
+        run = DataParallelRunner(eng, info)
+        if dev.type == "cuda":
+            run.capture(warmup=1)
+        return run.step, B, dev, "bf16"
+    if cfg_id == 4:
+        from ..models.iaf_vae import IAFVAE, IAFVAEConfig, synthetic_images
+
+        B = batch or 1024
+        model = IAFVAE(IAFVAEConfig()).to(dev)
+        model = _ddp(model, info)
+        X = synthetic_images(B * 4, device=dev, seed=info.rank)
+        opt = torch.optim.Adam(model.parameters(), lr=3e-4)
+        inner = model.module if hasattr(model, "module") else model
+        it = [0]
+
+        def step():
+            i = it[0] % 4
+            it[0] += 1
+            F = _loss_ddp(model, inner, X[i * B:(i + 1) * B])
+            opt.zero_grad()
+            F.backward()
+            opt.step()
+        return step, B, dev, "bf16 (MFMA masked GEMMs)"
+    if cfg_id == 5:
+        from ..models.maf_density import MAFConfig, MAFDensity, banana_samples
+
+        B = batch or 1024
+        model = MAFDensity(MAFConfig()).to(dev)
+        model = _ddp(model, info)
+        inner = model.module if hasattr(model, "module") else model
+        X = banana_samples(B * 4, 1024, device=dev)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+        it = [0]
+
+        def step():
+            i = it[0] % 4
+            it[0] += 1
+            nll = -(model(X[i * B:(i + 1) * B]) if hasattr(model, "module") else
+                    inner.log_prob(X[i * B:(i + 1) * B])).mean()
+            opt.zero_grad()
+            nll.backward()
+            opt.step()
+        return step, B, dev, "bf16 (MFMA masked GEMMs)"
+    raise KeyError(cfg_id)
+
+
+class _Fwd(torch.nn.Module):
+    """DDP needs forward(); route it to the model's loss / log_prob."""
+
+    def __init__(self, m, kind):
+        super().__init__()
+        self.m, self.kind = m, kind
+
+    def forward(self, x):
+        return self.m.loss(x).F if self.kind == "loss" else self.m.log_prob(x)
+
+
+def _ddp(model, info):
+    if info.world <= 1:
+        return model
+    kind = "loss" if hasattr(model, "encode") else "log_prob"
+    wrapped = _Fwd(model, kind)
+    dev_ids = [info.local_rank] if info.device.type == "cuda" else None
+    ddp = torch.nn.parallel.DistributedDataParallel(wrapped, device_ids=dev_ids, bucket_cap_mb=32,
+                                                    gradient_as_bucket_view=True)
+    ddp.m_inner = model
+    return ddp
+
+
+def _loss_ddp(model, inner, x):
+    if hasattr(model, "module"):
+        return model(x)
+    return inner.loss(x).F
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, required=True)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=None)
+    a = ap.parse_args(argv)
+    info = vdist.init(device_type="cpu" if a.config == 1 else None)
+    step, B, dev, dtype = build(a.config, info, a.batch)
+    for _ in range(a.warmup):
+        step()
+    _sync(dev)
+    vdist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    _sync(dev)
+    vdist.barrier()
+    dt = vdist.all_reduce_max(time.perf_counter() - t0)
+    if info.is_main:
+        print(json.dumps({"config": a.config, "name": NAMES[a.config], "n_ranks": info.world,
+                          "per_rank_batch": B, "ms_per_step": 1000 * dt / a.steps,
+                          "samples_per_s": B * info.world * a.steps / dt, "dtype": dtype}))
+    vdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -70,14 +70,30 @@ class Trainer:
             dist.all_reduce(tot)
         return bool(torch.isfinite(tot))
 
-    def _allreduce_grads(self):
+    def _allreduce_grads(self, bucket_mb: float = 64.0):
+        """Coalesced gradient averaging: grads are packed into flat buckets (one collective
+        per ~64 MB instead of one per tensor), all-reduced, and unpacked."""
         if not (dist.is_initialized() and dist.get_world_size() > 1):
             return
         ws = dist.get_world_size()
-        for p in self.params:
-            if p.grad is not None:
-                dist.all_reduce(p.grad)
-                p.grad.div_(ws)
+        grads = [p.grad for p in self.params if p.grad is not None]
+        cap = int(bucket_mb * 2 ** 20)
+        bucket, size = [], 0
+        for g in grads + [None]:
+            if g is not None and (not bucket or (size + g.numel() * g.element_size() <= cap
+                                                 and g.dtype == bucket[0].dtype)):
+                bucket.append(g)
+                size += g.numel() * g.element_size()
+                continue
+            if bucket:
+                flat = torch.cat([b.reshape(-1) for b in bucket])
+                dist.all_reduce(flat)
+                flat.div_(ws)
+                o = 0
+                for b in bucket:
+                    b.copy_(flat[o:o + b.numel()].view_as(b))
+                    o += b.numel()
+            bucket, size = ([g], g.numel() * g.element_size()) if g is not None else ([], 0)
 
     def step(self):
         t = self.t

@@ -46,5 +46,84 @@ def masked_fraction(mask: torch.Tensor, tile_n: int = _TILE, tile_k: int = 64) -
     return skip / max(total, 1)
 
 
+def skip_flags(mask: torch.Tensor, tile: int = _TILE) -> torch.Tensor:
+    """uint8 [ceil(N/t) * ceil(K/t)]: 1 where a (tile x tile) block of ``mask`` is all zero."""
+    N, K = mask.shape
+    nz = (mask != 0)
+    out = []
+    for i in range(0, N, tile):
+        for j in range(0, K, tile):
+            out.append(0 if nz[i:i + tile, j:j + tile].any() else 1)
+    return torch.tensor(out, dtype=torch.uint8)
+
+
+class MaskPlan:
+    """Per-mask launch metadata for the three masked GEMMs (cached on the mask's device)."""
+
+    def __init__(self, mask: torch.Tensor):
+        m = mask.detach().float().cpu()
+        dev = mask.device
+        self.fwd = tile_ranges(m).to(dev).contiguous()          # y = x (W*M)^T : tiles over out
+        self.bwd = tile_ranges(m.t()).to(dev).contiguous()      # dx = dy (W*M) : tiles over in
+        self.wskip = skip_flags(m).to(dev).contiguous()         # dW tiles that are all masked
+        self.skipped_fraction = masked_fraction(m)
+
+
+_PLANS: dict = {}
+
+
+def plan_for(mask: torch.Tensor) -> MaskPlan:
+    key = (mask.data_ptr(), tuple(mask.shape), str(mask.device), mask._version)
+    p = _PLANS.get(key)
+    if p is None:
+        p = MaskPlan(mask)
+        _PLANS[key] = p
+    return p
+
+
+class _MaskedLinearFn(torch.autograd.Function):
+    """bf16 MFMA masked linear with tile skipping (fp32 master weights, fp32 grads)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, mask):
+        from ._ext import native
+
+        plan = plan_for(mask)
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
+        Wm = (W * mask).to(torch.bfloat16).contiguous()
+        bb = b.to(torch.bfloat16).contiguous() if b is not None else None
+        y = torch.empty(x2.shape[0], W.shape[0], device=x.device, dtype=torch.bfloat16)
+        native().masked_gemm_nt(x2, Wm, bb, y, 0, plan.fwd)
+        ctx.save_for_backward(x2, Wm, mask)
+        ctx.has_b = b is not None
+        ctx.in_shape = shp
+        ctx.out_dtype = x.dtype
+        return y.to(x.dtype).reshape(*shp[:-1], W.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        from ._ext import native
+
+        x2, Wm, mask = ctx.saved_tensors
+        plan = plan_for(mask)
+        g2 = gy.reshape(-1, gy.shape[-1]).to(torch.bfloat16).contiguous()
+        dx = torch.empty(x2.shape[0], x2.shape[1], device=gy.device, dtype=torch.float32)
+        native().masked_gemm_nn(g2, Wm, None, dx, plan.bwd)
+        dW = torch.empty(Wm.shape, device=gy.device, dtype=torch.float32)
+        db = torch.empty(Wm.shape[0], device=gy.device, dtype=torch.float32) if ctx.has_b else None
+        native().masked_gemm_tn(g2, x2, dW, db, plan.wskip)
+        dW.mul_(mask)
+        return dx.to(ctx.out_dtype).reshape(ctx.in_shape), dW, db, None
+
+
+def kernel_ok(x, W) -> bool:
+    N, K = W.shape
+    return x.is_cuda and K % 32 == 0 and N % 32 == 0 and x.reshape(-1, K).shape[0] % 32 == 0
+
+
 def masked_linear(x, W, b, mask):
+    """x (W * mask)^T + b. GPU + MFMA-compatible shapes -> tile-skipping HIP GEMMs; else composite."""
+    if kernel_ok(x, W):
+        return _MaskedLinearFn.apply(x, W, b, mask)
     return F.linear(x, W * mask, b)

@@ -1,0 +1,203 @@
+"""Training CLI.
+
+    python -m vi_normflows_amd.train --config <preset|file.json|file.yaml> [key=value ...]
+    torchrun --nproc-per-node 8 -m vi_normflows_amd.train --config config3_realnvp32_dp8
+
+Tasks: flow_vi (non-amortized VI on a named target), realnvp_vi (explicit-backward engine,
+data parallel, hipGraph), planar_vae (reference MNIST workload on synthetic binary data or a
+user .npy), iaf_vae, maf_density, bbvi. Writes ``<out_dir>/<name>/``: config.json,
+metrics.jsonl, final.json, checkpoints, figures and (planar_vae) the reference ``.npy``
+weights + ``free_energy.txt`` line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import time
+from pathlib import Path
+
+import torch
+
+from .parallel import dist as vdist
+from .utils.config import load, rank_seed
+from .utils.metrics import JsonlLogger, append_free_energy
+
+
+def _device(cfg, info):
+    if cfg.device == "cpu":
+        return torch.device("cpu")
+    return info.device
+
+
+def run_flow_vi(cfg, out, info, logger):
+    from .inference.flow_vi import fit_flow_vi
+    from .viz.plots import plot_density_and_samples, plot_loss
+
+    dev = _device(cfg, info)
+    r = fit_flow_vi(cfg.target, cfg.flow, cfg.K, cfg.iters, cfg.lr, cfg.batch, cfg.optimizer,
+                    cfg.schedule, device=dev, seed=rank_seed(cfg.seed, info.rank),
+                    log_every=cfg.log_every, logger=logger, hidden=cfg.hidden)
+    if info.is_main:
+        with torch.no_grad():
+            zs = r.flow(r.base.sample(2000).to(dev))[0].cpu().double()
+        plot_density_and_samples(r.target, zs, path=out / "density_samples.png",
+                                 title=f"{cfg.flow} K={cfg.K} on {r.target.name}")
+        floor = -r.final["logZ"] if "logZ" in r.final else None
+        plot_loss([h["F"] for h in r.history], path=out / "loss.png", floor=floor)
+        torch.save(r.flow.state_dict(), out / "flow.pt")
+    return r.final
+
+
+def run_realnvp(cfg, out, info, logger):
+    from .models.realnvp import RealNVPConfig, RealNVPVI
+    from .parallel.runner import DataParallelRunner
+    from .utils.checkpoint import load_engine, save_engine
+
+    dev = _device(cfg, info)
+    rc = RealNVPConfig(dim=cfg.dim, n_layers=cfg.K, hidden=cfg.hidden, n_hidden=cfg.n_hidden,
+                       target=cfg.extra.get("target", "banana"), anneal=cfg.schedule
+                       if cfg.schedule in ("reference", "none") else "reference",
+                       anneal_iters=cfg.iters)
+    eng = RealNVPVI(rc, batch=cfg.batch, device=dev, seed=cfg.seed, rank=info.rank, lr=cfg.lr)
+    if cfg.extra.get("resume"):
+        load_engine(eng, cfg.extra["resume"], info.rank)
+    run = DataParallelRunner(eng, info)
+    if dev.type == "cuda" and cfg.extra.get("graph", True):
+        run.capture(warmup=1)
+    t0 = time.perf_counter()
+    start = int(eng.step_t.item())
+    for t in range(start, cfg.iters):
+        run.step()
+        if t % cfg.log_every == 0 or t == cfg.iters - 1:
+            F = float(eng.loss.item())
+            el = time.perf_counter() - t0
+            logger.log({"step": t, "F": F, "beta": float(eng.beta.item()),
+                        "grad_norm": math.sqrt(max(float(eng.gnorm2.item()), 0.0)),
+                        "skipped": float(eng.n_skipped.item()),
+                        "samples_per_s": (t - start + 1) * cfg.batch * info.world / el})
+        if cfg.ckpt_every and (t + 1) % cfg.ckpt_every == 0:
+            save_engine(eng, out / "ckpt.pt", info.rank)
+    save_engine(eng, out / "ckpt.pt", info.rank)
+    return {"free_energy": float(eng.loss.item()), "steps": cfg.iters,
+            "skipped_steps": float(eng.n_skipped.item())}
+
+
+def run_planar_vae(cfg, out, info, logger):
+    import numpy as np
+
+    from .inference.trainer import TrainConfig, Trainer
+    from .models.vae import PlanarVAE, VAEConfig, synthetic_binary_images
+    from .utils.batching import make_batch_iter
+
+    dev = _device(cfg, info)
+    g = torch.Generator().manual_seed(rank_seed(cfg.seed, info.rank))
+    if cfg.extra.get("data_path"):
+        X = torch.from_numpy(np.load(cfg.extra["data_path"], allow_pickle=False)).float()
+    else:
+        X = synthetic_binary_images(cfg.extra.get("n_data", 2000), cfg.dim, seed=cfg.seed)
+    vae = PlanarVAE(VAEConfig(dim_x=cfg.dim, dim_z=cfg.dim_z, K=cfg.K, width=cfg.hidden,
+                              hidden_layers=cfg.n_hidden))
+    vae.init_reference(generator=torch.Generator().manual_seed(cfg.seed))
+    vae.to(dev)
+    it = make_batch_iter(X, cfg.batch, cfg.iters, generator=g, rank=info.rank, world=info.world)
+    gd = torch.Generator(device=dev).manual_seed(rank_seed(cfg.seed, info.rank))
+
+    def loss_fn(t, beta):
+        return vae.loss(it(t).to(dev), beta, gd)
+
+    tr = Trainer(vae.parameters(), loss_fn,
+                 TrainConfig(iters=cfg.iters, lr=cfg.lr, optimizer=cfg.optimizer,
+                             schedule=cfg.schedule, log_every=cfg.log_every), logger=logger)
+    tr.fit()
+    F = tr.history[-1]["F"]
+    if info.is_main:
+        vae.cpu().save_reference(out / f"weights_phi_{cfg.K}.npy", out / f"weights_theta_{cfg.K}.npy")
+        append_free_energy(out / "free_energy.txt", cfg.K, F * cfg.batch)  # per-batch units (Q8)
+    return {"free_energy_per_sample": F}
+
+
+def run_iaf_vae(cfg, out, info, logger):
+    from .inference.trainer import TrainConfig, Trainer
+    from .models.iaf_vae import IAFVAE, IAFVAEConfig, synthetic_images
+
+    dev = _device(cfg, info)
+    model = IAFVAE(IAFVAEConfig(dim_z=cfg.dim_z, hidden=cfg.hidden, n_flows=cfg.K)).to(dev)
+    X = synthetic_images(cfg.extra.get("n_data", 8192), seed=cfg.seed + info.rank, device=dev)
+    gd = torch.Generator(device=dev).manual_seed(rank_seed(cfg.seed, info.rank))
+
+    def loss_fn(t, beta):
+        idx = torch.randint(0, X.shape[0], (cfg.batch,), device=dev, generator=gd)
+        return model.loss(X[idx], beta, gd)
+
+    tr = Trainer(model.parameters(), loss_fn,
+                 TrainConfig(iters=cfg.iters, lr=cfg.lr, optimizer=cfg.optimizer,
+                             schedule=cfg.schedule, log_every=cfg.log_every), logger=logger)
+    tr.fit()
+    return {"free_energy": tr.history[-1]["F"]}
+
+
+def run_maf(cfg, out, info, logger):
+    from .inference.elbo import FreeEnergy
+    from .inference.trainer import TrainConfig, Trainer
+    from .models.maf_density import MAFConfig, MAFDensity, banana_entropy, banana_samples
+
+    dev = _device(cfg, info)
+    model = MAFDensity(MAFConfig(dim=cfg.dim, n_layers=cfg.K, hidden=cfg.hidden,
+                                 n_hidden=cfg.n_hidden)).to(dev)
+    g = torch.Generator().manual_seed(rank_seed(cfg.seed, info.rank))
+
+    def loss_fn(t, beta):
+        x = banana_samples(cfg.batch, cfg.dim, generator=g, device=dev)
+        nll = model.loss(x)
+        return FreeEnergy(nll, {"nll": float(nll)})
+
+    tr = Trainer(model.parameters(), loss_fn,
+                 TrainConfig(iters=cfg.iters, lr=cfg.lr, optimizer=cfg.optimizer,
+                             log_every=cfg.log_every), logger=logger)
+    tr.fit()
+    return {"nll": tr.history[-1]["F"], "nll_floor_entropy": banana_entropy(cfg.dim)}
+
+
+def run_bbvi(cfg, out, info, logger):
+    from .inference.bbvi import black_box_vi, design, linreg_log_joint, linreg_posterior, load_hw0
+
+    x, y = load_hw0(cfg.extra.get("data_path", "data/HW0_data.csv"))
+    X = design(x)
+    prior = [[1.0, 0.0], [0.0, 0.5]]
+    nv = float(cfg.extra.get("noise_var", 0.5))
+    res = black_box_vi(linreg_log_joint(X, y, prior, nv), 2, num_samples=cfg.batch,
+                       iters=cfg.iters, lr=cfg.lr, seed=cfg.seed,
+                       callback=lambda t, lb, m, s: logger.log({"step": t, "lower_bound": lb}))
+    mu, cov = linreg_posterior(X, y, prior, nv)
+    return {"mu_vi": res.mean.tolist(), "sd_vi": torch.exp(res.log_std).tolist(),
+            "mu_post": mu.tolist(), "sd_post": torch.sqrt(torch.diag(cov)).tolist()}
+
+
+TASKS = {"flow_vi": run_flow_vi, "realnvp_vi": run_realnvp, "planar_vae": run_planar_vae,
+         "iaf_vae": run_iaf_vae, "maf_density": run_maf, "bbvi": run_bbvi}
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--config", default=None)
+    ap.add_argument("overrides", nargs="*")
+    a = ap.parse_args(argv)
+    cfg = load(a.config, a.overrides)
+    info = vdist.init(device_type="cpu" if cfg.device == "cpu" else None)
+    torch.manual_seed(rank_seed(cfg.seed, info.rank))
+    out = Path(cfg.out_dir) / cfg.name
+    out.mkdir(parents=True, exist_ok=True)
+    if info.is_main:
+        cfg.save(out / "config.json")
+    logger = JsonlLogger(out / "metrics.jsonl", echo=info.is_main, rank=info.rank)
+    final = TASKS[cfg.task](cfg, out, info, logger)
+    if info.is_main:
+        (out / "final.json").write_text(json.dumps(final, indent=2))
+        print(json.dumps({"final": final}))
+    vdist.shutdown()
+    return final
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,125 @@
+"""Typed run configuration: dataclasses, YAML/JSON files, ``key=value`` CLI overrides, presets.
+
+Replaces the reference's scattered module constants / arch dicts / sys.argv parsing
+(SURVEY §5.6). One seed per run, derived per rank. The five north-star configurations
+of BASELINE.json are shipped as presets:
+
+    config1_two_moons_cpu   2-D two-moons (U1) planar-flow VI on CPU (plumbing)
+    config2_realnvp8        8-layer RealNVP on 784-d synthetic, bf16, 1 GPU
+    config3_realnvp32_dp8   32-layer RealNVP on 784-d synthetic, data-parallel (the headline)
+    config4_iaf10_vae       IAF-10 amortized VI (VAE encoder) on 3x32x32 synthetic, DP
+    config5_maf64           MAF-64 density estimation on 1024-d synthetic, DP
+plus ``mnist_planar_vae`` (the reference's main workload, src/learning_mnist.py).
+"""
+from __future__ import annotations
+
+import copy
+import json
+from dataclasses import asdict, dataclass, field, fields, is_dataclass
+from pathlib import Path
+
+
+@dataclass
+class RunConfig:
+    name: str = "custom"
+    task: str = "flow_vi"          # flow_vi | realnvp_vi | planar_vae | iaf_vae | maf_density | bbvi
+    device: str = "auto"           # auto | cpu | cuda
+    seed: int = 0
+    iters: int = 1000
+    lr: float = 1e-3
+    optimizer: str = "adam"
+    schedule: str = "none"         # reference | theano | linear | none
+    batch: int = 256               # per-rank batch / MC samples per step
+    log_every: int = 100
+    ckpt_every: int = 0
+    out_dir: str = "runs"
+    # flow / model
+    target: str = "U1"
+    flow: str = "planar"
+    K: int = 8
+    dim: int = 2
+    hidden: int = 64
+    n_hidden: int = 2
+    dim_z: int = 40
+    extra: dict = field(default_factory=dict)
+
+    def override(self, items: list[str]) -> "RunConfig":
+        """Apply ``key=value`` overrides (values parsed as JSON when possible)."""
+        c = copy.deepcopy(self)
+        names = {f.name: f for f in fields(c)}
+        for it in items:
+            if "=" not in it:
+                raise ValueError(f"override must be key=value: {it}")
+            k, v = it.split("=", 1)
+            try:
+                val = json.loads(v)
+            except json.JSONDecodeError:
+                val = v
+            if k.startswith("extra."):
+                c.extra[k[6:]] = val
+            elif k in names:
+                setattr(c, k, type(getattr(c, k))(val) if getattr(c, k) is not None and
+                        not isinstance(getattr(c, k), dict) else val)
+            else:
+                raise KeyError(f"unknown config key {k}")
+        return c
+
+    def to_dict(self) -> dict:
+        return asdict(self)
+
+    def save(self, path) -> None:
+        Path(path).parent.mkdir(parents=True, exist_ok=True)
+        Path(path).write_text(json.dumps(self.to_dict(), indent=2))
+
+
+PRESETS: dict[str, RunConfig] = {
+    "config1_two_moons_cpu": RunConfig(name="config1_two_moons_cpu", task="flow_vi", device="cpu",
+                                       target="U1", flow="planar", K=16, dim=2, iters=10000,
+                                       lr=1e-2, batch=256, optimizer="adam"),
+    "config2_realnvp8": RunConfig(name="config2_realnvp8", task="realnvp_vi", device="cuda",
+                                  K=8, dim=784, hidden=1024, batch=16384, iters=200, lr=1e-4,
+                                  schedule="reference"),
+    "config3_realnvp32_dp8": RunConfig(name="config3_realnvp32_dp8", task="realnvp_vi",
+                                       device="cuda", K=32, dim=784, hidden=1024, batch=16384,
+                                       iters=200, lr=1e-4, schedule="reference"),
+    "config4_iaf10_vae": RunConfig(name="config4_iaf10_vae", task="iaf_vae", device="cuda", K=10,
+                                   dim=3072, hidden=1024, dim_z=256, batch=1024, iters=200,
+                                   lr=3e-4),
+    "config5_maf64": RunConfig(name="config5_maf64", task="maf_density", device="cuda", K=64,
+                               dim=1024, hidden=1024, n_hidden=1, batch=1024, iters=200, lr=1e-4),
+    "mnist_planar_vae": RunConfig(name="mnist_planar_vae", task="planar_vae", device="auto", K=4,
+                                  dim=784, hidden=64, n_hidden=3, dim_z=40, batch=128,
+                                  iters=10000, lr=1e-3, schedule="reference"),
+}
+
+
+def load(spec: str | None, overrides: list[str] | None = None) -> RunConfig:
+    """``spec``: preset name, path to .json/.yaml, or None (defaults)."""
+    if spec is None:
+        cfg = RunConfig()
+    elif spec in PRESETS:
+        cfg = copy.deepcopy(PRESETS[spec])
+    else:
+        p = Path(spec)
+        text = p.read_text()
+        if p.suffix in (".yaml", ".yml"):
+            import yaml
+
+            data = yaml.safe_load(text)
+        else:
+            data = json.loads(text)
+        base = copy.deepcopy(PRESETS.get(data.get("preset", ""), RunConfig()))
+        data.pop("preset", None)
+        cfg = base.override([f"{k}={json.dumps(v)}" for k, v in data.items()
+                             if k != "extra"])
+        cfg.extra.update(data.get("extra", {}))
+    return cfg.override(overrides or [])
+
+
+def rank_seed(seed: int, rank: int) -> int:
+    """Per-rank seed derivation (one seed per run)."""
+    return (int(seed) * 1_000_003 + 7919 * int(rank)) % (2 ** 31 - 1)
+
+
+def is_config(obj) -> bool:
+    return is_dataclass(obj)
