@@ -56,7 +56,7 @@ def black_box_vi(logprob, D: int, num_samples: int = 1000, iters: int = 1000, lr
         loss.backward()
         opt.step()
         if t % log_every == 0 or t == iters - 1:
-            trace.append((t, float(lower)))
+            trace.append((t, float(lower.detach())))
             if callback:
                 callback(t, float(lower), mean.detach(), log_std.detach())
     return BBVIResult(mean.detach(), log_std.detach(), trace)
