@@ -94,6 +94,40 @@ void gemm_tn(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dW,
                     M, N, K, splits, wp, cur_stream());
 }
 
+// Grouped weight gradients: dW[p] = dy[p]^T x[p], db[p] = colsum(dy[p]) in one launch (+ reduce).
+void gemm_tn_group(at::TensorList dy, at::TensorList x, at::TensorList dW,
+                   const c10::List<c10::optional<at::Tensor>>& db) {
+  const size_t n = dy.size();
+  TORCH_CHECK(n >= 1 && n <= 4 && x.size() == n && dW.size() == n && db.size() == n,
+              "gemm_tn_group: 1..4 problems with matching lists");
+  NfTnProblem pr[4];
+  for (size_t p = 0; p < n; ++p) {
+    chk_mat(dy[p], "dy", at::kBFloat16);
+    chk_mat(x[p], "x", at::kBFloat16);
+    chk_mat(dW[p], "dW", at::kFloat);
+    const int K = dy[p].size(0), M = dy[p].size(1), N = x[p].size(1);
+    TORCH_CHECK(x[p].size(0) == K, "batch mismatch");
+    TORCH_CHECK(dW[p].size(0) == M && dW[p].size(1) == N, "dW shape");
+    TORCH_CHECK(K % 32 == 0 && M % 8 == 0 && N % 8 == 0, "K % 32, M % 8, N % 8 required");
+    float* dbp = nullptr;
+    const c10::optional<at::Tensor> b = db.get(p);
+    if (b && b->defined()) {
+      TORCH_CHECK(b->scalar_type() == at::kFloat && b->numel() == M && b->is_contiguous(), "db");
+      dbp = b->data_ptr<float>();
+    }
+    pr[p] = NfTnProblem{dy[p].data_ptr(), ld2(dy[p]), x[p].data_ptr(), ld2(x[p]),
+                        dW[p].data_ptr<float>(), ld2(dW[p]), dbp, M, N, K};
+  }
+  at::Tensor work;
+  float* wp = nullptr;
+  const long ws = nf_gemm_tn_group_workspace((int)n, pr);
+  if (ws > 0) {
+    work = at::empty({ws}, dW[0].options());
+    wp = work.data_ptr<float>();
+  }
+  nf_launch_gemm_tn_group((int)n, pr, wp, cur_stream());
+}
+
 // ----------------------------------------------------------------- masked (MADE) variants
 void chk_ranges(const at::Tensor& r, long ntiles, const char* n) {
   TORCH_CHECK(r.is_cuda() && r.scalar_type() == at::kInt && r.is_contiguous() && r.numel() == 2 * ntiles,
@@ -162,13 +196,17 @@ void masked_gemm_tn(const at::Tensor& dy, const at::Tensor& x, const at::Tensor&
 
 }  // namespace
 
+void gemm_set_mode(int64_t mode, int64_t depth) { nf_gemm_set_mode((int)mode, (int)depth); }
+
 TORCH_LIBRARY_FRAGMENT(vinf, m) {
+  m.def("gemm_set_mode(int mode, int depth) -> ()", &gemm_set_mode);
   m.def("masked_gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu, Tensor krange) -> ()");
   m.def("masked_gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, Tensor krange) -> ()");
   m.def("masked_gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db, Tensor skip) -> ()");
   m.def("gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu) -> ()");
   m.def("gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, bool accumulate) -> ()");
   m.def("gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db) -> ()");
+  m.def("gemm_tn_group(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
@@ -178,4 +216,5 @@ TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
   m.impl("gemm_nt", &gemm_nt);
   m.impl("gemm_nn", &gemm_nn);
   m.impl("gemm_tn", &gemm_tn);
+  m.impl("gemm_tn_group", &gemm_tn_group);
 }

@@ -1,0 +1,127 @@
+// Shared pieces of the bf16 MFMA GEMM kernels (gemm.hip: 128x128 tile, gemm256.hip: 256x256
+// 8-phase tile): argument block, epilogue kinds, LDS operand-image swizzles and fragment reads.
+//
+// LDS operand images (one 128 x 64 bf16 block, 16 KiB):
+//   k-major  [128 rows][64 k]  : 16-B chunk c of row r stored at c ^ (r & 7)
+//   mn-major [64 k][128 mn]    : 16-B chunk c of k-row k stored at c ^ mn_swz(k)
+// both conflict-free for the fragment reads below (tools/lds_bank_model.py).
+#pragma once
+#include "nf_common.h"
+
+namespace nf {
+namespace gemm {
+
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+#define LDS_AS __attribute__((address_space(3)))
+
+enum Epi : int {
+  EPI_BF16 = 0,          // C(bf16) = act(acc + bias)
+  EPI_F32 = 1,           // C(fp32) = acc  (split-K slab when gridDim.y > 1)
+  EPI_BF16_RELUMASK = 2, // C(bf16) = acc * 1(aux > 0)
+  EPI_F32_ACC = 3,       // C(fp32) += acc
+};
+
+struct GemmArgs {
+  const bf16_t* A;
+  long lda;
+  const bf16_t* B;
+  long ldb;
+  void* C;
+  long ldc;
+  long c_split_stride;   // elements between split-K slabs (EPI_F32)
+  const bf16_t* bias;    // [N] bf16 (EPI_BF16), may be null
+  const bf16_t* aux;     // [M][ld_aux] (EPI_BF16_RELUMASK)
+  long ld_aux;
+  float* dbias;          // [splits][M] partial sum_k Aop(m,k), may be null
+  int M, N, K;
+  int k_per_split;       // multiple of BK
+  int relu;
+  // Masked (MADE) GEMMs - structural sparsity of the weight mask:
+  const int* krange;           // [ntn][2] per output N-tile K range [lo, hi) (multiples of 64), or null
+  const unsigned char* skip;   // [ntm*ntn] 1 -> tile entirely masked: write zeros, no MFMA, or null
+};
+
+// Grouped launch: up to 4 independent problems (the weight gradients of one conditioner MLP),
+// blocks [start[p], start[p+1]) belong to problem p, split-major inside a problem so the column
+// tiles sharing an A panel sit on consecutive (XCD-remapped) block ids.
+struct GroupArgs {
+  GemmArgs p[4];
+  int start[5];
+  int nprob;
+};
+
+__device__ __forceinline__ int mn_swz(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
+
+// 8 consecutive k (k-step ks in {0,1}) for tile row r0 + (lane & 15).
+template <bool KMAJOR>
+__device__ __forceinline__ v8s read_frag(const char* lds_tile, int r0, int ks, int lane) {
+  if (KMAJOR) {
+    const int r = r0 + (lane & 15);
+    const int c = ks * 4 + (lane >> 4);
+    return *(const LDS_AS v8s*)(lds_tile + r * 128 + ((c ^ (r & 7)) << 4));
+  } else {
+    const int i = lane & 15, g = lane >> 4;
+    const int col = r0 + 4 * (i & 3);
+    const int chunk = col >> 3, sub = (col >> 2) & 1;
+    v8s out;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = ks * 32 + 8 * g + 4 * h + (i >> 2);
+      const LDS_AS v4s* p =
+          (const LDS_AS v4s*)(lds_tile + k * 256 + ((chunk ^ mn_swz(k)) << 4) + sub * 8);
+      const v4s t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS v4s*)p);
+      if (h == 0) {
+        out[0] = t[0]; out[1] = t[1]; out[2] = t[2]; out[3] = t[3];
+      } else {
+        out[4] = t[0]; out[5] = t[1]; out[6] = t[2]; out[7] = t[3];
+      }
+    }
+    return out;
+  }
+}
+
+// Epilogue for one accumulator fragment: 4 consecutive n of output row m.
+template <int EPI>
+__device__ __forceinline__ void epi_store(const GemmArgs& a, v4f v, int m, int n, int split) {
+  if (EPI == EPI_BF16) {
+    if (a.bias) {
+      const ushort4 bb = *reinterpret_cast<const ushort4*>(a.bias + n);
+      v[0] += bf2f(bb.x); v[1] += bf2f(bb.y); v[2] += bf2f(bb.z); v[3] += bf2f(bb.w);
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+    }
+    ushort4 o;
+    o.x = f2bf(v[0]); o.y = f2bf(v[1]); o.z = f2bf(v[2]); o.w = f2bf(v[3]);
+    *reinterpret_cast<ushort4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
+  } else if (EPI == EPI_BF16_RELUMASK) {
+    const ushort4 h = *reinterpret_cast<const ushort4*>(a.aux + (long)m * a.ld_aux + n);
+    // bf16 > 0  <=>  sign bit clear and not +0
+    v[0] = (h.x != 0 && !(h.x & 0x8000)) ? v[0] : 0.f;
+    v[1] = (h.y != 0 && !(h.y & 0x8000)) ? v[1] : 0.f;
+    v[2] = (h.z != 0 && !(h.z & 0x8000)) ? v[2] : 0.f;
+    v[3] = (h.w != 0 && !(h.w & 0x8000)) ? v[3] : 0.f;
+    ushort4 o;
+    o.x = f2bf(v[0]); o.y = f2bf(v[1]); o.z = f2bf(v[2]); o.w = f2bf(v[3]);
+    *reinterpret_cast<ushort4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
+  } else if (EPI == EPI_F32) {
+    float* cp = (float*)a.C + (long)split * a.c_split_stride + (long)m * a.ldc + n;
+    *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {  // EPI_F32_ACC
+    float* cp = (float*)a.C + (long)m * a.ldc + n;
+    float4 o = *reinterpret_cast<float4*>(cp);
+    o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
+    *reinterpret_cast<float4*>(cp) = o;
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+}  // namespace gemm
+}  // namespace nf

@@ -54,6 +54,29 @@ void nf_launch_gemm_tn(const void* dy, long lddy, const void* x, long ldx, float
                        float* db, int M, int N, int K, int splits, float* work,
                        hipStream_t stream);
 long nf_gemm_tn_workspace(int M, int N, int splits);
+// grouped weight gradients dW_p = dy_p^T x_p, db_p = colsum(dy_p) (p < 4), one GEMM launch +
+// one reduce launch
+struct NfTnProblem {
+  const void* dy; long lddy;
+  const void* x; long ldx;
+  float* dW; long lddw;
+  float* db;
+  int M, N, K;
+};
+long nf_gemm_tn_group_workspace(int nprob, const NfTnProblem* pr);
+void nf_launch_gemm_tn_group(int nprob, const NfTnProblem* pr, float* work, hipStream_t stream);
+// gemm256.hip: 256x256 8-phase kernel (forward / input-gradient products)
+void nf_launch_gemm256_nt(const void* x, long ldx, const void* W, long ldw, const void* bias,
+                          void* y, long ldy, int M, int N, int K, int relu, hipStream_t stream);
+void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, const void* aux,
+                          long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
+                          int N, int K, hipStream_t stream);
+void nf_gemm256_set_depth(int d);
+int nf_launch_gemm256_tn_partials(const void* dy, long lddy, const void* x, long ldx, float* C,
+                                  long ldc, long slab_stride, float* dbias, int M, int N, int K,
+                                  int splits, hipStream_t stream);
+// mode: 0 auto, 1 force 128x128, 2 force 256x256; depth: half-tiles in flight (3 or 4)
+void nf_gemm_set_mode(int mode, int depth);
 int nf_gemm_tn_splits(int M, int N, int K);
 
 // planar.hip / radial.hip (fused K-layer stacks; per-row parameter gradients)

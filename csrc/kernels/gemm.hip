@@ -26,51 +26,17 @@
 //     A row-panel run on one XCD's L2.
 // Requirements (checked on the host): K % 32 == 0, M % 8 == 0 (M-major A), N % 8 == 0,
 // 16-byte aligned rows (ld % 8 == 0).
-#include "nf_common.h"
+#include "gemm_tile.h"
 
 #include <cstdlib>
 
 namespace nf {
 namespace gemm {
 
-typedef short v8s __attribute__((ext_vector_type(8)));
-typedef short v4s __attribute__((ext_vector_type(4)));
-typedef float v4f __attribute__((ext_vector_type(4)));
-#define LDS_AS __attribute__((address_space(3)))
-
 constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
 constexpr int TILE_BYTES = 128 * 64 * 2;       // one operand, one stage
 constexpr int STAGE_BYTES = 2 * TILE_BYTES;    // A + B
 constexpr int SMEM_BYTES = 2 * STAGE_BYTES;    // double buffered
-
-enum Epi : int {
-  EPI_BF16 = 0,          // C(bf16) = act(acc + bias)
-  EPI_F32 = 1,           // C(fp32) = acc  (split-K slab when gridDim.y > 1)
-  EPI_BF16_RELUMASK = 2, // C(bf16) = acc * 1(aux > 0)
-  EPI_F32_ACC = 3,       // C(fp32) += acc
-};
-
-struct GemmArgs {
-  const bf16_t* A;
-  long lda;
-  const bf16_t* B;
-  long ldb;
-  void* C;
-  long ldc;
-  long c_split_stride;   // elements between split-K slabs (EPI_F32)
-  const bf16_t* bias;    // [N] bf16 (EPI_BF16), may be null
-  const bf16_t* aux;     // [M][ld_aux] (EPI_BF16_RELUMASK)
-  long ld_aux;
-  float* dbias;          // [splits][M] partial sum_k Aop(m,k), may be null
-  int M, N, K;
-  int k_per_split;       // multiple of BK
-  int relu;
-  // Masked (MADE) GEMMs - structural sparsity of the weight mask:
-  const int* krange;           // [ntn][2] per output N-tile K range [lo, hi) (multiples of 64), or null
-  const unsigned char* skip;   // [ntm*ntn] 1 -> tile entirely masked: write zeros, no MFMA, or null
-};
-
-__device__ __forceinline__ int mn_swz(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
 
 // Stage one 128 x 64 operand tile into LDS (wave-uniform dst per 1 KiB piece).
 template <bool KMAJOR>
@@ -107,52 +73,15 @@ __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ base, long
   }
 }
 
-// 8 consecutive k (k-step ks in {0,1}) for tile row r0 + (lane & 15).
-template <bool KMAJOR>
-__device__ __forceinline__ v8s read_frag(const char* lds_tile, int r0, int ks, int lane) {
-  if (KMAJOR) {
-    const int r = r0 + (lane & 15);
-    const int c = ks * 4 + (lane >> 4);
-    return *(const LDS_AS v8s*)(lds_tile + r * 128 + ((c ^ (r & 7)) << 4));
-  } else {
-    const int i = lane & 15, g = lane >> 4;
-    const int col = r0 + 4 * (i & 3);
-    const int chunk = col >> 3, sub = (col >> 2) & 1;
-    v8s out;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int k = ks * 32 + 8 * g + 4 * h + (i >> 2);
-      const LDS_AS v4s* p =
-          (const LDS_AS v4s*)(lds_tile + k * 256 + ((chunk ^ mn_swz(k)) << 4) + sub * 8);
-      const v4s t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS v4s*)p);
-      if (h == 0) {
-        out[0] = t[0]; out[1] = t[1]; out[2] = t[2]; out[3] = t[3];
-      } else {
-        out[4] = t[0]; out[5] = t[1]; out[6] = t[2]; out[7] = t[3];
-      }
-    }
-    return out;
-  }
-}
-
-__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
-  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-}
-
 template <bool A_KMAJOR, bool B_KMAJOR, int EPI>
-__global__ void __launch_bounds__(NTHR, 2) gemm_kernel(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+__device__ __forceinline__ void gemm_body(const GemmArgs& a, int wg, int split, char* smem) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
 
   const int ntn = (a.N + BN - 1) / BN;
-  const int ntm = (a.M + BM - 1) / BM;
-  const int wg = xcd_remap(blockIdx.x, ntm * ntn);
   const int tm = wg / ntn, tn = wg % ntn;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int split = blockIdx.y;
   int kbeg = split * a.k_per_split;
   int kend = kbeg + a.k_per_split;
   kend = kend < a.K ? kend : a.K;
@@ -236,40 +165,30 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(GemmArgs a) {
     for (int i = 0; i < 4; ++i) {
       const int n = n0 + wn * 64 + i * 16 + g * 4;
       if (n >= a.N) continue;
-      v4f v = acc[i][j];
-      if (EPI == EPI_BF16) {
-        if (a.bias) {
-          const ushort4 bb = *reinterpret_cast<const ushort4*>(a.bias + n);
-          v[0] += bf2f(bb.x); v[1] += bf2f(bb.y); v[2] += bf2f(bb.z); v[3] += bf2f(bb.w);
-        }
-        if (a.relu) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-        }
-        ushort4 o;
-        o.x = f2bf(v[0]); o.y = f2bf(v[1]); o.z = f2bf(v[2]); o.w = f2bf(v[3]);
-        *reinterpret_cast<ushort4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
-      } else if (EPI == EPI_BF16_RELUMASK) {
-        const ushort4 h = *reinterpret_cast<const ushort4*>(a.aux + (long)m * a.ld_aux + n);
-        // bf16 > 0  <=>  sign bit clear and not +0
-        v[0] = (h.x != 0 && !(h.x & 0x8000)) ? v[0] : 0.f;
-        v[1] = (h.y != 0 && !(h.y & 0x8000)) ? v[1] : 0.f;
-        v[2] = (h.z != 0 && !(h.z & 0x8000)) ? v[2] : 0.f;
-        v[3] = (h.w != 0 && !(h.w & 0x8000)) ? v[3] : 0.f;
-        ushort4 o;
-        o.x = f2bf(v[0]); o.y = f2bf(v[1]); o.z = f2bf(v[2]); o.w = f2bf(v[3]);
-        *reinterpret_cast<ushort4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
-      } else if (EPI == EPI_F32) {
-        float* cp = (float*)a.C + (long)split * a.c_split_stride + (long)m * a.ldc + n;
-        *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
-      } else {  // EPI_F32_ACC
-        float* cp = (float*)a.C + (long)m * a.ldc + n;
-        float4 o = *reinterpret_cast<float4*>(cp);
-        o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
-        *reinterpret_cast<float4*>(cp) = o;
-      }
+      epi_store<EPI>(a, acc[i][j], m, n, split);
     }
   }
+}
+
+template <bool A_KMAJOR, bool B_KMAJOR, int EPI>
+__global__ void __launch_bounds__(NTHR, 2) gemm_kernel(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  gemm_body<A_KMAJOR, B_KMAJOR, EPI>(a, xcd_remap(blockIdx.x, ntm * ntn), blockIdx.y, smem);
+}
+
+template <bool A_KMAJOR, bool B_KMAJOR, int EPI>
+__global__ void __launch_bounds__(NTHR, 2) gemm_group_kernel(GroupArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+  const int id = xcd_remap(blockIdx.x, g.start[g.nprob]);
+  int p = 0;
+#pragma unroll
+  for (int q = 1; q < 4; ++q)
+    if (q < g.nprob && id >= g.start[q]) p = q;
+  const GemmArgs& a = g.p[p];
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  const int local = id - g.start[p];
+  gemm_body<A_KMAJOR, B_KMAJOR, EPI>(a, local % tiles, local / tiles, smem);
 }
 
 // One launch for the split-K epilogue of a weight-gradient GEMM:
@@ -304,6 +223,50 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   }
 }
 
+// Grouped split-K epilogue: problem p owns items [istart[p], istart[p+1]) laid out as in
+// splitk_reduce_kernel.
+struct ReduceGroup {
+  const float* slabs[4];
+  long slab_stride[4];
+  int splits[4];
+  float* out[4];
+  long ld_out[4];
+  int rows[4], cols[4];
+  const float* dpart[4];
+  float* db[4];
+  long istart[5];
+  int nprob;
+};
+
+__global__ void __launch_bounds__(256) splitk_reduce_group_kernel(ReduceGroup r) {
+  const long total = r.istart[r.nprob];
+  for (long gidx = (long)blockIdx.x * blockDim.x + threadIdx.x; gidx < total;
+       gidx += (long)gridDim.x * blockDim.x) {
+    int p = 0;
+#pragma unroll
+    for (int q = 1; q < 4; ++q)
+      if (q < r.nprob && gidx >= r.istart[q]) p = q;
+    const long idx = gidx - r.istart[p];
+    const int cols = r.cols[p], c4 = cols >> 2, splits = r.splits[p];
+    const long n_w = (long)r.rows[p] * c4;
+    if (idx < n_w) {
+      const int row = (int)(idx / c4), q = (int)(idx % c4);
+      const float* sp = r.slabs[p] + (long)row * cols + 4 * q;
+      float4 acc = *reinterpret_cast<const float4*>(sp);
+      for (int k = 1; k < splits; ++k) {
+        const float4 t = *reinterpret_cast<const float4*>(sp + k * r.slab_stride[p]);
+        acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+      }
+      *reinterpret_cast<float4*>(r.out[p] + (long)row * r.ld_out[p] + 4 * q) = acc;
+    } else {
+      const int m = (int)(idx - n_w);
+      float acc = 0.f;
+      for (int k = 0; k < splits; ++k) acc += r.dpart[p][(long)k * r.rows[p] + m];
+      r.db[p][m] = acc;
+    }
+  }
+}
+
 template <bool AK, bool BK_, int EPI>
 static void launch(const GemmArgs& a, int splits, hipStream_t stream) {
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
@@ -318,6 +281,8 @@ static void launch(const GemmArgs& a, int splits, hipStream_t stream) {
 using namespace nf;
 using namespace nf::gemm;
 
+void nf_launch_gemm256_tn_group(const nf::gemm::GroupArgs& g, hipStream_t stream);
+
 static int device_cus() {
   static int cus = 0;
   if (cus == 0) {
@@ -330,10 +295,42 @@ static int device_cus() {
   return cus;
 }
 
+// Kernel choice: 0 auto, 1 the 128x128 kernel here, 2 the 256x256 8-phase kernel (gemm256.hip)
+// for the M = batch products (forward / input-gradient), 3 also for the split-K weight
+// gradients. VINF_GEMM_TILE=128|256|257 selects 1|2|3.
+static int g_tile_mode = -1;
+
+void nf_gemm_set_mode(int mode, int depth) {
+  g_tile_mode = mode;
+  nf_gemm256_set_depth(depth);
+}
+
+static bool use_256(int M, int N, int K) {
+  if (g_tile_mode < 0) {
+    g_tile_mode = 0;
+    if (const char* e = getenv("VINF_GEMM_TILE"))
+      g_tile_mode = atoi(e) == 256 ? 2 : (atoi(e) == 128 ? 1 : (atoi(e) == 257 ? 3 : 0));
+  }
+  if (g_tile_mode == 1) return false;
+  if (g_tile_mode >= 2) return true;
+  // auto: enough 256x256 tiles to cover every CU once
+  const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+  return tiles >= device_cus() && K >= 256;
+}
+
+static bool use_256_tn() {
+  if (g_tile_mode < 0) use_256(1, 1, 1);  // resolve the env default
+  return g_tile_mode == 3;
+}
+
 // y[M][N] = act(x[M][K] W[N][K]^T + bias)   -> bf16
 void nf_launch_gemm_nt(const void* x, long ldx, const void* W, long ldw, const void* bias, void* y,
                        long ldy, int M, int N, int K, int relu, hipStream_t stream) {
   if (M <= 0 || N <= 0) return;
+  if (use_256(M, N, K)) {
+    nf_launch_gemm256_nt(x, ldx, W, ldw, bias, y, ldy, M, N, K, relu, stream);
+    return;
+  }
   GemmArgs a{};
   a.A = (const bf16_t*)x; a.lda = ldx;
   a.B = (const bf16_t*)W; a.ldb = ldw;
@@ -348,6 +345,11 @@ void nf_launch_gemm_nn(const void* dy, long lddy, const void* W, long ldw, const
                        long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
                        int N, int K, hipStream_t stream) {
   if (M <= 0 || N <= 0) return;
+  if (use_256(M, N, K)) {
+    nf_launch_gemm256_nn(dy, lddy, W, ldw, aux, ld_aux, dx, lddx, dx_is_f32, accumulate, M, N, K,
+                         stream);
+    return;
+  }
   GemmArgs a{};
   a.A = (const bf16_t*)dy; a.lda = lddy;
   a.B = (const bf16_t*)W; a.ldb = ldw;
@@ -371,6 +373,13 @@ long nf_gemm_tn_workspace(int M, int N, int splits) {
 // Split-K count for the weight-gradient GEMM: fill exactly one wave of resident blocks
 // (2 per CU); a partial second wave costs more than it buys (profiles/r1_wgrad_splitk_sweep.txt).
 int nf_gemm_tn_splits(int M, int N, int K) {
+  if (use_256_tn()) {  // one 256x256 block per CU
+    const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+    int sp = device_cus() / tiles;
+    const int nkt = (K + 63) / 64;
+    if (sp > nkt / 4) sp = nkt / 4;
+    return sp < 1 ? 1 : sp;
+  }
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   int target = 2 * device_cus();
   if (const char* e = getenv("VINF_TN_TARGET_BLOCKS")) target = atoi(e);
@@ -386,6 +395,24 @@ void nf_launch_gemm_tn(const void* dy, long lddy, const void* x, long ldx, float
                        float* db, int M, int N, int K, int splits, float* work,
                        hipStream_t stream) {
   if (M <= 0 || N <= 0) return;
+  if (use_256_tn()) {  // 256x256 split-K kernel (gemm256.hip), splits from nf_gemm_tn_splits
+    int sp = splits < 1 ? 1 : splits;
+    if (sp == 1) {
+      nf_launch_gemm256_tn_partials(dy, lddy, x, ldx, dW, lddw, 0, db, M, N, K, 1, stream);
+      return;
+    }
+    const long slab = (long)M * N;
+    float* dpart = db ? work + (long)sp * slab : nullptr;
+    const int used = nf_launch_gemm256_tn_partials(dy, lddy, x, ldx, work, N, slab, dpart, M, N, K,
+                                                   sp, stream);
+    const long total = (long)M * (N / 4) + (db ? M : 0);
+    long blocks = (total + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, work,
+                       slab, used, dW, lddw, M, N, dpart, db);
+    NF_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const int nkt = (K + BK - 1) / BK;
   if (splits < 1) splits = 1;
   if (splits > nkt) splits = nkt;
@@ -474,4 +501,89 @@ void nf_launch_gemm_tn_masked(const void* dy, long lddy, const void* x, long ldx
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, work,
                      slab, used, dW, lddw, M, N, a.dbias, db);
   NF_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- grouped weight gradients
+// All weight gradients of one conditioner MLP in ONE launch: a common split count S chosen so
+// that S x (sum of tiles) fills one wave of resident blocks (2 per CU). Compared with one
+// launch per layer this cuts the split count (3 vs 8-16 at B = 16384), so each block streams a
+// 3x longer K range and the fp32 slab traffic drops by the same factor.
+static int tn_group_splits(int nprob, const NfTnProblem* pr) {
+  const bool t256 = use_256_tn();
+  const int bm = t256 ? 256 : BM, bn = t256 ? 256 : BN;
+  long tiles = 0;
+  int cap = 1 << 30;
+  for (int p = 0; p < nprob; ++p) {
+    tiles += (long)((pr[p].M + bm - 1) / bm) * ((pr[p].N + bn - 1) / bn);
+    const int c = ((pr[p].K + BK - 1) / BK) / 4;
+    cap = c < cap ? c : cap;
+  }
+  int target = (t256 ? 1 : 2) * device_cus();
+  if (const char* e = getenv("VINF_TN_TARGET_BLOCKS")) target = atoi(e);
+  int S = (int)(target / (tiles > 0 ? tiles : 1));
+  if (S > cap) S = cap;
+  return S < 1 ? 1 : S;
+}
+
+long nf_gemm_tn_group_workspace(int nprob, const NfTnProblem* pr) {
+  const int S = tn_group_splits(nprob, pr);
+  if (S == 1) return 0;
+  long w = 0;
+  for (int p = 0; p < nprob; ++p) w += (long)S * pr[p].M * pr[p].N + (pr[p].db ? (long)S * pr[p].M : 0);
+  return w;
+}
+
+void nf_launch_gemm_tn_group(int nprob, const NfTnProblem* pr, float* work, hipStream_t stream) {
+  if (nprob < 1 || nprob > 4) return;
+  const int S = tn_group_splits(nprob, pr);
+  GroupArgs g{};
+  ReduceGroup r{};
+  g.nprob = nprob;
+  r.nprob = nprob;
+  g.start[0] = 0;
+  r.istart[0] = 0;
+  float* wp = work;
+  for (int p = 0; p < nprob; ++p) {
+    const NfTnProblem& q = pr[p];
+    const int nkt = (q.K + BK - 1) / BK;
+    const int kts = (nkt + S - 1) / S;
+    const int used = (nkt + kts - 1) / kts;
+    GemmArgs& a = g.p[p];
+    a = GemmArgs{};
+    a.A = (const bf16_t*)q.dy; a.lda = q.lddy;
+    a.B = (const bf16_t*)q.x; a.ldb = q.ldx;
+    a.M = q.M; a.N = q.N; a.K = q.K; a.k_per_split = kts * BK;
+    const int tb = use_256_tn() ? 256 : BM;
+    const int tiles = ((q.M + tb - 1) / tb) * ((q.N + tb - 1) / tb);
+    g.start[p + 1] = g.start[p] + tiles * used;
+    if (S == 1 || used == 1) {
+      a.C = q.dW; a.ldc = q.lddw; a.c_split_stride = 0;
+      a.dbias = q.db;
+      r.splits[p] = 0;  // nothing to reduce
+      r.istart[p + 1] = r.istart[p];
+      continue;
+    }
+    const long slab = (long)q.M * q.N;
+    a.C = wp; a.ldc = q.N; a.c_split_stride = slab;
+    a.dbias = q.db ? wp + (long)used * slab : nullptr;
+    r.slabs[p] = wp; r.slab_stride[p] = slab; r.splits[p] = used;
+    r.out[p] = q.dW; r.ld_out[p] = q.lddw; r.rows[p] = q.M; r.cols[p] = q.N;
+    r.dpart[p] = a.dbias; r.db[p] = q.db;
+    r.istart[p + 1] = r.istart[p] + (long)q.M * (q.N / 4) + (q.db ? q.M : 0);
+    wp += (long)S * slab + (q.db ? (long)S * q.M : 0);
+  }
+  if (use_256_tn()) {
+    nf_launch_gemm256_tn_group(g, stream);
+  } else {
+    hipLaunchKernelGGL((gemm_group_kernel<false, false, EPI_F32>), dim3(g.start[nprob]), dim3(NTHR),
+                       0, stream, g);
+    NF_HIP_CHECK(hipGetLastError());
+  }
+  const long total = r.istart[nprob];
+  if (total > 0) {
+    long blocks = (total + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(splitk_reduce_group_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, r);
+    NF_HIP_CHECK(hipGetLastError());
+  }
 }

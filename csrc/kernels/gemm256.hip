@@ -1,0 +1,397 @@
+// 256x256 bf16 MFMA GEMM with the CDNA4 8-phase pipelined schedule (gfx950).
+//
+// Same contract as gemm.hip (C[m][n] = sum_k Aop(m,k) Bop(n,k), fp32 accumulate, fused
+// epilogues), used for the M = batch products of the flow conditioners (forward y = x W^T and
+// input-gradient dx = dy W, M = 16384 per GPU), where the 128x128 two-barrier loop of gemm.hip
+// stalls on the vmcnt(0) its barrier implies (~700 TF at K = 1024).
+//
+// Geometry: 512 threads = 8 waves as 2 (M) x 4 (N); block tile 256x256, BK = 64; each wave owns
+// 128 (M) x 64 (N) = 8 x 4 tiles of v_mfma_f32_16x16x32_bf16 (128 accumulator VGPRs).
+// LDS: 2 K-tile buffers x 4 half-tiles x 16 KiB = 128 KiB (1 block / CU), staged by
+// global_load_lds_dwordx4 (2 per thread per half-tile). A K-tile's operands are split into
+// half-tiles by their *reader*, so each can be restaged as soon as its own readers are done:
+//   A-lo = tile rows {0..63, 128..191}, A-hi = {64..127, 192..255}   (wave row-group wr reads
+//          rows wr*128 + [0..63] from A-lo and wr*128 + [64..127] from A-hi)
+//   B-lo = tile cols {wc*64 + 0..31}, B-hi = {wc*64 + 32..63}
+// Per K-tile, 4 phases, 16 MFMAs (one 64x32 quadrant x K=64) each:
+//   r1: read A-lo (8 frags) + B-lo (4)   mfma M0-3 x N0-1      issue half (t+1, B-hi)
+//   r2: read B-hi (4)                    mfma M0-3 x N2-3      issue half (t+1, A-hi)
+//   r3: read A-hi (8)                    mfma M4-7 x N2-3      issue half (t+2, A-lo)
+//   r4: -                                mfma M4-7 x N0-1      issue half (t+2, B-lo)
+// i.e. half j of K-tile t is issued at global phase 4t - 5 + j (prologue: 6 halves). Every
+// phase ends its read section with a counted `s_waitcnt vmcnt(2*D)` that retires the half
+// issued D phases earlier (never vmcnt(0) in the main loop), then raw s_barrier, lgkmcnt(0),
+// setprio(1) MFMAs setprio(0), s_barrier (CDNA4 guide §5 "The 256^2 8-phase template").
+//   RAW: a half issued at phase q is read at >= q + D + 1 (checked for every half, D = 3, 4).
+//   WAR: a slot is restaged >= 2 phases after its last ds_read (the lgkmcnt(0) that retires a
+//        lagging wave's reads sits one barrier after the issuing barrier).
+// The two wave row-groups run one barrier apart (wr == 1 takes an extra barrier up front), so
+// on each SIMD one wave issues its LDS reads / DMA while the other runs MFMAs.
+#include "gemm_tile.h"
+
+namespace nf {
+namespace gemm {
+namespace g256 {
+
+constexpr int BM = 256, BN = 256, BK = 64, NTHR = 512;
+constexpr int HALF_BYTES = 128 * 64 * 2;  // 16 KiB
+constexpr int BUF_BYTES = 4 * HALF_BYTES;  // A-lo, B-lo, B-hi, A-hi
+constexpr int SMEM_BYTES = 2 * BUF_BYTES;  // 128 KiB
+// slot order inside a buffer == issue order j
+constexpr int H_ALO = 0, H_BLO = 1, H_BHI = 2, H_AHI = 3;
+
+// local row (0..127) of a half-tile -> row of the 256-row block tile
+__device__ __forceinline__ int half_row(bool is_a, bool hi, int lr) {
+  return is_a ? (lr & 63) + ((lr >> 6) << 7) + (hi ? 64 : 0)
+              : ((lr >> 5) << 6) + (lr & 31) + (hi ? 32 : 0);
+}
+
+template <bool KMAJOR>
+__device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long ld, int row0,
+                                           int rows_total, int k0, int K, bool is_a, bool hi,
+                                           char* dst, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int piece = wave * 2 + i;  // 16 x 1 KiB
+    const bf16_t* src;
+    if (KMAJOR) {
+      const int r = piece * 8 + (lane >> 3);
+      const int lc = (lane & 7) ^ (r & 7);
+      int gr = row0 + half_row(is_a, hi, r);
+      gr = gr < rows_total ? gr : rows_total - 1;
+      int gk = k0 + lc * 8;
+      gk = gk < K ? gk : K - 8;
+      src = base + (long)gr * ld + gk;
+    } else {
+      const int kr = piece * 4 + (lane >> 4);
+      const int lc = (lane & 15) ^ mn_swz(kr);
+      int gk = k0 + kr;
+      gk = gk < K ? gk : K - 1;
+      int gm = row0 + half_row(is_a, hi, lc * 8);
+      gm = gm < rows_total ? gm : rows_total - 8;
+      src = base + (long)gk * ld + gm;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(dst + piece * 1024), 16, 0,
+                                     0);
+  }
+}
+
+__device__ __forceinline__ void barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int N>
+__device__ __forceinline__ void vmwait() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
+// retire every half issued at phase <= P - D; `cnt` = valid halves issued in (P - D, P]
+template <int D>
+__device__ __forceinline__ void vmwait_count(int cnt) {
+  if (cnt >= D) vmwait<2 * D>();
+  else if (cnt == 3) vmwait<6>();
+  else if (cnt == 2) vmwait<4>();
+  else if (cnt == 1) vmwait<2>();
+  else vmwait<0>();
+}
+
+// sum of the 8 bf16 of a fragment (fp32)
+__device__ __forceinline__ float frag_sum(v8s f) {
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s += __uint_as_float(((unsigned)(unsigned short)f[e]) << 16);
+  return s;
+}
+
+template <bool A_KMAJOR, bool B_KMAJOR, int EPI, int D, bool DB>
+__device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int split, char* smem) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int ntn = (a.N + BN - 1) / BN;
+  const int tm = wg / ntn, tn = wg % ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  int kbeg = split * a.k_per_split;
+  int kend = kbeg + a.k_per_split;
+  kend = kend < a.K ? kend : a.K;
+  const int nkt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  v4f acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+  // bias gradient db[m] = sum_k Aop(m,k) (weight-gradient launches): VALU sums of the A
+  // fragments the wc == 0 waves of the tn == 0 blocks already hold, overlapping the MFMAs
+  const bool do_db = DB && a.dbias != nullptr && tn == 0 && wc == 0;
+  float dba[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dba[j] = 0.f;
+
+  // issue half j of K-tile t (no-op past the end)
+  auto issue = [&](int t, int j) {
+    if (t >= nkt) return;
+    char* dst = smem + (t & 1) * BUF_BYTES + j * HALF_BYTES;
+    const int k0 = kbeg + t * BK;
+    if (j == H_ALO || j == H_AHI)
+      stage_half<A_KMAJOR>(a.A, a.lda, m0, a.M, k0, kend, true, j == H_AHI, dst, wave, lane);
+    else
+      stage_half<B_KMAJOR>(a.B, a.ldb, n0, a.N, k0, kend, false, j == H_BHI, dst, wave, lane);
+  };
+  // valid halves issued at global phases (P - D, P]; half (t, j) is issued at 4t - 5 + j
+  auto outstanding = [&](int P) {
+    int hi = P < 4 * nkt - 6 ? P : 4 * nkt - 6;
+    int c = hi - (P - D);
+    return c < 0 ? 0 : (c > D ? D : c);
+  };
+
+  if (nkt > 0) {
+    issue(0, H_ALO); issue(0, H_BLO); issue(0, H_BHI); issue(0, H_AHI);
+    issue(1, H_ALO); issue(1, H_BLO);
+    vmwait_count<D>(outstanding(0));
+    barrier();
+    if (wr == 1) barrier();
+
+    v8s fa[4][2], fbl[2][2], fbh[2][2];
+    for (int t = 0; t < nkt; ++t) {
+      const char* buf = smem + (t & 1) * BUF_BYTES;
+      const bool two = (kend - (kbeg + t * BK)) > 32;
+      const int P = 4 * t;
+      // ---- r1: M0-3 x N0-1
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          fbl[i][ks] = read_frag<B_KMAJOR>(buf + H_BLO * HALF_BYTES, wc * 32 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          fa[j][ks] = read_frag<A_KMAJOR>(buf + H_ALO * HALF_BYTES, wr * 64 + j * 16, ks, lane);
+      issue(t + 1, H_BHI);
+      vmwait_count<D>(outstanding(P + 1));
+      barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        if (ks == 0 || two)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbl[i][ks], fa[j][ks], acc[i][j],
+                                                                  0, 0, 0);
+      if (do_db)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dba[j] += frag_sum(fa[j][0]) + (two ? frag_sum(fa[j][1]) : 0.f);
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+      // ---- r2: M0-3 x N2-3
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          fbh[i][ks] = read_frag<B_KMAJOR>(buf + H_BHI * HALF_BYTES, wc * 32 + i * 16, ks, lane);
+      issue(t + 1, H_AHI);
+      vmwait_count<D>(outstanding(P + 2));
+      barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        if (ks == 0 || two)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[2 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbh[i][ks], fa[j][ks],
+                                                                      acc[2 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+      // ---- r3: M4-7 x N2-3
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          fa[j][ks] = read_frag<A_KMAJOR>(buf + H_AHI * HALF_BYTES, wr * 64 + j * 16, ks, lane);
+      issue(t + 2, H_ALO);
+      vmwait_count<D>(outstanding(P + 3));
+      barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        if (ks == 0 || two)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[2 + i][4 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  fbh[i][ks], fa[j][ks], acc[2 + i][4 + j], 0, 0, 0);
+      if (do_db)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          dba[4 + j] += frag_sum(fa[j][0]) + (two ? frag_sum(fa[j][1]) : 0.f);
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+      // ---- r4: M4-7 x N0-1 (no LDS reads)
+      issue(t + 2, H_BLO);
+      vmwait_count<D>(outstanding(P + 4));
+      barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        if (ks == 0 || two)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][4 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbl[i][ks], fa[j][ks],
+                                                                      acc[i][4 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+    }
+    if (wr == 0) barrier();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  // acc[i][j]: n = n0 + wc*64 + i*16 + (lane>>4)*4 + r, m = m0 + wr*128 + j*16 + (lane&15)
+  const int g = lane >> 4, c = lane & 15;
+  if (do_db) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = dba[j];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      const int m = m0 + wr * 128 + j * 16 + c;
+      if (g == 0 && m < a.M) a.dbias[(long)split * a.M + m] = v;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int m = m0 + wr * 128 + j * 16 + c;
+    if (m >= a.M) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + wc * 64 + i * 16 + g * 4;
+      if (n >= a.N) continue;
+      epi_store<EPI>(a, acc[i][j], m, n, split);
+    }
+  }
+}
+
+template <bool A_KMAJOR, bool B_KMAJOR, int EPI, int D, bool DB>
+__global__ void __launch_bounds__(NTHR, 1) gemm256_kernel(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  gemm256_body<A_KMAJOR, B_KMAJOR, EPI, D, DB>(a, xcd_remap(blockIdx.x, ntm * ntn), blockIdx.y,
+                                                smem);
+}
+
+// grouped weight gradients (same block layout as gemm.hip's gemm_group_kernel)
+template <int D>
+__global__ void __launch_bounds__(NTHR, 1) gemm256_group_kernel(GroupArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+  const int id = xcd_remap(blockIdx.x, g.start[g.nprob]);
+  int p = 0;
+#pragma unroll
+  for (int q = 1; q < 4; ++q)
+    if (q < g.nprob && id >= g.start[q]) p = q;
+  const GemmArgs& a = g.p[p];
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  const int local = id - g.start[p];
+  gemm256_body<false, false, EPI_F32, D, true>(a, local % tiles, local / tiles, smem);
+}
+
+static int g_depth = 4;
+
+template <bool AK, bool BK_, int EPI, bool DB = false>
+void launch(const GemmArgs& a, int splits, hipStream_t stream) {
+  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  dim3 grid(ntm * ntn, splits), block(NTHR);
+  if (g_depth == 4)
+    hipLaunchKernelGGL((gemm256_kernel<AK, BK_, EPI, 4, DB>), grid, block, 0, stream, a);
+  else
+    hipLaunchKernelGGL((gemm256_kernel<AK, BK_, EPI, 3, DB>), grid, block, 0, stream, a);
+  NF_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace g256
+}  // namespace gemm
+}  // namespace nf
+
+using namespace nf::gemm;
+
+void nf_gemm256_set_depth(int d) { g256::g_depth = d == 3 ? 3 : 4; }
+
+// y[M][N] = act(x[M][K] W[N][K]^T + bias) -> bf16
+void nf_launch_gemm256_nt(const void* x, long ldx, const void* W, long ldw, const void* bias,
+                          void* y, long ldy, int M, int N, int K, int relu, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  GemmArgs a{};
+  a.A = (const nf::bf16_t*)x; a.lda = ldx;
+  a.B = (const nf::bf16_t*)W; a.ldb = ldw;
+  a.C = y; a.ldc = ldy;
+  a.bias = (const nf::bf16_t*)bias;
+  a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + 63) / 64) * 64; a.relu = relu;
+  g256::launch<true, true, EPI_BF16>(a, 1, stream);
+}
+
+// dx[M][N] = dy[M][K] W[K][N]  (* 1(aux>0) -> bf16)  or  fp32 dx (+)= ...
+void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, const void* aux,
+                          long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
+                          int N, int K, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  GemmArgs a{};
+  a.A = (const nf::bf16_t*)dy; a.lda = lddy;
+  a.B = (const nf::bf16_t*)W; a.ldb = ldw;
+  a.C = dx; a.ldc = lddx;
+  a.aux = (const nf::bf16_t*)aux; a.ld_aux = ld_aux;
+  a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + 63) / 64) * 64;
+  if (dx_is_f32) {
+    if (accumulate) g256::launch<true, false, EPI_F32_ACC>(a, 1, stream);
+    else g256::launch<true, false, EPI_F32>(a, 1, stream);
+  } else if (aux) {
+    g256::launch<true, false, EPI_BF16_RELUMASK>(a, 1, stream);
+  } else {
+    g256::launch<true, false, EPI_BF16>(a, 1, stream);
+  }
+}
+
+// dW[M][N] (+ db[M]) = split-K partials of dy[K][M]^T x[K][N] written to `work` slabs (or
+// straight to dW/db when splits == 1); the caller reduces them (gemm.hip).
+int nf_launch_gemm256_tn_partials(const void* dy, long lddy, const void* x, long ldx, float* C,
+                                  long ldc, long slab_stride, float* dbias, int M, int N, int K,
+                                  int splits, hipStream_t stream) {
+  const int nkt = (K + 63) / 64;
+  if (splits < 1) splits = 1;
+  if (splits > nkt) splits = nkt;
+  const int kts = (nkt + splits - 1) / splits;
+  const int used = (nkt + kts - 1) / kts;
+  GemmArgs a{};
+  a.A = (const nf::bf16_t*)dy; a.lda = lddy;
+  a.B = (const nf::bf16_t*)x; a.ldb = ldx;
+  a.C = C; a.ldc = ldc; a.c_split_stride = slab_stride;
+  a.dbias = dbias;
+  a.M = M; a.N = N; a.K = K; a.k_per_split = kts * 64;
+  g256::launch<false, false, EPI_F32, true>(a, used, stream);
+  return used;
+}
+
+void nf_launch_gemm256_tn_group(const GroupArgs& g, hipStream_t stream) {
+  if (g256::g_depth == 3)
+    hipLaunchKernelGGL(g256::gemm256_group_kernel<3>, dim3(g.start[g.nprob]), dim3(g256::NTHR), 0,
+                       stream, g);
+  else
+    hipLaunchKernelGGL(g256::gemm256_group_kernel<4>, dim3(g.start[g.nprob]), dim3(g256::NTHR), 0,
+                       stream, g);
+  NF_HIP_CHECK(hipGetLastError());
+}

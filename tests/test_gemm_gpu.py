@@ -97,3 +97,90 @@ def test_engine_mfma_backend_matches_blas(gpu):
     assert abs(res["blas"][0] - res["mfma"][0]) < 1e-2 * (1 + abs(res["blas"][0]))
     g0, g1 = res["blas"][1], res["mfma"][1]
     assert (g0 - g1).abs().max() <= 3e-2 * g0.abs().max()
+
+
+# ---------------------------------------------------------------- 256x256 8-phase kernel
+@pytest.fixture(params=[3, 4], ids=["d3", "d4"])
+def tile256(request, gpu):
+    torch.ops.vinf.gemm_set_mode(2, request.param)   # force the 256x256 kernel
+    yield request.param
+    torch.ops.vinf.gemm_set_mode(0, 4)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 8, 32), (300, 800, 416), (1000, 1024, 96),
+                                   (16384, 1024, 1024), (512, 416, 1024), (2048, 256, 4096)])
+def test_gemm256_nt(gpu, tile256, M, N, K):
+    torch.manual_seed(M + N + K)
+    x, W, b = _bf(M, K, device=gpu), _bf(N, K, device=gpu, scale=0.05), _bf(N, device=gpu)
+    y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    torch.ops.vinf.gemm_nt(x, W, b, y, 1)
+    _check(y, (x.float() @ W.float().t() + b.float()).clamp_min(0), 1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 1024, 1024), (300, 416, 1024), (16384, 1024, 800),
+                                   (520, 8, 32), (1000, 1024, 96)])
+def test_gemm256_nn(gpu, tile256, M, N, K):
+    torch.manual_seed(1)
+    dy, W, h = _bf(M, K, device=gpu), _bf(K, N, device=gpu, scale=0.05), _bf(M, N, device=gpu)
+    dx = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    torch.ops.vinf.gemm_nn(dy, W, h, dx, False)
+    _check(dx, (dy.float() @ W.float()) * (h.float() > 0), 1e-2)
+    base = torch.randn(M, N, device=gpu)
+    dxf = base.clone()
+    torch.ops.vinf.gemm_nn(dy, W, None, dxf, True)
+    _check(dxf, dy.float() @ W.float() + base, 2e-2)
+
+
+def test_gemm256_repeatable(gpu, tile256):
+    """Race screen: the same product 20x must be bitwise identical (LDS-DMA RAW/WAR schedule)."""
+    torch.manual_seed(5)
+    x, W = _bf(8192, 1024, device=gpu), _bf(1024, 1024, device=gpu, scale=0.05)
+    y0 = torch.empty(8192, 1024, device=gpu, dtype=torch.bfloat16)
+    torch.ops.vinf.gemm_nt(x, W, None, y0, 0)
+    _check(y0, x.float() @ W.float().t(), 1e-2)
+    y = torch.empty_like(y0)
+    for _ in range(20):
+        torch.ops.vinf.gemm_nt(x, W, None, y, 0)
+        assert torch.equal(y, y0)
+
+
+@pytest.mark.parametrize("K,M,N", [(64, 1024, 416), (96, 256, 256), (16384, 1024, 1024),
+                                   (16384, 800, 1024), (4096, 1024, 416), (8192, 8, 40),
+                                   (2080, 520, 264)])
+@pytest.mark.parametrize("with_db", [True, False])
+def test_gemm256_tn_wgrad(gpu, K, M, N, with_db):
+    torch.ops.vinf.gemm_set_mode(3, 3)
+    try:
+        torch.manual_seed(3)
+        dy, x = _bf(K, M, device=gpu), _bf(K, N, device=gpu)
+        dW = torch.full((M, N), 7.0, device=gpu)
+        db = torch.full((M,), 7.0, device=gpu) if with_db else None
+        torch.ops.vinf.gemm_tn(dy, x, dW, db)
+        _check(dW, dy.float().t() @ x.float(), 1e-4)
+        if with_db:
+            _check(db, dy.float().sum(0), 1e-4)
+    finally:
+        torch.ops.vinf.gemm_set_mode(0, 4)
+
+
+@pytest.mark.parametrize("mode", [0, 3], ids=["auto", "t256"])
+@pytest.mark.parametrize("B", [16384, 4096, 96])
+def test_gemm_tn_group(gpu, B, mode):
+    """Grouped weight gradients (one launch) == per-problem references, with and without db."""
+    torch.ops.vinf.gemm_set_mode(mode, 4)
+    torch.manual_seed(4)
+    shapes = [(800, 1024), (1024, 1024), (1024, 416)]
+    items, refs = [], []
+    for p, (M, N) in enumerate(shapes):
+        dy, x = _bf(B, M, device=gpu), _bf(B, N, device=gpu)
+        dW = torch.full((M, N), 3.0, device=gpu)
+        db = torch.full((M,), 3.0, device=gpu) if p != 1 else None
+        items.append((dy, x, dW, db))
+        refs.append((dy.float().t() @ x.float(), dy.float().sum(0)))
+    torch.ops.vinf.gemm_tn_group([i[0] for i in items], [i[1] for i in items],
+                                 [i[2] for i in items], [i[3] for i in items])
+    torch.ops.vinf.gemm_set_mode(0, 4)
+    for (dy, x, dW, db), (rW, rb) in zip(items, refs):
+        _check(dW, rW, 1e-4)
+        if db is not None:
+            _check(db, rb, 1e-4)

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--only", default=None, help="comma-separated shape names")
     ap.add_argument("--mine-only", action="store_true", help="skip the hipBLASLt reference")
+    ap.add_argument("--modes", default=None,
+                    help="compare kernel choices, e.g. 128,256d3,256d4 (M = batch products)")
     a = ap.parse_args()
     ops = native()
     dev = torch.device("cuda")
@@ -44,6 +46,7 @@ def main():
               ("dgrad_l1", "nn_f32acc", B, 416, 1024),
               ("wgrad_l3", "tn", 800, 1024, B), ("wgrad_l2", "tn", 1024, 1024, B),
               ("wgrad_l1", "tn", 1024, 416, B),
+              ("wgrad_group", "tn_group", 0, 0, B),
               ("sq4096", "nt", 4096, 4096, 4096), ("fwd_k4096", "nt", B, 1024, 4096),
               ("fwd_k2048", "nt", B, 1024, 2048), ("fwd_m64k", "nt", 65536, 1024, 1024)]
     if a.only:
@@ -70,6 +73,18 @@ def main():
                 y = torch.zeros(M, N, device=dev)
                 mine = lambda: ops.gemm_nn(dy, W, None, y, True)
                 ref = lambda: y.add_(torch.mm(dy, W, out_dtype=torch.float32))
+        elif kind == "tn_group":   # the three weight gradients of one conditioner
+            its = []
+            for (m_, n_) in [(800, 1024), (1024, 1024), (1024, 416)]:
+                its.append((torch.randn(K, m_, device=dev).to(bf), torch.randn(K, n_, device=dev).to(bf),
+                            torch.empty(m_, n_, device=dev), torch.empty(m_, device=dev)))
+            M, N = 1, 800 * 1024 + 1024 * 1024 + 1024 * 416
+            mine = lambda: ops.gemm_tn_group([i[0] for i in its], [i[1] for i in its],
+                                             [i[2] for i in its], [i[3] for i in its])
+
+            def ref():
+                for i in its:
+                    ops.gemm_tn(*i)
         else:
             dy = torch.randn(K, M, device=dev).to(bf)
             x = torch.randn(K, N, device=dev).to(bf)
@@ -81,6 +96,21 @@ def main():
                 dW.copy_(torch.mm(dy.t(), x, out_dtype=torch.float32))
                 torch.sum(dy, 0, dtype=torch.float32, out=db)
         flops = 2.0 * M * N * K
+        if a.modes:
+            res = {m: [] for m in a.modes.split(",")}
+            for _ in range(3):
+                for m in res:
+                    mode = 1 if m == "128" else (3 if m.startswith("256t") else
+                                                 (2 if m.startswith("256") else 0))
+                    ops.gemm_set_mode(mode, 3 if m.endswith("d3") else 4)
+                    res[m].append(_time(mine, a.iters))
+            ops.gemm_set_mode(0, 4)
+            rec = {"shape": name, "M": M, "N": N, "K": K}
+            for m, ts in res.items():
+                rec[f"{m}_us"] = round(min(ts) * 1e6, 1)
+                rec[f"{m}_tflops"] = round(flops / min(ts) / 1e12, 1)
+            print(json.dumps(rec), flush=True)
+            continue
         tm, tr = [], []
         for _ in range(3):
             tm.append(_time(mine, a.iters))

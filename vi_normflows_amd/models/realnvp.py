@@ -154,7 +154,9 @@ class RealNVPVI:
         self.S = torch.empty(L, B, Dh, dtype=f32, device=dev)
         self.st = torch.empty(B, Np, dtype=self.cdt, device=dev)
         self.dst = torch.empty(B, Np, dtype=self.cdt, device=dev)
-        self.dH = [torch.empty(B, H, dtype=self.cdt, device=dev) for _ in range(2)]
+        # one input-gradient buffer per hidden layer: the grouped weight-gradient launch at the
+        # end of each layer's backward reads all of them
+        self.dH = [torch.empty(B, H, dtype=self.cdt, device=dev) for _ in range(max(cfg.n_hidden, 1))]
         self._G = torch.zeros(L + 2, B, Dp, dtype=f32, device=dev)   # dL/dh_i, 0-padded rows
         self.G = self._G[:, :, :Dh]
         self.logq0 = torch.empty(B, dtype=f32, device=dev)
@@ -295,15 +297,18 @@ class RealNVPVI:
             fused.coupling_bwd(self.G[l + 2], self.S[l], self.h(l), self.dst, self.G[l], c=c,
                                scale=cfg.scale_bound, gx_accumulate=False)
             d = self.dst
+            wg = []
             for i in range(nh, -1, -1):
                 inp = self.Act[l, i - 1] if i > 0 else self.Hbf[l]
-                gemm.linear_wgrad(d, inp, P.g(f"l{l}.W{i}"), P.g(f"l{l}.b{i}"))
+                wg.append((d, inp, P.g(f"l{l}.W{i}"), P.g(f"l{l}.b{i}")))
                 if i > 0:
-                    nd = self.dH[i % 2]
+                    nd = self.dH[i - 1]
                     gemm.linear_dgrad(d, P.c(f"l{l}.W{i}"), nd, relu_of=self.Act[l, i - 1])
                     d = nd
                 else:
                     gemm.linear_dgrad(d, P.c(f"l{l}.W0"), self._G[l + 1], accumulate=True)
+            # the layer's weight gradients after its input-gradient chain: one grouped launch
+            gemm.linear_wgrad_group(wg)
             if self.unit_ready_hook is not None:
                 self.unit_ready_hook(l + 1)
         self._base_backward()

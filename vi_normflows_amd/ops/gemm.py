@@ -74,6 +74,27 @@ def linear_dgrad(dy: torch.Tensor, W: torch.Tensor, out: torch.Tensor,
     return out
 
 
+def linear_wgrad_group(items) -> None:
+    """Several weight gradients at once: ``items`` = [(dy, x, dW, db), ...] (<= 4).
+
+    On the MFMA backend this is ONE grouped split-K launch + one reduce launch
+    (csrc/kernels/gemm.hip ``nf_launch_gemm_tn_group``): all layers of a conditioner share a
+    small split count, so every block streams a long K range; elsewhere a loop of
+    :func:`linear_wgrad`.
+    """
+    items = list(items)
+    if items and all(_mfma_ok(dy) and dy.is_cuda for dy, _, _, _ in items):
+        from ._ext import native
+
+        for c in range(0, len(items), 4):
+            ch = items[c:c + 4]
+            native().gemm_tn_group([i[0] for i in ch], [i[1] for i in ch], [i[2] for i in ch],
+                                   [i[3] for i in ch])
+        return
+    for dy, x, dW, db in items:
+        linear_wgrad(dy, x, dW, db)
+
+
 def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dW: torch.Tensor,
                  db: torch.Tensor | None) -> None:
     """dW = dy^T x and db = sum_rows(dy), both written in dW/db's dtype (fp32)."""
