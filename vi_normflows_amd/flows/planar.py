@@ -43,7 +43,10 @@ def get_uhat(u, w, norm: str = "sq"):
     wu = (w * u).sum(-1, keepdim=True)
     nw = (w * w).sum(-1, keepdim=True)
     denom = nw if norm == "sq" else torch.sqrt(nw)
-    return u + (m(wu) - wu) * w / denom
+    # w = 0: the flow is a translation by u tanh(b), invertible for any u -> u_hat = u
+    # (the reference app guards this case, app/js/flows.js:41-42; flows.py:39 divides by zero)
+    safe = torch.where(nw > 0, denom, torch.ones_like(denom))
+    return u + torch.where(nw > 0, (m(wu) - wu) / safe, torch.zeros_like(wu)) * w
 
 
 def planar_flow(z, w, u, b, h=torch.tanh, variant: str = "paper", uhat_norm: str = "sq"):
