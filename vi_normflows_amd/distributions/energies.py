@@ -146,6 +146,36 @@ def gaussian(dim: int, scale: float = 0.7, mean: float = 0.0):
     return f
 
 
+def planar_pushforward(w=(-5.0, 1.0), u=(-2.0, 1.0), b: float = 0.0):
+    """Exact density of y = z + u_hat tanh(w^T z + b), z ~ N(0, I): the known flow that
+    ``src/learning_basic_flow.py:18-20`` asks a planar flow to recover (w = [-5, 1],
+    u = [-2, 1]). The reference evaluates the log-det at y instead of at the preimage; here
+    the preimage is solved exactly: s = w^T z is the unique root of s + c tanh(s + b) = w^T y
+    (c = w^T u_hat >= -1 makes it monotone), z = y - u_hat tanh(s + b), and
+    log p(y) = log N(z) - log|1 + c (1 - tanh^2(s + b))|  (normalised: log Z = 0)."""
+    from ..flows.planar import get_uhat
+
+    wt = torch.tensor(w, dtype=torch.float64)
+    uh = get_uhat(torch.tensor(u, dtype=torch.float64)[None], wt[None])[0]
+    c = float(wt @ uh)
+
+    def f(y):
+        yd = y.double()
+        wy = yd @ wt.to(yd.device)
+        lo, hi = wy - abs(c) - 1.0, wy + abs(c) + 1.0
+        for _ in range(80):  # bisection on the monotone scalar equation
+            mid = 0.5 * (lo + hi)
+            g = mid + c * torch.tanh(mid + b) - wy
+            lo = torch.where(g < 0, mid, lo)
+            hi = torch.where(g < 0, hi, mid)
+        s_ = 0.5 * (lo + hi)
+        th = torch.tanh(s_ + b)
+        z = yd - th[:, None] * uh.to(yd.device)
+        lp = -0.5 * (z * z).sum(1) - y.shape[1] * 0.5 * LOG2PI - torch.log(torch.abs(1 + c * (1 - th * th)))
+        return lp.to(y.dtype)
+    return f
+
+
 def get_target(name: str, dim: int | None = None, **kw) -> Target:
     """Targets by name (reference aliases p1..p4, gmm, trial1 accepted)."""
     n = name.lower()
@@ -169,6 +199,8 @@ def get_target(name: str, dim: int | None = None, **kw) -> Target:
         return Target("gmm1d_final", 1, gmm1d([0.3, 0.7], [-1.5, 1.5], [1, 1]), logZ=0.0)
     if n == "gmm1d_wide":  # "Final (master).ipynb" cell 22
         return Target("gmm1d_wide", 1, gmm1d([0.3, 0.7], [-3, 3], [1, 1]), logZ=0.0, grid=(-9, 9))
+    if n in ("planar_pushforward", "basic_flow"):
+        return Target("planar_pushforward", 2, planar_pushforward(**kw), logZ=0.0, grid=(-8, 8))
     if n == "banana":
         d = dim or 784
         return Target("banana", d, banana(d, **kw), logZ=0.0)

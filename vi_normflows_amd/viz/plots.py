@@ -158,8 +158,10 @@ def plot_flow_panels(target, base_samples, flow, lims=(-4, 4), n=100, path=None)
     sc = axs[3].scatter(zK[:, 0], zK[:, 1], c=np.exp(lq), s=3, cmap="viridis")
     axs[3].set_title("q_K density at samples")
     fig.colorbar(sc, ax=axs[3])
-    if hasattr(flow, "hyperplanes"):
-        W, B = flow.hyperplanes()
+    hp = getattr(flow, "hyperplanes", None) or next(
+        (f.hyperplanes for f in getattr(flow, "flows", []) if hasattr(f, "hyperplanes")), None)
+    if hp is not None:
+        W, B = hp()
         xs = np.linspace(lims[0], lims[1], 10)
         for w, b in zip(_np(W), _np(B)):
             if abs(w[1]) > 1e-6:
