@@ -90,3 +90,37 @@ def test_bucket_layout_reverse_order_and_contiguous():
     assert starts == sorted(starts, reverse=True)
     total = sum(b.numel for b in red.buckets)
     assert total == eng.layout.total
+
+
+def _fault_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      VINF_FAULT_STEP="2", VINF_FAULT_RANK="0", VINF_FAULT_KIND="nan")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from vi_normflows_amd.parallel.dist import DistInfo
+    from vi_normflows_amd.parallel.runner import DataParallelRunner
+
+    eng = RealNVPVI(RealNVPConfig(**CFG), batch=B, device="cpu", seed=100 + rank, rank=rank)
+    run = DataParallelRunner(eng, DistInfo(rank=rank, world=world, backend="gloo"), bucket_cap_mb=0.001)
+    snaps = []
+    for _ in range(4):
+        run.step()
+        snaps.append(eng.params.master.clone())
+    torch.save({"snaps": torch.stack(snaps), "skipped": eng.n_skipped.clone()},
+               os.path.join(out_dir, f"f{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_injected_nan_on_one_rank_skips_step_on_all(tmp_path):
+    """a non-finite gradient on ONE rank (fault injection, step 2, rank 0) reaches
+    every rank through the bucketed all-reduce; the guard skips that step everywhere, the
+    replicas stay bitwise identical and training continues."""
+    world = 2
+    mp.spawn(_fault_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    f0 = torch.load(tmp_path / "f0.pt", weights_only=True)
+    f1 = torch.load(tmp_path / "f1.pt", weights_only=True)
+    assert f0["skipped"].item() == 1.0 and f1["skipped"].item() == 1.0
+    assert torch.equal(f0["snaps"], f1["snaps"])
+    assert torch.equal(f0["snaps"][2], f0["snaps"][1])        # step 2 skipped
+    assert not torch.equal(f0["snaps"][3], f0["snaps"][2])    # training continued
+    assert torch.isfinite(f0["snaps"]).all()

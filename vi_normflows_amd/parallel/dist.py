@@ -58,6 +58,17 @@ def init(backend: str | None = None, device_type: str | None = None) -> DistInfo
         kw = {}
         if backend == "nccl":
             kw["device_id"] = device
+        if "TORCHELASTIC_RESTART_COUNT" in os.environ:
+            # under torchrun: key the rendezvous by restart attempt, so a job restarted by
+            # --max-restarts never reads the dead attempt's peer addresses from the store
+            from datetime import timedelta
+
+            agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True"
+            store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
+                                  is_master=(rank == 0 and not agent), timeout=timedelta(seconds=300),
+                                  wait_for_workers=False)
+            store = dist.PrefixStore(f"vinf/attempt_{os.environ['TORCHELASTIC_RESTART_COUNT']}", store)
+            kw["store"] = store
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     _INFO = DistInfo(rank=rank, local_rank=local, world=world,
                      backend=backend if world > 1 else "none", device=device)

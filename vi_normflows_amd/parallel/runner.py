@@ -16,6 +16,7 @@ import os
 import torch
 import torch.distributed as dist
 
+from ..utils import faults
 from .dist import DistInfo
 from .reducer import BucketedAllReduce
 
@@ -27,6 +28,7 @@ class DataParallelRunner:
         self.info = info
         self.graph = None
         self.reducer = None
+        self._t = int(engine.step_t.item())   # host step counter (fault injection only)
         if info.world > 1:
             P = engine.params
             dist.broadcast(P.master, 0)
@@ -38,11 +40,32 @@ class DataParallelRunner:
             engine.unit_ready_hook = self.reducer.mark_ready
 
     def _eager_step(self):
+        kind = faults.armed(self._t, self.info.rank)
+        self._t += 1
+        poison = kind in ("nan", "inf")
+        grad = self.engine.params.grad
         if self.reducer is not None:
             self.reducer.start_step()
-            self.engine.train_step(reduce_fn=self.reducer.finish)
+            if poison:
+                # inject into this rank's first-ready gradient slice BEFORE its bucket is
+                # reduced: the all-reduce spreads it to every rank, so all ranks skip
+                mark = self.reducer.mark_ready
+                ranges = self.engine.layout.unit_ranges
+
+                def hook(u, _mark=mark):
+                    if self.engine.unit_ready_hook is hook:
+                        faults.maybe_inject(self._t - 1, self.info.rank, grad[ranges[u][0]:ranges[u][1]])
+                        self.engine.unit_ready_hook = _mark
+                    _mark(u)
+
+                self.engine.unit_ready_hook = hook
+            try:
+                self.engine.train_step(reduce_fn=self.reducer.finish)
+            finally:
+                self.engine.unit_ready_hook = self.reducer.mark_ready
         else:
-            self.engine.train_step()
+            fn = (lambda: faults.maybe_inject(self._t - 1, self.info.rank, grad)) if poison else None
+            self.engine.train_step(reduce_fn=fn)
 
     def capture(self, warmup: int = 2) -> bool:
         """Capture one training step into a hipGraph. Returns False if capture is unsupported."""

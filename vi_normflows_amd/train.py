@@ -14,6 +14,7 @@ from __future__ import annotations
 import argparse
 import json
 import math
+import os
 import time
 from pathlib import Path
 
@@ -21,6 +22,7 @@ import torch
 
 from .parallel import dist as vdist
 from .utils.config import load, rank_seed
+from .utils.faults import maybe_inject
 from .utils.metrics import JsonlLogger, append_free_energy
 
 
@@ -60,14 +62,23 @@ def run_realnvp(cfg, out, info, logger):
                        if cfg.schedule in ("reference", "none") else "reference",
                        anneal_iters=cfg.iters)
     eng = RealNVPVI(rc, batch=cfg.batch, device=dev, seed=cfg.seed, rank=info.rank, lr=cfg.lr)
+    ckpt = out / "ckpt.pt"
     if cfg.extra.get("resume"):
         load_engine(eng, cfg.extra["resume"], info.rank)
+    elif cfg.extra.get("auto_resume", True) and ckpt.exists():
+        # elastic-lite: a job restarted by torchrun --max-restarts continues from its last
+        # checkpoint (every rank reads the shared state + its own RNG stream)
+        load_engine(eng, ckpt, info.rank)
+        if info.is_main:
+            print(f"[train] resumed from {ckpt} at step {int(eng.step_t.item())}", flush=True)
     run = DataParallelRunner(eng, info)
-    if dev.type == "cuda" and cfg.extra.get("graph", True):
+    fault = os.environ.get("VINF_FAULT_STEP") is not None
+    if dev.type == "cuda" and cfg.extra.get("graph", True) and not fault:
         run.capture(warmup=1)
     t0 = time.perf_counter()
     start = int(eng.step_t.item())
     for t in range(start, cfg.iters):
+        maybe_inject(t, info.rank)
         run.step()
         if t % cfg.log_every == 0 or t == cfg.iters - 1:
             F = float(eng.loss.item())
@@ -77,8 +88,10 @@ def run_realnvp(cfg, out, info, logger):
                         "skipped": float(eng.n_skipped.item()),
                         "samples_per_s": (t - start + 1) * cfg.batch * info.world / el})
         if cfg.ckpt_every and (t + 1) % cfg.ckpt_every == 0:
-            save_engine(eng, out / "ckpt.pt", info.rank)
-    save_engine(eng, out / "ckpt.pt", info.rank)
+            save_engine(eng, ckpt, info.rank)
+            vdist.barrier()   # the checkpoint is complete on every rank before anyone moves on
+    save_engine(eng, ckpt, info.rank)
+    vdist.barrier()
     return {"free_energy": float(eng.loss.item()), "steps": cfg.iters,
             "skipped_steps": float(eng.n_skipped.item())}
 

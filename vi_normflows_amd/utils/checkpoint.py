@@ -37,7 +37,7 @@ def save_engine(engine, path, rank: int = 0, extra: dict | None = None) -> None:
         if extra:
             payload["extra"] = extra
         atomic_save(payload, path)
-    atomic_save({"rng_offset": sd["rng_offset"], "rank": rank,
+    atomic_save({"rng_offset": sd["rng_offset"], "rank": rank, "step": sd.get("step"),
                  "torch_rng": torch.get_rng_state()}, f"{path}.rank{rank}.rng")
 
 
@@ -47,8 +47,14 @@ def load_engine(engine, path, rank: int = 0) -> dict:
     rng_path = f"{path}.rank{rank}.rng"
     if os.path.exists(rng_path):
         r = safe_load(rng_path)
-        engine.rng_offset.copy_(r["rng_offset"])
-        torch.set_rng_state(r["torch_rng"])
+        # a crash between rank 0's write and this rank's can leave an RNG file from another
+        # step: only a file from the same step is used (the counter-based streams are a
+        # function of the step anyway)
+        st = payload["engine"].get("step")
+        if r.get("step") is None or st is None or torch.equal(torch.as_tensor(r["step"]).cpu(),
+                                                              torch.as_tensor(st).cpu()):
+            engine.rng_offset.copy_(r["rng_offset"])
+            torch.set_rng_state(r["torch_rng"])
     return payload.get("extra", {})
 
 
