@@ -61,3 +61,16 @@ def test_fault_arming():
     finally:
         for k in ("VINF_FAULT_STEP", "VINF_FAULT_RANK", "VINF_FAULT_KIND", "TORCHELASTIC_RESTART_COUNT"):
             os.environ.pop(k, None)
+
+
+def test_allreduce_bench_world2():
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "vi_normflows_amd.bench.allreduce",
+           "--backend", "gloo", "--sizes-mb", "1,2", "--iters", "3", "--warmup", "1"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    import json
+
+    recs = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(recs) == 2 and all(r["world"] == 2 and r["busbw_GBps"] > 0 for r in recs)

@@ -196,3 +196,14 @@ def test_viz_smoke(tmp_path):
     plot_flow_panels(t, torch.randn(100, 2), f, path=tmp_path / "b.png")
     plot_free_energy_vs_K({1: 3.0, 2: 2.0, 4: 1.5}, path=tmp_path / "c.png", floor=-2.08)
     assert all((tmp_path / n).exists() for n in ("a.png", "b.png", "c.png"))
+
+
+def test_profiling_hooks(tmp_path):
+    from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI
+    from vi_normflows_amd.utils import profiling
+
+    e = RealNVPVI(RealNVPConfig(dim=6, n_layers=2, hidden=8, anneal="none"), batch=8, device="cpu")
+    table = profiling.profile_steps(e.train_step, steps=2, warmup=1, out_dir=tmp_path)
+    assert "flow_backward" in table and "optimizer" in table
+    assert (tmp_path / "trace.json").exists() and not profiling.enabled()
+    assert profiling.debug_env()["HIP_LAUNCH_BLOCKING"] == "1"

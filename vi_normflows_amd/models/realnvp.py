@@ -37,6 +37,7 @@ import torch
 from ..ops import fused
 from ..ops import gemm
 from ..utils.flat import FlatLayout, FlatParams
+from ..utils.profiling import trace_range
 
 
 @dataclass
@@ -347,11 +348,15 @@ class RealNVPVI:
     def train_step(self, reduce_fn=None):
         """One full ELBO step: sample, flow fwd, target, bwd, [grad all-reduce], optimizer."""
         self._update_schedule()
-        self.forward()
-        self.backward()
+        with trace_range("flow_forward+elbo"):
+            self.forward()
+        with trace_range("flow_backward"):
+            self.backward()
         if reduce_fn is not None:
-            reduce_fn()
-        self.optimizer_step()
+            with trace_range("grad_allreduce_wait"):
+                reduce_fn()
+        with trace_range("optimizer"):
+            self.optimizer_step()
 
     # ------------------------------------------------------------------ inference
     @torch.no_grad()
