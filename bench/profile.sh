@@ -8,6 +8,9 @@
 # summary is written to OUT/summary.txt.
 set -o pipefail
 mode=$1; out=$2; shift 2
+repo=$(cd "$(dirname "$0")/.." && pwd)
+case "$out" in /*) ;; *) out="$PWD/$out" ;; esac
+export PYTHONPATH="$repo${PYTHONPATH:+:$PYTHONPATH}"
 cd /tmp && export TMPDIR=/tmp
 case "$mode" in
   trace)
@@ -24,5 +27,5 @@ case "$mode" in
     ;;
   *) echo "usage: $0 trace|pmc|markers OUT [COUNTERS] -- CMD..."; exit 2 ;;
 esac
-cd - > /dev/null
+cd "$repo"
 python3 -m vi_normflows_amd.bench.prof_summary "$out" > "$out/summary.txt" 2>/dev/null && cat "$out/summary.txt"

@@ -35,6 +35,16 @@ def _from_csv(path):
     return [(n, c, t) for n, (c, t) in acc.items()]
 
 
+def _regions(path):
+    """roctx ranges (host time) by name: count, total and mean duration (us)."""
+    con = sqlite3.connect(path)
+    try:
+        rows = con.execute("select name, count(*), sum(end-start) from regions group by name").fetchall()
+    except sqlite3.Error:
+        return []
+    return [(n, c, t / 1e3) for n, c, t in rows]
+
+
 def summarize(root: str, steps: int | None = None, top: int = 30) -> str:
     dbs = glob.glob(os.path.join(root, "**", "*.db"), recursive=True)
     csvs = glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), recursive=True) or \
@@ -51,6 +61,12 @@ def summarize(root: str, steps: int | None = None, top: int = 30) -> str:
         if steps:
             line += f" {t / 1e3 / steps:8.3f}"
         out.append(line + "  " + n[:120])
+    regs = _regions(dbs[0]) if dbs else []
+    if regs:
+        out.append("")
+        out.append("roctx ranges (host-side enqueue time; VINF_TRACE=1)")
+        for n, c, t in sorted(regs, key=lambda r: -r[2]):
+            out.append(f"{t / 1e3:9.2f} ms {c:6d} calls {t / c:9.1f} us/call  {n}")
     return "\n".join(out)
 
 
