@@ -10,6 +10,7 @@ from __future__ import annotations
 import argparse
 import csv
 import glob
+import json
 import os
 import sqlite3
 from collections import defaultdict
@@ -39,10 +40,18 @@ def _regions(path):
     """roctx ranges (host time) by name: count, total and mean duration (us)."""
     con = sqlite3.connect(path)
     try:
-        rows = con.execute("select name, count(*), sum(end-start) from regions group by name").fetchall()
+        rows = con.execute("select name, extdata, end-start from regions").fetchall()
     except sqlite3.Error:
         return []
-    return [(n, c, t / 1e3) for n, c, t in rows]
+    acc = defaultdict(lambda: [0, 0.0])
+    for name, ext, dur in rows:
+        try:
+            name = json.loads(ext).get("message", name)
+        except (TypeError, ValueError):
+            pass
+        acc[name][0] += 1
+        acc[name][1] += dur / 1e3
+    return [(n, c, t) for n, (c, t) in acc.items()]
 
 
 def summarize(root: str, steps: int | None = None, top: int = 30) -> str:
