@@ -22,6 +22,14 @@ void chk_mat(const at::Tensor& t, const char* n, at::ScalarType dt) {
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, n, " must be 16-B aligned");
 }
 
+void chk_q(const at::Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 2, n, " must be a 2-D GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kByte || t.scalar_type() == at::kFloat8_e4m3fn, n,
+              " must be uint8 / float8_e4m3fn");
+  TORCH_CHECK(t.stride(1) == 1 && ld2(t) % 16 == 0, n, " rows must be 16-B aligned");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, n, " must be 16-B aligned");
+}
+
 // y = act(x W^T + b): x [M,K], W [N,K], b [N] (bf16), y [M,N] bf16
 void gemm_nt(const at::Tensor& x, const at::Tensor& W, const c10::optional<at::Tensor>& b,
              const at::Tensor& y, int64_t relu) {
@@ -96,7 +104,9 @@ void gemm_tn(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dW,
 
 // Grouped weight gradients: dW[p] = dy[p]^T x[p], db[p] = colsum(dy[p]) in one launch (+ reduce).
 void gemm_tn_group(at::TensorList dy, at::TensorList x, at::TensorList dW,
-                   const c10::List<c10::optional<at::Tensor>>& db) {
+                   const c10::List<c10::optional<at::Tensor>>& db,
+                   const c10::List<c10::optional<at::Tensor>>& skip,
+                   const c10::List<c10::optional<at::Tensor>>& cmask) {
   const size_t n = dy.size();
   TORCH_CHECK(n >= 1 && n <= 4 && x.size() == n && dW.size() == n && db.size() == n,
               "gemm_tn_group: 1..4 problems with matching lists");
@@ -117,6 +127,23 @@ void gemm_tn_group(at::TensorList dy, at::TensorList x, at::TensorList dW,
     }
     pr[p] = NfTnProblem{dy[p].data_ptr(), ld2(dy[p]), x[p].data_ptr(), ld2(x[p]),
                         dW[p].data_ptr<float>(), ld2(dW[p]), dbp, M, N, K};
+    if (skip.size() == n) {
+      const c10::optional<at::Tensor> sk = skip.get(p);
+      if (sk && sk->defined()) {
+        TORCH_CHECK(sk->is_cuda() && sk->scalar_type() == at::kByte && sk->is_contiguous() &&
+                        sk->numel() == (long)((M + 127) / 128) * ((N + 127) / 128), "skip flags");
+        pr[p].skip = sk->data_ptr<uint8_t>();
+      }
+    }
+    if (cmask.size() == n) {
+      const c10::optional<at::Tensor> cm = cmask.get(p);
+      if (cm && cm->defined()) {
+        TORCH_CHECK(cm->is_cuda() && cm->scalar_type() == at::kByte && cm->is_contiguous() &&
+                        cm->numel() == (long)M * N && N % 4 == 0, "cmask [M,N] uint8");
+        TORCH_CHECK(ld2(dW[p]) == N, "cmask needs a dense dW");
+        pr[p].cmask = cm->data_ptr<uint8_t>();
+      }
+    }
   }
   at::Tensor work;
   float* wp = nullptr;
@@ -126,6 +153,74 @@ void gemm_tn_group(at::TensorList dy, at::TensorList x, at::TensorList dW,
     wp = work.data_ptr<float>();
   }
   nf_launch_gemm_tn_group((int)n, pr, wp, cur_stream());
+}
+
+// all `layers` weights of one kind (rows_per x C each, layer_stride elements apart in the flat
+// fp32 buffer starting at x) quantised per row in one launch
+void fp8_quant_rows_strided(const at::Tensor& x, int64_t layer_stride, int64_t rows_per,
+                            int64_t layers, int64_t C, const at::Tensor& q, const at::Tensor& scale) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(), "x fp32 GPU");
+  TORCH_CHECK(x.numel() >= (layers - 1) * layer_stride + rows_per * C, "x too small");
+  chk_q(q, "q");
+  TORCH_CHECK(q.size(0) == rows_per * layers && q.size(1) >= C && q.size(1) % 4 == 0, "q shape");
+  TORCH_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat &&
+                  scale.numel() == rows_per * layers, "scale");
+  nf_launch_fp8_quant_rows_strided(x.data_ptr(), 0, C, layer_stride, (int)rows_per,
+                                   (int)(rows_per * layers), (int)C, q.data_ptr(), ld2(q), q.size(1),
+                                   scale.data_ptr<float>(), cur_stream());
+}
+
+// ----------------------------------------------------------------- MAF transform (maf.hip)
+void maf_fwd(const at::Tensor& x, const at::Tensor& o, double bound, const at::Tensor& u,
+             const c10::optional<at::Tensor>& ubf, const c10::optional<at::Tensor>& uq,
+             const c10::optional<at::Tensor>& amax_prev, const c10::optional<at::Tensor>& scale,
+             const c10::optional<at::Tensor>& amax_cur, const at::Tensor& ldj, bool ldj_init) {
+  chk_mat(x, "x", at::kFloat);
+  chk_mat(o, "o", at::kBFloat16);
+  chk_mat(u, "u", at::kFloat);
+  const int B = x.size(0), D = x.size(1);
+  TORCH_CHECK(D % 4 == 0 && o.size(0) == B && o.size(1) == 2 * D && u.size(0) == B && u.size(1) == D,
+              "maf_fwd shapes");
+  TORCH_CHECK(ldj.is_cuda() && ldj.scalar_type() == at::kFloat && ldj.numel() == B, "ldj");
+  void* ub = nullptr;
+  long ldub = 0;
+  if (ubf && ubf->defined()) {
+    chk_mat(*ubf, "ubf", at::kBFloat16);
+    ub = ubf->data_ptr();
+    ldub = ld2(*ubf);
+  }
+  void* q = nullptr;
+  long ldq = 0;
+  const float* ap = nullptr;
+  float* sc = nullptr;
+  float* ac = nullptr;
+  if (uq && uq->defined()) {
+    chk_q(*uq, "uq");
+    TORCH_CHECK(amax_prev && scale && amax_cur, "fp8 output needs the delayed-scale state");
+    q = uq->data_ptr();
+    ldq = ld2(*uq);
+    ap = amax_prev->data_ptr<float>();
+    sc = scale->data_ptr<float>();
+    ac = amax_cur->data_ptr<float>();
+  }
+  nf_launch_maf_fwd(x.data_ptr<float>(), ld2(x), o.data_ptr(), ld2(o), B, D, (float)bound,
+                    u.data_ptr<float>(), ld2(u), ub, ldub, q, ldq, ap, sc, ac,
+                    ldj.data_ptr<float>(), ldj_init, cur_stream());
+}
+
+void maf_bwd(const at::Tensor& gu, const at::Tensor& u, const at::Tensor& o, double bound,
+             double c_ldj, const at::Tensor& dout, const at::Tensor& gx) {
+  chk_mat(gu, "gu", at::kFloat);
+  chk_mat(u, "u", at::kFloat);
+  chk_mat(o, "o", at::kBFloat16);
+  chk_mat(dout, "dout", at::kBFloat16);
+  chk_mat(gx, "gx", at::kFloat);
+  const int B = gu.size(0), D = gu.size(1);
+  TORCH_CHECK(D % 4 == 0 && u.size(0) == B && u.size(1) == D && o.size(1) == 2 * D &&
+                  dout.size(1) == 2 * D && gx.size(1) == D, "maf_bwd shapes");
+  nf_launch_maf_bwd(gu.data_ptr<float>(), ld2(gu), u.data_ptr<float>(), ld2(u), o.data_ptr(),
+                    ld2(o), B, D, (float)bound, (float)c_ldj, dout.data_ptr(), ld2(dout),
+                    gx.data_ptr<float>(), ld2(gx), cur_stream());
 }
 
 // ----------------------------------------------------------------- masked (MADE) variants
@@ -149,7 +244,7 @@ void masked_gemm_nt(const at::Tensor& x, const at::Tensor& W, const c10::optiona
 }
 
 void masked_gemm_nn(const at::Tensor& dy, const at::Tensor& W, const c10::optional<at::Tensor>& h,
-                    const at::Tensor& dx, const at::Tensor& krange) {
+                    const at::Tensor& dx, const at::Tensor& krange, bool accumulate) {
   chk_mat(dy, "dy", at::kBFloat16);
   chk_mat(W, "W", at::kBFloat16);
   const bool f32 = dx.scalar_type() == at::kFloat;
@@ -165,8 +260,9 @@ void masked_gemm_nn(const at::Tensor& dy, const at::Tensor& W, const c10::option
     hp = h->data_ptr();
     ldh = ld2(*h);
   }
+  TORCH_CHECK(!accumulate || f32, "accumulate needs an fp32 dx");
   nf_launch_gemm_nn_masked(dy.data_ptr(), ld2(dy), W.data_ptr(), ld2(W), hp, ldh, dx.data_ptr(),
-                           ld2(dx), f32, M, N, K, krange.data_ptr<int>(), cur_stream());
+                           ld2(dx), f32, accumulate, M, N, K, krange.data_ptr<int>(), cur_stream());
 }
 
 void masked_gemm_tn(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dW,
@@ -196,17 +292,99 @@ void masked_gemm_tn(const at::Tensor& dy, const at::Tensor& x, const at::Tensor&
 
 }  // namespace
 
+// ----------------------------------------------------------------- fp8 (OCP e4m3)
+
+// q = e4m3(x / scale[row]), scale[row] = amax(row) / 448; q may be wider than x (zero pad)
+void fp8_quant_rows(const at::Tensor& x, const at::Tensor& q, const at::Tensor& scale) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x: 2-D GPU, unit inner stride");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat, "x bf16/fp32");
+  chk_q(q, "q");
+  TORCH_CHECK(q.size(0) == x.size(0) && q.size(1) >= x.size(1) && q.size(1) % 4 == 0, "q shape");
+  TORCH_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale.numel() == x.size(0) &&
+                  scale.is_contiguous(), "scale [rows] fp32");
+  nf_launch_fp8_quant_rows(x.data_ptr(), x.scalar_type() == at::kBFloat16, ld2(x), x.size(0),
+                           x.size(1), q.data_ptr(), ld2(q), q.size(1), scale.data_ptr<float>(),
+                           cur_stream());
+}
+
+// delayed per-tensor scaling: q = e4m3(sat(x / s)), s = amax_prev / 448; amax_cur = max(amax_cur, |x|)
+void fp8_quant_tensor(const at::Tensor& x, const at::Tensor& q, const at::Tensor& amax_prev,
+                      const at::Tensor& scale, const at::Tensor& amax_cur) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x: 2-D GPU, unit inner stride");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat, "x bf16/fp32");
+  chk_q(q, "q");
+  TORCH_CHECK(q.size(0) == x.size(0) && q.size(1) >= x.size(1) && q.size(1) % 4 == 0, "q shape");
+  for (const at::Tensor* t : {&amax_prev, &scale, &amax_cur})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() >= 1, "scalars fp32");
+  nf_launch_fp8_quant_tensor(x.data_ptr(), x.scalar_type() == at::kBFloat16, ld2(x), x.size(0),
+                             x.size(1), q.data_ptr(), ld2(q), q.size(1), amax_prev.data_ptr<float>(),
+                             scale.data_ptr<float>(), amax_cur.data_ptr<float>(), cur_stream());
+}
+
+// y = act((xq * sx) (wq * sw)^T + b) -> bf16; K % 128 == 0; optional MADE krange per 128-row tile
+// sx: [M] per-row or [1] per-tensor
+void gemm_fp8_nt(const at::Tensor& xq, const at::Tensor& sx, const at::Tensor& wq,
+                 const at::Tensor& sw, const c10::optional<at::Tensor>& b, const at::Tensor& y,
+                 int64_t relu, const c10::optional<at::Tensor>& krange,
+                 const c10::optional<at::Tensor>& yq, const c10::optional<at::Tensor>& q_amax_prev,
+                 const c10::optional<at::Tensor>& q_scale, const c10::optional<at::Tensor>& q_amax_cur) {
+  chk_q(xq, "xq");
+  chk_q(wq, "wq");
+  chk_mat(y, "y", at::kBFloat16);
+  const int M = xq.size(0), K = xq.size(1), N = wq.size(0);
+  TORCH_CHECK(wq.size(1) == K && y.size(0) == M && y.size(1) == N, "shapes");
+  TORCH_CHECK(K % 128 == 0 && N % 8 == 0, "K % 128 and N % 8 required");
+  TORCH_CHECK(sx.is_cuda() && sx.scalar_type() == at::kFloat && (sx.numel() == M || sx.numel() == 1) &&
+                  sx.is_contiguous(), "sx [M] or [1]");
+  TORCH_CHECK(sw.is_cuda() && sw.scalar_type() == at::kFloat && sw.numel() == N && sw.is_contiguous(), "sw");
+  const void* bp = nullptr;
+  if (b && b->defined()) {
+    TORCH_CHECK(b->scalar_type() == at::kBFloat16 && b->numel() == N && b->is_contiguous(), "bias");
+    bp = b->data_ptr();
+  }
+  const int* kr = nullptr;
+  if (krange && krange->defined()) {
+    chk_ranges(*krange, (N + 127) / 128, "krange");
+    kr = krange->data_ptr<int>();
+  }
+  void* qp = nullptr;
+  long ldq = 0;
+  const float* qap = nullptr;
+  float* qs = nullptr;
+  float* qac = nullptr;
+  if (yq && yq->defined()) {
+    chk_q(*yq, "yq");
+    TORCH_CHECK(yq->size(0) == M && yq->size(1) == N, "yq shape");
+    TORCH_CHECK(q_amax_prev && q_scale && q_amax_cur, "yq needs the delayed-scale state");
+    qp = yq->data_ptr();
+    ldq = ld2(*yq);
+    qap = q_amax_prev->data_ptr<float>();
+    qs = q_scale->data_ptr<float>();
+    qac = q_amax_cur->data_ptr<float>();
+  }
+  nf_launch_gemm_fp8_nt(xq.data_ptr(), ld2(xq), sx.data_ptr<float>(), sx.numel() == M && M > 1,
+                        wq.data_ptr(), ld2(wq),
+                        sw.data_ptr<float>(), bp, y.data_ptr(), ld2(y), M, N, K, (int)relu, kr,
+                        qp, ldq, qap, qs, qac, cur_stream());
+}
+
 void gemm_set_mode(int64_t mode, int64_t depth) { nf_gemm_set_mode((int)mode, (int)depth); }
 
 TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("gemm_set_mode(int mode, int depth) -> ()", &gemm_set_mode);
+  m.def("fp8_quant_rows(Tensor x, Tensor(a!) q, Tensor(b!) scale) -> ()");
+  m.def("fp8_quant_tensor(Tensor x, Tensor(a!) q, Tensor amax_prev, Tensor(b!) scale, Tensor(c!) amax_cur) -> ()");
+  m.def("gemm_fp8_nt(Tensor xq, Tensor sx, Tensor wq, Tensor sw, Tensor? b, Tensor(a!) y, int relu, Tensor? krange, Tensor(b!)? yq=None, Tensor? q_amax_prev=None, Tensor(c!)? q_scale=None, Tensor(d!)? q_amax_cur=None) -> ()");
   m.def("masked_gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu, Tensor krange) -> ()");
-  m.def("masked_gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, Tensor krange) -> ()");
+  m.def("masked_gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, Tensor krange, bool accumulate=False) -> ()");
   m.def("masked_gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db, Tensor skip) -> ()");
   m.def("gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu) -> ()");
   m.def("gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, bool accumulate) -> ()");
   m.def("gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db) -> ()");
-  m.def("gemm_tn_group(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db) -> ()");
+  m.def("gemm_tn_group(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, Tensor?[] skip, Tensor?[] cmask) -> ()");
+  m.def("fp8_quant_rows_strided(Tensor x, int layer_stride, int rows_per, int layers, int C, Tensor(a!) q, Tensor(b!) scale) -> ()");
+  m.def("maf_fwd(Tensor x, Tensor o, float bound, Tensor(a!) u, Tensor(b!)? ubf, Tensor(c!)? uq, Tensor? amax_prev, Tensor(d!)? scale, Tensor(e!)? amax_cur, Tensor(f!) ldj, bool ldj_init) -> ()");
+  m.def("maf_bwd(Tensor gu, Tensor u, Tensor o, float bound, float c_ldj, Tensor(a!) dout, Tensor(b!) gx) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
@@ -217,4 +395,10 @@ TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
   m.impl("gemm_nn", &gemm_nn);
   m.impl("gemm_tn", &gemm_tn);
   m.impl("gemm_tn_group", &gemm_tn_group);
+  m.impl("fp8_quant_rows", &fp8_quant_rows);
+  m.impl("fp8_quant_rows_strided", &fp8_quant_rows_strided);
+  m.impl("maf_fwd", &maf_fwd);
+  m.impl("maf_bwd", &maf_bwd);
+  m.impl("fp8_quant_tensor", &fp8_quant_tensor);
+  m.impl("gemm_fp8_nt", &gemm_fp8_nt);
 }

@@ -41,6 +41,7 @@ struct GemmArgs {
   // Masked (MADE) GEMMs - structural sparsity of the weight mask:
   const int* krange;           // [ntn][2] per output N-tile K range [lo, hi) (multiples of 64), or null
   const unsigned char* skip;   // [ntm*ntn] 1 -> tile entirely masked: write zeros, no MFMA, or null
+  const unsigned char* cmask;  // [M][N] 0/1 applied to fp32 outputs (masked weight gradients), or null
 };
 
 // Grouped launch: up to 4 independent problems (the weight gradients of one conditioner MLP),
@@ -108,6 +109,10 @@ __device__ __forceinline__ void epi_store(const GemmArgs& a, v4f v, int m, int n
     o.x = f2bf(v[0]); o.y = f2bf(v[1]); o.z = f2bf(v[2]); o.w = f2bf(v[3]);
     *reinterpret_cast<ushort4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
   } else if (EPI == EPI_F32) {
+    if (a.cmask) {
+      const uchar4 mk = *reinterpret_cast<const uchar4*>(a.cmask + (long)m * a.N + n);
+      v[0] = mk.x ? v[0] : 0.f; v[1] = mk.y ? v[1] : 0.f; v[2] = mk.z ? v[2] : 0.f; v[3] = mk.w ? v[3] : 0.f;
+    }
     float* cp = (float*)a.C + (long)split * a.c_split_stride + (long)m * a.ldc + n;
     *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
   } else {  // EPI_F32_ACC

@@ -62,6 +62,8 @@ struct NfTnProblem {
   float* dW; long lddw;
   float* db;
   int M, N, K;
+  const unsigned char* skip = nullptr;   // masked (MADE) weights: all-zero 128x128 tiles of dW
+  const unsigned char* cmask = nullptr;  // [M][N] 0/1: zero the masked entries of dW
 };
 long nf_gemm_tn_group_workspace(int nprob, const NfTnProblem* pr);
 void nf_launch_gemm_tn_group(int nprob, const NfTnProblem* pr, float* work, hipStream_t stream);
@@ -77,6 +79,17 @@ int nf_launch_gemm256_tn_partials(const void* dy, long lddy, const void* x, long
                                   int splits, hipStream_t stream);
 // mode: 0 auto, 1 force 128x128, 2 force 256x256; depth: half-tiles in flight (3 or 4)
 void nf_gemm_set_mode(int mode, int depth);
+// fp8.hip (OCP e4m3): per-row quantisation and the MX-scaled K=128 MFMA GEMM
+void nf_launch_fp8_quant_rows(const void* x, int x_is_bf16, long ldx, int R, int C, void* q,
+                              long ldq, int Cq, float* scale, hipStream_t stream);
+void nf_launch_fp8_quant_tensor(const void* x, int x_is_bf16, long ldx, int R, int C, void* q,
+                                long ldq, int Cq, const float* amax_prev, float* scale_out,
+                                float* amax_cur, hipStream_t stream);
+void nf_launch_gemm_fp8_nt(const void* xq, long ldx, const float* sx, int sx_per_row,
+                           const void* wq, long ldw, const float* sw, const void* bias, void* y,
+                           long ldy, int M, int N, int K, int relu, const int* krange,
+                           void* yq, long ldyq, const float* q_amax_prev, float* q_scale_out,
+                           float* q_amax_cur, hipStream_t stream);
 int nf_gemm_tn_splits(int M, int N, int K);
 
 // planar.hip / radial.hip (fused K-layer stacks; per-row parameter gradients)
@@ -99,8 +112,21 @@ void nf_launch_gemm_nt_masked(const void* x, long ldx, const void* W, long ldw, 
                               void* y, long ldy, int M, int N, int K, int relu, const int* krange,
                               hipStream_t stream);
 void nf_launch_gemm_nn_masked(const void* dy, long lddy, const void* W, long ldw, const void* aux,
-                              long ld_aux, void* dx, long lddx, int dx_is_f32, int M, int N, int K,
-                              const int* krange, hipStream_t stream);
+                              long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
+                              int N, int K, const int* krange, hipStream_t stream);
 void nf_launch_gemm_tn_masked(const void* dy, long lddy, const void* x, long ldx, float* dW,
                               long lddw, float* db, int M, int N, int K, int splits, float* work,
                               const unsigned char* skip, hipStream_t stream);
+
+// maf.hip: masked autoregressive flow transform (density direction) fwd / bwd
+void nf_launch_maf_fwd(const float* x, long ldx, const void* o, long ldo, int B, int D, float bound,
+                       float* u, long ldu, void* ubf, long ldub, void* uq, long lduq,
+                       const float* amax_prev, float* scale_out, float* amax_cur, float* ldj,
+                       int ldj_init, hipStream_t stream);
+void nf_launch_maf_bwd(const float* gu, long ldg, const float* u, long ldu, const void* o, long ldo,
+                       int B, int D, float bound, float c_ldj, void* dout, long lddo, float* gx,
+                       long ldgx, hipStream_t stream);
+// fp8.hip: layer-strided per-row weight quantisation (rows r -> layer r / rows_per)
+void nf_launch_fp8_quant_rows_strided(const void* x, int x_is_bf16, long ldx, long layer_stride,
+                                      int rows_per, int R, int C, void* q, long ldq, int Cq,
+                                      float* scale, hipStream_t stream);

@@ -234,6 +234,7 @@ struct ReduceGroup {
   int rows[4], cols[4];
   const float* dpart[4];
   float* db[4];
+  const unsigned char* cmask[4];   // [rows][cols] 0/1 or null
   long istart[5];
   int nprob;
 };
@@ -256,6 +257,11 @@ __global__ void __launch_bounds__(256) splitk_reduce_group_kernel(ReduceGroup r)
       for (int k = 1; k < splits; ++k) {
         const float4 t = *reinterpret_cast<const float4*>(sp + k * r.slab_stride[p]);
         acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+      }
+      if (r.cmask[p]) {
+        const uchar4 mk = *reinterpret_cast<const uchar4*>(r.cmask[p] + (long)row * cols + 4 * q);
+        acc.x = mk.x ? acc.x : 0.f; acc.y = mk.y ? acc.y : 0.f;
+        acc.z = mk.z ? acc.z : 0.f; acc.w = mk.w ? acc.w : 0.f;
       }
       *reinterpret_cast<float4*>(r.out[p] + (long)row * r.ld_out[p] + 4 * q) = acc;
     } else {
@@ -456,8 +462,8 @@ void nf_launch_gemm_nt_masked(const void* x, long ldx, const void* W, long ldw, 
 }
 
 void nf_launch_gemm_nn_masked(const void* dy, long lddy, const void* W, long ldw, const void* aux,
-                              long ld_aux, void* dx, long lddx, int dx_is_f32, int M, int N, int K,
-                              const int* krange, hipStream_t stream) {
+                              long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
+                              int N, int K, const int* krange, hipStream_t stream) {
   if (M <= 0 || N <= 0) return;
   GemmArgs a{};
   a.A = (const bf16_t*)dy; a.lda = lddy;
@@ -466,7 +472,8 @@ void nf_launch_gemm_nn_masked(const void* dy, long lddy, const void* W, long ldw
   a.aux = (const bf16_t*)aux; a.ld_aux = ld_aux;
   a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + BK - 1) / BK) * BK;
   a.krange = krange;
-  if (dx_is_f32) launch<true, false, EPI_F32>(a, 1, stream);
+  if (dx_is_f32 && accumulate) launch<true, false, EPI_F32_ACC>(a, 1, stream);
+  else if (dx_is_f32) launch<true, false, EPI_F32>(a, 1, stream);
   else if (aux) launch<true, false, EPI_BF16_RELUMASK>(a, 1, stream);
   else launch<true, false, EPI_BF16>(a, 1, stream);
 }
@@ -553,6 +560,9 @@ void nf_launch_gemm_tn_group(int nprob, const NfTnProblem* pr, float* work, hipS
     a.A = (const bf16_t*)q.dy; a.lda = q.lddy;
     a.B = (const bf16_t*)q.x; a.ldb = q.ldx;
     a.M = q.M; a.N = q.N; a.K = q.K; a.k_per_split = kts * BK;
+    a.skip = q.skip;
+    a.cmask = q.cmask;
+    r.cmask[p] = q.cmask;
     const int tb = use_256_tn() ? 256 : BM;
     const int tiles = ((q.M + tb - 1) / tb) * ((q.N + tb - 1) / tb);
     g.start[p + 1] = g.start[p] + tiles * used;

@@ -178,7 +178,7 @@ def test_gemm_tn_group(gpu, B, mode):
         items.append((dy, x, dW, db))
         refs.append((dy.float().t() @ x.float(), dy.float().sum(0)))
     torch.ops.vinf.gemm_tn_group([i[0] for i in items], [i[1] for i in items],
-                                 [i[2] for i in items], [i[3] for i in items])
+                                 [i[2] for i in items], [i[3] for i in items], [], [])
     torch.ops.vinf.gemm_set_mode(0, 4)
     for (dy, x, dW, db), (rW, rb) in zip(items, refs):
         _check(dW, rW, 1e-4)

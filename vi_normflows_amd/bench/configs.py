@@ -21,7 +21,7 @@ NAMES = {1: "2D two-moons planar-flow VI on CPU (plumbing, no GPU)",
          2: "8-layer RealNVP on 784-dim synthetic (MNIST-shape), bf16, 1xMI355X",
          3: "32-layer RealNVP on 784-dim synthetic, DP over xGMI (see bench.py)",
          4: "IAF-10 amortized VI (VAE encoder) on 3x32x32 synthetic",
-         5: "MAF-64 density estimation on 1024-dim synthetic"}
+         5: "MAF-64 density estimation on 1024-dim synthetic, fp8 MFMA"}
 
 
 def _sync(dev):
@@ -29,7 +29,25 @@ def _sync(dev):
         torch.cuda.synchronize()
 
 
-def build(cfg_id: int, info, batch: int | None):
+def graphed(step_fn, dev, warmup: int = 3):
+    """Capture one whole training step (forward, backward, optimizer) into a hipGraph and
+    return its replay: the Python/launch cost of the ~2000 small kernels of a MAF-64 /
+    IAF-10 step disappears. Needs a capturable optimizer and static input buffers."""
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        for _ in range(warmup):
+            step_fn()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step_fn()
+    return g
+
+
+def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: bool = True,
+          impl: str = "engine"):
     dev = info.device
     if cfg_id == 1:
         from ..distributions.base import StdNormal
@@ -68,38 +86,65 @@ def build(cfg_id: int, info, batch: int | None):
         model = IAFVAE(IAFVAEConfig()).to(dev)
         model = _ddp(model, info)
         X = synthetic_images(B * 4, device=dev, seed=info.rank)
-        opt = torch.optim.Adam(model.parameters(), lr=3e-4)
+        use_graph = graph and dev.type == "cuda" and info.world == 1
+        opt = torch.optim.Adam(model.parameters(), lr=3e-4, capturable=use_graph)
         inner = model.module if hasattr(model, "module") else model
+        xs = X[:B].clone()
         it = [0]
+
+        def compute():
+            F = _loss_ddp(model, inner, xs)
+            opt.zero_grad(set_to_none=True)
+            F.backward()
+            opt.step()
+
+        g = graphed(compute, dev) if use_graph else None
 
         def step():
             i = it[0] % 4
             it[0] += 1
-            F = _loss_ddp(model, inner, X[i * B:(i + 1) * B])
-            opt.zero_grad()
-            F.backward()
-            opt.step()
-        return step, B, dev, "bf16 (MFMA masked GEMMs)"
+            xs.copy_(X[i * B:(i + 1) * B])   # a new batch every step
+            g.replay() if g is not None else compute()
+        return step, B, dev, "bf16 (MFMA masked GEMMs)" + (", hipGraph" if use_graph else "")
+    if cfg_id == 5 and impl == "engine":
+        from ..models.maf_engine import MAFEngine, MAFEngineConfig
+        from ..parallel.runner import DataParallelRunner
+
+        B = batch or 8192
+        eng = MAFEngine(MAFEngineConfig(precision=precision), batch=B, device=dev, rank=info.rank)
+        run = DataParallelRunner(eng, info)
+        if graph and dev.type == "cuda":
+            run.capture(warmup=2)
+        return run.step, B, dev, (("fp8 e4m3 forward (MX K=128 MFMA) + bf16 backward" if precision == "fp8"
+                                   else "bf16") + ", MAF engine" + (", hipGraph" if run.graph else ""))
     if cfg_id == 5:
         from ..models.maf_density import MAFConfig, MAFDensity, banana_samples
 
         B = batch or 1024
-        model = MAFDensity(MAFConfig()).to(dev)
+        model = MAFDensity(MAFConfig(precision=precision)).to(dev)
         model = _ddp(model, info)
         inner = model.module if hasattr(model, "module") else model
         X = banana_samples(B * 4, 1024, device=dev)
-        opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+        use_graph = graph and dev.type == "cuda" and info.world == 1
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4, capturable=use_graph)
+        xs = X[:B].clone()
         it = [0]
+
+        def compute():
+            nll = -(model(xs) if hasattr(model, "module") else inner.log_prob(xs)).mean()
+            opt.zero_grad(set_to_none=True)
+            nll.backward()
+            opt.step()
+
+        g = graphed(compute, dev) if use_graph else None
 
         def step():
             i = it[0] % 4
             it[0] += 1
-            nll = -(model(X[i * B:(i + 1) * B]) if hasattr(model, "module") else
-                    inner.log_prob(X[i * B:(i + 1) * B])).mean()
-            opt.zero_grad()
-            nll.backward()
-            opt.step()
-        return step, B, dev, "bf16 (MFMA masked GEMMs)"
+            xs.copy_(X[i * B:(i + 1) * B])
+            g.replay() if g is not None else compute()
+        return step, B, dev, (("fp8 e4m3 forward (MX K=128 MFMA) + bf16 backward" if precision == "fp8"
+                               else "bf16 (MFMA masked GEMMs)") + (", hipGraph" if use_graph else ""))
     raise KeyError(cfg_id)
 
 
@@ -111,7 +156,7 @@ class _Fwd(torch.nn.Module):
         self.m, self.kind = m, kind
 
     def forward(self, x):
-        return self.m.loss(x).F if self.kind == "loss" else self.m.log_prob(x)
+        return self.m.loss(x, with_stats=False).F if self.kind == "loss" else self.m.log_prob(x)
 
 
 def _ddp(model, info):
@@ -129,7 +174,7 @@ def _ddp(model, info):
 def _loss_ddp(model, inner, x):
     if hasattr(model, "module"):
         return model(x)
-    return inner.loss(x).F
+    return inner.loss(x, with_stats=False).F
 
 
 def main(argv=None):
@@ -138,9 +183,13 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--precision", default="fp8", choices=["fp8", "bf16"], help="config 5 GEMMs")
+    ap.add_argument("--graph", default="on", choices=["on", "off"])
+    ap.add_argument("--impl", default="engine", choices=["engine", "module"],
+                    help="config 5: explicit-backward MAF engine or the autograd MAFDensity module")
     a = ap.parse_args(argv)
     info = vdist.init(device_type="cpu" if a.config == 1 else None)
-    step, B, dev, dtype = build(a.config, info, a.batch)
+    step, B, dev, dtype = build(a.config, info, a.batch, a.precision, a.graph == "on", a.impl)
     for _ in range(a.warmup):
         step()
     _sync(dev)

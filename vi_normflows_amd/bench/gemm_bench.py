@@ -80,7 +80,7 @@ def main():
                             torch.empty(m_, n_, device=dev), torch.empty(m_, device=dev)))
             M, N = 1, 800 * 1024 + 1024 * 1024 + 1024 * 416
             mine = lambda: ops.gemm_tn_group([i[0] for i in its], [i[1] for i in its],
-                                             [i[2] for i in its], [i[3] for i in its])
+                                             [i[2] for i in its], [i[3] for i in its], [], [])
 
             def ref():
                 for i in its:

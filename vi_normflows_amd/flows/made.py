@@ -50,6 +50,8 @@ def made_masks(d_in, hs, out_mult: int):
 
 
 class MaskedLinear(nn.Linear):
+    precision = "bf16"   # GPU product precision: "bf16" | "fp8" (forward on e4m3 MX MFMA)
+
     def __init__(self, d_in, d_out, mask: torch.Tensor):
         super().__init__(d_in, d_out)
         self.register_buffer("mask", mask)
@@ -59,7 +61,23 @@ class MaskedLinear(nn.Linear):
     def forward(self, x):
         from ..ops.masked import masked_linear
 
-        return masked_linear(x, self.weight, self.bias, self.mask)
+        act_scale = None
+        if self.precision == "fp8" and x.is_cuda:
+            from ..ops.fp8 import DelayedScale
+
+            act_scale = self.__dict__.get("_fp8_scale")
+            if act_scale is None or act_scale.amax.device != x.device:
+                act_scale = self.__dict__["_fp8_scale"] = DelayedScale(x.device)
+        return masked_linear(x, self.weight, self.bias, self.mask, self.precision, act_scale)
+
+
+def set_precision(module: nn.Module, precision: str) -> nn.Module:
+    """Select the GEMM precision of every MaskedLinear inside ``module`` ("bf16" | "fp8")."""
+    assert precision in ("bf16", "fp8"), precision
+    for m in module.modules():
+        if isinstance(m, MaskedLinear):
+            m.precision = precision
+    return module
 
 
 class MADE(nn.Module):

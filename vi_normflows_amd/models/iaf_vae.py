@@ -56,7 +56,7 @@ class IAFVAE(nn.Module):
         o = self.enc_out(self.encoder(x))
         return o[:, :dz], o[:, dz:2 * dz], o[:, 2 * dz:]
 
-    def loss(self, x, beta: float = 1.0, generator=None) -> FreeEnergy:
+    def loss(self, x, beta: float = 1.0, generator=None, with_stats: bool = True) -> FreeEnergy:
         x = x.reshape(x.shape[0], -1)
         mu, logvar, h = self.encode(x)
         eps = torch.randn(mu.shape, device=mu.device, dtype=mu.dtype, generator=generator)
@@ -68,6 +68,8 @@ class IAFVAE(nn.Module):
             ldj = ldj + l
         lp = log_bern_logits(x, self.decoder(z)) + log_std_norm(z)
         F = (lq - ldj - beta * lp).mean()
+        if not with_stats:   # no host syncs (hipGraph capture)
+            return FreeEnergy(F, {})
         st = {"log_q0": float(lq.mean()), "ldj": float(ldj.mean()), "log_p": float(lp.mean())}
         return FreeEnergy(F, st)
 

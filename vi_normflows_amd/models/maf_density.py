@@ -15,7 +15,7 @@ from dataclasses import dataclass
 import torch
 from torch import nn
 
-from ..flows.made import MAF
+from ..flows.made import MAF, set_precision
 
 LOG2PI = math.log(2 * math.pi)
 
@@ -26,6 +26,7 @@ class MAFConfig:
     n_layers: int = 64
     hidden: int = 1024
     n_hidden: int = 1
+    precision: str = "bf16"   # "fp8": MADE forward products on the e4m3 MX MFMA kernel
 
 
 class MAFDensity(nn.Module):
@@ -34,6 +35,7 @@ class MAFDensity(nn.Module):
         self.cfg = cfg
         self.layers = nn.ModuleList(MAF(cfg.dim, cfg.hidden, cfg.n_hidden, reverse=bool(l % 2))
                                     for l in range(cfg.n_layers))
+        set_precision(self, cfg.precision)
 
     def log_prob(self, x):
         ldj = torch.zeros(x.shape[0], device=x.device, dtype=torch.float32)

@@ -1,0 +1,341 @@
+"""MAF-L density-estimation engine (north-star config 5: "MAF-64 density estimation on
+1024-dim synthetic, fp8 MFMA, DP=8").
+
+Same design as the RealNVP engine (``models/realnvp.py``): every parameter lives in one flat
+fp32 master buffer (bf16 working copy, fp32 gradient, Adam moments), the backward pass is
+written out explicitly, and a whole step is allocation-free, so it can be captured into one
+hipGraph and its gradient buckets all-reduced during backward (``parallel.runner``).
+
+Per layer l (MADE with one hidden layer, Papamakarios et al. 2017; autoregressive order
+reversed on odd layers):
+
+    h   = relu(x W1^T + b1)            W1 = W1 * M1   [H, D]
+    o   = h W2^T + b2 = [mu | s_raw]   W2 = W2 * M2   [2D, H]
+    u   = (x - mu) exp(-alpha),  alpha = bound tanh(s_raw / bound),  ldj -= sum(alpha)
+
+    NLL = mean_b( |u_L|^2 / 2 + D/2 log 2 pi - ldj )
+
+Kernels: the two forward products run on the fp8 e4m3 MX K=128 MFMA kernel
+(``csrc/kernels/fp8.hip``; weights quantised per row once per step by one strided launch per
+weight kind, activations with delayed per-tensor scales - the MAF transform kernel emits the
+next layer's e4m3 input directly) or on the bf16 masked kernels; the backward products are
+the bf16 tile-skipping masked kernels (``gemm.hip``: ReLU-mask dgrad epilogue, fp32
+accumulate for the input gradient, grouped split-K weight gradients with the dense MADE mask
+applied in the epilogue so masked weights stay exactly zero under Adam). The elementwise
+transform is ``csrc/kernels/maf.hip``. Data: fresh synthetic 1024-d twisted-Gaussian
+("banana") samples drawn on the device every step (Philox, rank-distinct streams), whose
+entropy is the NLL floor.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from ..flows.made import made_degrees, made_masks
+from ..ops import fused
+from ..ops import gemm
+from ..utils.flat import FlatLayout, FlatParams
+from ..utils.profiling import trace_range
+
+LOG2PI = math.log(2 * math.pi)
+
+
+@dataclass
+class MAFEngineConfig:
+    dim: int = 1024
+    n_layers: int = 64
+    hidden: int = 1024
+    alpha_bound: float = 5.0
+    precision: str = "fp8"          # "fp8" | "bf16" forward products (GPU); CPU runs fp32
+    init_out_std: float = 1e-2
+    banana_sigma1: float = 1.0
+    banana_sigma2: float = 0.5
+    banana_bend: float = 0.5
+
+    def n_params(self) -> int:
+        D, H = self.dim, self.hidden
+        return self.n_layers * (H * D + H + 2 * D * H + 2 * D)
+
+    def flops_per_sample(self, masked: bool = True) -> float:
+        """Forward + backward GEMM FLOPs per sample (masked: ~half the dense MACs)."""
+        D, H = self.dim, self.hidden
+        macs = H * D + 2 * D * H
+        return 6.0 * macs * self.n_layers * (0.5 if masked else 1.0)
+
+    def entropy(self) -> float:
+        """Differential entropy of the data distribution (the NLL floor)."""
+        return (self.dim // 2) * (1.0 + LOG2PI + math.log(self.banana_sigma1) +
+                                  math.log(self.banana_sigma2))
+
+
+class MAFEngine:
+    def __init__(self, cfg: MAFEngineConfig, batch: int, device="cuda", seed: int = 0,
+                 rank: int = 0, lr: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, max_grad_norm: float = 0.0):
+        self.cfg = cfg
+        self.B = int(batch)
+        self.device = torch.device(device)
+        gpu = self.device.type == "cuda"
+        self.cdt = torch.bfloat16 if gpu else torch.float32
+        self.fp8 = gpu and cfg.precision == "fp8"
+        self.seed, self.rank = int(seed), int(rank)
+        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+        self.opt_kind = fused.OPT_ADAM
+        self.max_grad_norm = float(max_grad_norm)
+        self.grad_scale_host = 1.0
+        self.unit_ready_hook = None
+        self.data_override = None      # fixed data [B, D] (tests)
+        D, H, L = cfg.dim, cfg.hidden, cfg.n_layers
+        if gpu:
+            assert D % 128 == 0 and H % 128 == 0, "dim and hidden must be multiples of 128"
+        layout = FlatLayout()
+        for l in range(L):
+            layout.add_unit([(f"l{l}.W1", (H, D)), (f"l{l}.b1", (H,)),
+                             (f"l{l}.W2", (2 * D, H)), (f"l{l}.b2", (2 * D,))])
+        self.layout = layout
+        self.params = FlatParams(layout, self.device, self.cdt)
+        s0, s1 = layout.slots["l0.W1"], layout.slots["l1.W1"] if L > 1 else None
+        self.layer_stride = (s1.offset - s0.offset) if s1 is not None else layout.total
+        self._build_masks()
+        self._alloc()
+        self.init_params(seed)
+
+    # ------------------------------------------------------------------ setup
+    def _build_masks(self):
+        from ..ops.masked import MaskPlan
+
+        cfg, dev = self.cfg, self.device
+        D, H = cfg.dim, cfg.hidden
+        self.masks = []          # per parity: (M1 float, M2 float, M1 u8, M2 u8, plan1, plan2)
+        for parity in range(min(2, cfg.n_layers)):
+            order = torch.arange(D, 0, -1) if parity else None
+            d_in, hs = made_degrees(D, H, 1, order)
+            m1, m2 = made_masks(d_in, hs, 2)
+            m1, m2 = m1.float().to(dev), m2.float().to(dev)
+            entry = {"M1": m1, "M2": m2, "M1u": m1.to(torch.uint8).contiguous(),
+                     "M2u": m2.to(torch.uint8).contiguous()}
+            if dev.type == "cuda":
+                entry["P1"], entry["P2"] = MaskPlan(m1), MaskPlan(m2)
+            self.masks.append(entry)
+
+    def _mask(self, l):
+        return self.masks[l % 2]
+
+    def _alloc(self):
+        cfg, B, dev = self.cfg, self.B, self.device
+        D, H, L = cfg.dim, cfg.hidden, cfg.n_layers
+        f32 = torch.float32
+        self.step_t = torch.zeros((), dtype=f32, device=dev)
+        self.rng_offset = torch.zeros((), dtype=torch.int64, device=dev)
+        self.loss = torch.zeros((), dtype=f32, device=dev)
+        self.gnorm2 = torch.zeros((), dtype=f32, device=dev)
+        self.skip = torch.zeros((), dtype=f32, device=dev)
+        self.gscale = torch.ones((), dtype=f32, device=dev)
+        self.n_skipped = torch.zeros((), dtype=f32, device=dev)
+        self._partials = torch.zeros(512, dtype=f32, device=dev)
+        self.X = torch.empty(L + 1, B, D, dtype=f32, device=dev)          # x_0 .. u_L
+        self.Xbf = torch.empty(L + 1, B, D, dtype=self.cdt, device=dev)
+        self.Hbf = torch.empty(L, B, H, dtype=self.cdt, device=dev)        # relu(h) per layer
+        self.O = torch.empty(L, B, 2 * D, dtype=self.cdt, device=dev)      # [mu | s_raw]
+        self.ldj = torch.empty(B, dtype=f32, device=dev)
+        self.nll_row = torch.empty(B, dtype=f32, device=dev)
+        self.gU = torch.empty(B, D, dtype=f32, device=dev)
+        self.gX = torch.empty(B, D, dtype=f32, device=dev)
+        self.dO = torch.empty(B, 2 * D, dtype=self.cdt, device=dev)
+        self.dH = torch.empty(B, H, dtype=self.cdt, device=dev)
+        self.noise = torch.empty(B, D, dtype=f32, device=dev)
+        if self.fp8:
+            from ..ops.fp8 import DelayedScale
+
+            e4 = torch.float8_e4m3fn
+            self.Xq = torch.empty(B, D, dtype=e4, device=dev)
+            self.Hq = torch.empty(B, H, dtype=e4, device=dev)
+            self.W1q = torch.empty(L * H, D, dtype=e4, device=dev)
+            self.W2q = torch.empty(L * 2 * D, H, dtype=e4, device=dev)
+            self.s1 = torch.empty(L * H, dtype=f32, device=dev)
+            self.s2 = torch.empty(L * 2 * D, dtype=f32, device=dev)
+            self.sx = [DelayedScale(dev) for _ in range(L)]   # input of layer l
+            self.sh = [DelayedScale(dev) for _ in range(L)]   # hidden of layer l
+            self._wq_fresh = False
+
+    def init_params(self, seed: int = 0):
+        cfg = self.cfg
+        g = torch.Generator(device="cpu").manual_seed(int(seed))
+        P = self.params
+        D, H = cfg.dim, cfg.hidden
+        for l in range(cfg.n_layers):
+            mk = self._mask(l)
+            a1 = 1.0 / math.sqrt(D)
+            W1 = (torch.rand(H, D, generator=g) * 2 - 1) * a1
+            b1 = (torch.rand(H, generator=g) * 2 - 1) * a1
+            W2 = torch.randn(2 * D, H, generator=g) * cfg.init_out_std / math.sqrt(H)
+            P.p(f"l{l}.W1").copy_(W1.to(self.device) * mk["M1"])
+            P.p(f"l{l}.b1").copy_(b1)
+            P.p(f"l{l}.W2").copy_(W2.to(self.device) * mk["M2"])
+            P.p(f"l{l}.b2").zero_()
+        P.sync_compute()
+        P.m.zero_()
+        P.v.zero_()
+        self.step_t.zero_()
+        self.rng_offset.zero_()
+        if self.fp8:
+            self._wq_fresh = False
+
+    # ------------------------------------------------------------------ data
+    def _sample_data(self):
+        """Fresh twisted-Gaussian samples on the device (Philox stream per rank and step)."""
+        cfg = self.cfg
+        x = self.X[0]
+        if self.data_override is not None:
+            x.copy_(self.data_override)
+            return
+        if self.device.type == "cuda":
+            fused.normal_fill(self.noise, seed=self.seed + 11, offset=self.rng_offset,
+                              stream_id=self.rank)
+        else:
+            g = torch.Generator().manual_seed(self.seed * 7919 + int(self.rng_offset.item()) * 31 +
+                                              self.rank)
+            self.noise.copy_(torch.randn(self.noise.shape, generator=g))
+        e = self.noise.view(self.B, -1, 2)
+        xv = x.view(self.B, -1, 2)
+        a = xv[:, :, 0]
+        torch.mul(e[:, :, 0], cfg.banana_sigma1, out=a)
+        torch.addcmul(torch.full_like(a, -cfg.banana_bend * cfg.banana_sigma1 ** 2), a, a,
+                      value=cfg.banana_bend, out=xv[:, :, 1])
+        xv[:, :, 1].add_(e[:, :, 1], alpha=cfg.banana_sigma2)
+
+    # ------------------------------------------------------------------ forward
+    def quantize_weights(self):
+        """Per-row e4m3 copies of every W1 / W2 (two strided launches over the flat buffer)."""
+        if not self.fp8:
+            return
+        from ..ops._ext import native
+
+        cfg, P = self.cfg, self.params
+        D, H, L = cfg.dim, cfg.hidden, cfg.n_layers
+        o1 = self.layout.slots["l0.W1"].offset
+        o2 = self.layout.slots["l0.W2"].offset
+        native().fp8_quant_rows_strided(P.master[o1:], self.layer_stride, H, L, D, self.W1q, self.s1)
+        native().fp8_quant_rows_strided(P.master[o2:], self.layer_stride, 2 * D, L, H, self.W2q,
+                                        self.s2)
+        self._wq_fresh = True
+
+    def forward(self):
+        cfg, P = self.cfg, self.params
+        D, H, L = cfg.dim, cfg.hidden, cfg.n_layers
+        self._sample_data()
+        self.Xbf[0].copy_(self.X[0])
+        if self.fp8:
+            from ..ops.fp8 import gemm_fp8
+
+            if not self._wq_fresh:
+                self.quantize_weights()
+            _, sxs = self.sx[0].quantize(self.X[0], out=self.Xq)
+        for l in range(L):
+            mk = self._mask(l)
+            b1, b2 = P.c(f"l{l}.b1"), P.c(f"l{l}.b2")
+            if self.fp8:
+                # h (bf16, kept for backward) and its e4m3 copy from one epilogue
+                _, sh = gemm_fp8(self.Xq, sxs, self.W1q[l * H:(l + 1) * H],
+                                 self.s1[l * H:(l + 1) * H], b1, relu=True, krange=mk["P1"].fwd,
+                                 out=self.Hbf[l], out_q=self.Hq, out_scale=self.sh[l])
+                gemm_fp8(self.Hq, sh, self.W2q[l * 2 * D:(l + 1) * 2 * D],
+                         self.s2[l * 2 * D:(l + 1) * 2 * D], b2, relu=False,
+                         krange=mk["P2"].fwd, out=self.O[l])
+            elif self.device.type == "cuda":
+                from ..ops._ext import native
+
+                native().masked_gemm_nt(self.Xbf[l], P.c(f"l{l}.W1"), b1, self.Hbf[l], 1, mk["P1"].fwd)
+                native().masked_gemm_nt(self.Hbf[l], P.c(f"l{l}.W2"), b2, self.O[l], 0, mk["P2"].fwd)
+            else:
+                gemm.linear_fwd(self.Xbf[l], P.c(f"l{l}.W1"), b1, self.Hbf[l], relu=True)
+                gemm.linear_fwd(self.Hbf[l], P.c(f"l{l}.W2"), b2, self.O[l], relu=False)
+            last = l == L - 1
+            nxt = None if (last or not self.fp8) else self.sx[l + 1]
+            fused.maf_fwd(self.X[l], self.O[l], self.X[l + 1], self.ldj, bound=cfg.alpha_bound,
+                          ubf=self.Xbf[l + 1], uq=self.Xq if nxt is not None else None,
+                          scale_state=nxt, ldj_init=(l == 0))
+            if nxt is not None:
+                sxs = nxt.scale
+        # NLL per row and dL/du_L
+        uL = self.X[L]
+        torch.sum(uL * uL, 1, out=self.nll_row)
+        self.nll_row.mul_(0.5).add_(0.5 * D * LOG2PI).sub_(self.ldj)
+        torch.mean(self.nll_row, 0, out=self.loss)
+        torch.mul(uL, 1.0 / self.B, out=self.gU)
+
+    # ------------------------------------------------------------------ backward
+    def backward(self):
+        cfg, P = self.cfg, self.params
+        L = cfg.n_layers
+        gpu = self.device.type == "cuda"
+        if gpu:
+            from ..ops._ext import native
+        gu, gx = self.gU, self.gX
+        for l in range(L - 1, -1, -1):
+            mk = self._mask(l)
+            fused.maf_bwd(gu, self.X[l + 1], self.O[l], self.dO, gx, bound=cfg.alpha_bound,
+                          c_ldj=1.0 / self.B)
+            W1c, W2c = P.c(f"l{l}.W1"), P.c(f"l{l}.W2")
+            if gpu:
+                native().masked_gemm_nn(self.dO, W2c, self.Hbf[l], self.dH, mk["P2"].bwd, False)
+                native().masked_gemm_nn(self.dH, W1c, None, gx, mk["P1"].bwd, True)
+                native().gemm_tn_group([self.dO, self.dH], [self.Hbf[l], self.Xbf[l]],
+                                       [P.g(f"l{l}.W2"), P.g(f"l{l}.W1")],
+                                       [P.g(f"l{l}.b2"), P.g(f"l{l}.b1")],
+                                       [mk["P2"].wskip, mk["P1"].wskip], [mk["M2u"], mk["M1u"]])
+            else:
+                gemm.linear_dgrad(self.dO, W2c, self.dH, relu_of=self.Hbf[l])
+                gemm.linear_dgrad(self.dH, W1c, gx, accumulate=True)
+                gemm.linear_wgrad_group([(self.dO, self.Hbf[l], P.g(f"l{l}.W2"), P.g(f"l{l}.b2")),
+                                         (self.dH, self.Xbf[l], P.g(f"l{l}.W1"), P.g(f"l{l}.b1"))])
+                P.g(f"l{l}.W2").mul_(mk["M2"])
+                P.g(f"l{l}.W1").mul_(mk["M1"])
+            gu, gx = gx, gu
+            if self.unit_ready_hook is not None:
+                self.unit_ready_hook(l)
+
+    # ------------------------------------------------------------------ optimizer / step
+    def optimizer_step(self):
+        P = self.params
+        fused.sumsq_guard(P.grad, self._partials, out_sumsq=self.gnorm2, skip=self.skip,
+                          scale=self.gscale, max_norm=self.max_grad_norm,
+                          base_scale=self.grad_scale_host)
+        b1, b2 = self.betas
+        fused.flat_optimizer(self.opt_kind, P.master, P.grad, P.m, P.v,
+                             pbf=None if P.compute is P.master else P.compute, lr=self.lr,
+                             b1=b1, b2=b2, eps=self.eps, wd=self.wd, step=self.step_t,
+                             gscale=self.gscale, skip=self.skip)
+        self.n_skipped.add_(self.skip)
+        if self.fp8:
+            self.quantize_weights()
+
+    def _update_schedule(self):
+        self.step_t.add_(1.0)
+        self.rng_offset.add_(1)
+
+    def train_step(self, reduce_fn=None):
+        self._update_schedule()
+        with trace_range("maf_forward"):
+            self.forward()
+        with trace_range("maf_backward"):
+            self.backward()
+        if reduce_fn is not None:
+            with trace_range("grad_allreduce_wait"):
+                reduce_fn()
+        with trace_range("optimizer"):
+            self.optimizer_step()
+
+    # ------------------------------------------------------------------ utils
+    def state_dict(self) -> dict:
+        return {"params": self.params.state_dict(), "step": self.step_t.detach().cpu(),
+                "rng_offset": self.rng_offset.detach().cpu(), "cfg": self.cfg.__dict__}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.params.load_state_dict(sd["params"])
+        self.step_t.copy_(sd["step"])
+        self.rng_offset.copy_(sd["rng_offset"])
+        if self.fp8:
+            self._wq_fresh = False

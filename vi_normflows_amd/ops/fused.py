@@ -96,3 +96,28 @@ def sumsq_guard(x, partial, out_sumsq=None, skip=None, scale=None, max_norm=0.0,
                              float(base_scale))
     else:
         ref.sumsq_guard(x, partial, out_sumsq, skip, scale, float(max_norm), float(base_scale))
+
+
+def maf_fwd(x, o, u, ldj, bound=5.0, ubf=None, uq=None, scale_state=None, ldj_init=False):
+    """MAF density-direction transform (csrc/kernels/maf.hip): u = (x - mu) exp(-alpha),
+    alpha = bound tanh(s_raw / bound), o = [mu | s_raw]; ldj (+)= -sum(alpha). Optional bf16
+    copy ``ubf`` and e4m3 copy ``uq`` (delayed per-tensor scale ``scale_state``, ops.fp8)."""
+    if _gpu(x):
+        if uq is not None:
+            st = scale_state
+            st.amax[0].copy_(st.amax[1])
+            st.amax[1].zero_()
+            native().maf_fwd(x, o, float(bound), u, ubf, uq, st.amax[0:1], st.scale, st.amax[1:2],
+                             ldj, bool(ldj_init))
+        else:
+            native().maf_fwd(x, o, float(bound), u, ubf, None, None, None, None, ldj, bool(ldj_init))
+    else:
+        ref.maf_fwd(x, o, float(bound), u, ubf, ldj, bool(ldj_init))
+
+
+def maf_bwd(gu, u, o, dout, gx, bound=5.0, c_ldj=0.0):
+    """d_o = [dL/dmu | dL/ds_raw] (bf16), gx = gu * exp(-alpha) (fp32, direct path)."""
+    if _gpu(gu):
+        native().maf_bwd(gu, u, o, float(bound), float(c_ldj), dout, gx)
+    else:
+        ref.maf_bwd(gu, u, o, float(bound), float(c_ldj), dout, gx)

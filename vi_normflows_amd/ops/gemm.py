@@ -89,7 +89,7 @@ def linear_wgrad_group(items) -> None:
         for c in range(0, len(items), 4):
             ch = items[c:c + 4]
             native().gemm_tn_group([i[0] for i in ch], [i[1] for i in ch], [i[2] for i in ch],
-                                   [i[3] for i in ch])
+                                   [i[3] for i in ch], [None] * len(ch), [None] * len(ch))
         return
     for dy, x, dW, db in items:
         linear_wgrad(dy, x, dW, db)

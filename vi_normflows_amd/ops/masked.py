@@ -82,19 +82,34 @@ def plan_for(mask: torch.Tensor) -> MaskPlan:
 
 
 class _MaskedLinearFn(torch.autograd.Function):
-    """bf16 MFMA masked linear with tile skipping (fp32 master weights, fp32 grads)."""
+    """MFMA masked linear with tile skipping (fp32 master weights, fp32 grads).
+
+    precision "bf16": every product on the bf16 kernels; "fp8": the forward product on the
+    e4m3 K=128 MX MFMA kernel (delayed per-tensor scale for x, per-row scales for W*M,
+    ops.fp8), backward in bf16.
+    """
 
     @staticmethod
-    def forward(ctx, x, W, b, mask):
+    def forward(ctx, x, W, b, mask, precision="bf16", act_scale=None):
         from ._ext import native
 
         plan = plan_for(mask)
         shp = x.shape
         x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
-        Wm = (W * mask).to(torch.bfloat16).contiguous()
+        Wm32 = W * mask
+        Wm = Wm32.to(torch.bfloat16).contiguous()
         bb = b.to(torch.bfloat16).contiguous() if b is not None else None
         y = torch.empty(x2.shape[0], W.shape[0], device=x.device, dtype=torch.bfloat16)
-        native().masked_gemm_nt(x2, Wm, bb, y, 0, plan.fwd)
+        if precision == "fp8" and shp[-1] % 128 == 0:
+            from .fp8 import DelayedScale, gemm_fp8, quantize_rows
+
+            if act_scale is None:
+                act_scale = DelayedScale(x.device)
+            xq, sx = act_scale.quantize(x2)
+            wq, sw = quantize_rows(Wm32.float().contiguous(), xq.shape[1])
+            gemm_fp8(xq, sx, wq, sw, bb, False, plan.fwd, out=y)
+        else:
+            native().masked_gemm_nt(x2, Wm, bb, y, 0, plan.fwd)
         ctx.save_for_backward(x2, Wm, mask)
         ctx.has_b = b is not None
         ctx.in_shape = shp
@@ -114,7 +129,7 @@ class _MaskedLinearFn(torch.autograd.Function):
         db = torch.empty(Wm.shape[0], device=gy.device, dtype=torch.float32) if ctx.has_b else None
         native().masked_gemm_tn(g2, x2, dW, db, plan.wskip)
         dW.mul_(mask)
-        return dx.to(ctx.out_dtype).reshape(ctx.in_shape), dW, db, None
+        return dx.to(ctx.out_dtype).reshape(ctx.in_shape), dW, db, None, None, None
 
 
 def kernel_ok(x, W) -> bool:
@@ -122,8 +137,10 @@ def kernel_ok(x, W) -> bool:
     return x.is_cuda and K % 32 == 0 and N % 32 == 0 and x.reshape(-1, K).shape[0] % 32 == 0
 
 
-def masked_linear(x, W, b, mask):
-    """x (W * mask)^T + b. GPU + MFMA-compatible shapes -> tile-skipping HIP GEMMs; else composite."""
+def masked_linear(x, W, b, mask, precision: str = "bf16", act_scale=None):
+    """x (W * mask)^T + b. GPU + MFMA-compatible shapes -> tile-skipping HIP GEMMs (bf16, or
+    fp8 forward with ``precision="fp8"``, ``act_scale`` an ops.fp8.DelayedScale); else the
+    composite."""
     if kernel_ok(x, W):
-        return _MaskedLinearFn.apply(x, W, b, mask)
+        return _MaskedLinearFn.apply(x, W, b, mask, precision, act_scale)
     return F.linear(x, W * mask, b)

@@ -169,3 +169,28 @@ def sumsq_guard(x, partial, out_sumsq, skip, scale, max_norm, base_scale):
             if nrm > max_norm:
                 sc *= max_norm / (nrm + 1e-6)
         scale.fill_(sc)
+
+
+# ---------------------------------------------------------------- MAF transform (maf.hip oracle)
+def maf_fwd(x, o, bound, u, ubf, ldj, ldj_init):
+    """u = (x - mu) exp(-alpha), alpha = bound tanh(s_raw / bound); ldj (+)= -sum(alpha)."""
+    D = x.shape[1]
+    mu, sr = o[:, :D].float(), o[:, D:2 * D].float()
+    al = bound * torch.tanh(sr / bound)
+    uv = (x - mu) * torch.exp(-al)
+    u.copy_(uv)
+    if ubf is not None:
+        ubf.copy_(uv.to(ubf.dtype))
+    if ldj_init:
+        ldj.copy_(-al.sum(1))
+    else:
+        ldj.sub_(al.sum(1))
+
+
+def maf_bwd(gu, u, o, bound, c_ldj, dout, gx):
+    D = gu.shape[1]
+    t = torch.tanh(o[:, D:2 * D].float() / bound)
+    ea = torch.exp(-bound * t)
+    gx.copy_(gu * ea)
+    dout[:, :D].copy_((-gu * ea).to(dout.dtype))
+    dout[:, D:2 * D].copy_(((c_ldj - gu * u) * (1 - t * t)).to(dout.dtype))
