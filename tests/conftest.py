@@ -38,3 +38,14 @@ def gpu():
 
     native()  # fail loudly if the HIP library is missing
     return torch.device("cuda")
+
+
+@pytest.fixture(autouse=True)
+def _gemm_backend_guard():
+    """No test may leak a GEMM backend change into later tests (GPU tests must exercise the
+    hand-written MFMA kernels unless they opt out explicitly)."""
+    from vi_normflows_amd.ops import gemm
+
+    prev = gemm.backend()
+    yield
+    assert gemm.backend() == prev, f"test changed the GEMM backend to {gemm.backend()}"

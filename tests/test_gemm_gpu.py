@@ -85,15 +85,18 @@ def test_engine_mfma_backend_matches_blas(gpu):
 
     cfg = RealNVPConfig(dim=784, n_layers=3, hidden=256, anneal="none", init_out_std=0.05)
     res = {}
-    for be in ("blas", "mfma"):
-        gemm.set_backend(be)
-        eng = RealNVPVI(cfg, batch=512, device=gpu, seed=7)
-        eng._update_schedule()
-        eng.forward()
-        eng.backward()
-        torch.cuda.synchronize()
-        res[be] = (eng.loss.item(), eng.params.grad.clone())
-    gemm.set_backend("blas")
+    prev = gemm.backend()
+    try:
+        for be in ("blas", "mfma"):
+            gemm.set_backend(be)
+            eng = RealNVPVI(cfg, batch=512, device=gpu, seed=7)
+            eng._update_schedule()
+            eng.forward()
+            eng.backward()
+            torch.cuda.synchronize()
+            res[be] = (eng.loss.item(), eng.params.grad.clone())
+    finally:
+        gemm.set_backend(prev)   # later tests must run on the MFMA kernels
     assert abs(res["blas"][0] - res["mfma"][0]) < 1e-2 * (1 + abs(res["blas"][0]))
     g0, g1 = res["blas"][1], res["mfma"][1]
     assert (g0 - g1).abs().max() <= 3e-2 * g0.abs().max()

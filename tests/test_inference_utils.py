@@ -175,6 +175,9 @@ def test_train_cli_tasks(tmp_path):
     assert math.isfinite(out["free_energy"])
     rec = [json.loads(l) for l in (tmp_path / "config2_realnvp8" / "metrics.jsonl").read_text().splitlines()]
     assert rec and "samples_per_s" in rec[-1]
+    out = main(["--config", "config5_maf64", "device=cpu", "iters=4", "batch=32", "dim=16",
+                "hidden=32", "K=2", "log_every=2", f"out_dir={tmp_path}"])
+    assert math.isfinite(out["nll"]) and out["precision"] == "fp32"
 
 
 def test_get_data_cli(capsys):

@@ -30,6 +30,7 @@ MI355X-first structure (no autograd tape on the hot path):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -154,10 +155,18 @@ class RealNVPVI:
         self.Act = torch.empty(L, cfg.n_hidden, B, H, dtype=self.cdt, device=dev)
         self.S = torch.empty(L, B, Dh, dtype=f32, device=dev)
         self.st = torch.empty(B, Np, dtype=self.cdt, device=dev)
-        self.dst = torch.empty(B, Np, dtype=self.cdt, device=dev)
-        # one input-gradient buffer per hidden layer: the grouped weight-gradient launch at the
-        # end of each layer's backward reads all of them
-        self.dH = [torch.empty(B, H, dtype=self.cdt, device=dev) for _ in range(max(cfg.n_hidden, 1))]
+        # gradient operands of the weight-gradient GEMMs, double-buffered by layer parity: the
+        # grouped weight-gradient launch of layer l runs on a side stream while layer l-1's
+        # backward chain (main stream) fills the other buffer set
+        self.dst2 = [torch.empty(B, Np, dtype=self.cdt, device=dev) for _ in range(2)]
+        self.dst = self.dst2[0]
+        # one input-gradient buffer per hidden layer (the grouped launch reads all of them)
+        self.dH2 = [[torch.empty(B, H, dtype=self.cdt, device=dev)
+                     for _ in range(max(cfg.n_hidden, 1))] for _ in range(2)]
+        self.dH = self.dH2[0]
+        self.wgrad_stream = None
+        if dev.type == "cuda" and os.environ.get("VINF_WGRAD_STREAM", "1") == "1":
+            self.wgrad_stream = torch.cuda.Stream(device=dev)
         self._G = torch.zeros(L + 2, B, Dp, dtype=f32, device=dev)   # dL/dh_i, 0-padded rows
         self.G = self._G[:, :, :Dh]
         self.logq0 = torch.empty(B, dtype=f32, device=dev)
@@ -294,24 +303,46 @@ class RealNVPVI:
         cfg, P = self.cfg, self.params
         L, nh = cfg.n_layers, cfg.n_hidden
         c = -1.0 / self.B
+        side = self.wgrad_stream
+        main = torch.cuda.current_stream(self.device) if side is not None else None
+        done = [None, None]          # side-stream event of the last wgrad launch per parity
         for l in range(L - 1, -1, -1):
-            fused.coupling_bwd(self.G[l + 2], self.S[l], self.h(l), self.dst, self.G[l], c=c,
+            par = l % 2
+            if done[par] is not None:
+                main.wait_event(done[par])      # WAR: wgrad(l+2) has read this buffer set
+            dst, dH = self.dst2[par], self.dH2[par]
+            fused.coupling_bwd(self.G[l + 2], self.S[l], self.h(l), dst, self.G[l], c=c,
                                scale=cfg.scale_bound, gx_accumulate=False)
-            d = self.dst
+            d = dst
             wg = []
             for i in range(nh, -1, -1):
                 inp = self.Act[l, i - 1] if i > 0 else self.Hbf[l]
                 wg.append((d, inp, P.g(f"l{l}.W{i}"), P.g(f"l{l}.b{i}")))
                 if i > 0:
-                    nd = self.dH[i - 1]
+                    nd = dH[i - 1]
                     gemm.linear_dgrad(d, P.c(f"l{l}.W{i}"), nd, relu_of=self.Act[l, i - 1])
                     d = nd
                 else:
                     gemm.linear_dgrad(d, P.c(f"l{l}.W0"), self._G[l + 1], accumulate=True)
-            # the layer's weight gradients after its input-gradient chain: one grouped launch
-            gemm.linear_wgrad_group(wg)
-            if self.unit_ready_hook is not None:
-                self.unit_ready_hook(l + 1)
+            # the layer's weight gradients: one grouped launch, off the critical path
+            if side is not None:
+                ready = torch.cuda.Event()
+                ready.record(main)
+                side.wait_event(ready)
+                with torch.cuda.stream(side):
+                    gemm.linear_wgrad_group(wg)
+                    if self.unit_ready_hook is not None:
+                        self.unit_ready_hook(l + 1)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                done[par] = ev
+            else:
+                gemm.linear_wgrad_group(wg)
+                if self.unit_ready_hook is not None:
+                    self.unit_ready_hook(l + 1)
+        for ev in done:
+            if ev is not None:
+                main.wait_event(ev)
         self._base_backward()
         if self.unit_ready_hook is not None:
             self.unit_ready_hook(0)

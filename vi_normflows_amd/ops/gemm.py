@@ -34,7 +34,10 @@ def backend() -> str:
 
 
 def _mfma_ok(*ts) -> bool:
-    return _BACKEND == "mfma" and all(t is None or t.is_cuda for t in ts)
+    """The hand-written MFMA kernels take bf16 GPU operands; fp32 compute (tests, CPU) takes
+    the torch path."""
+    return _BACKEND == "mfma" and all(t is None or (t.is_cuda and t.dtype == torch.bfloat16)
+                                      for t in ts)
 
 
 def linear_fwd(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, out: torch.Tensor,

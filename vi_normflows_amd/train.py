@@ -151,13 +151,40 @@ def run_iaf_vae(cfg, out, info, logger):
 
 
 def run_maf(cfg, out, info, logger):
+    """MAF density estimation. ``extra.impl``: "engine" (default: flat-buffer explicit-backward
+    engine, fp8/bf16 forward, DP runner + hipGraph) or "module" (autograd MAFDensity)."""
+    dev = _device(cfg, info)
+    if cfg.extra.get("impl", "engine") == "engine":
+        from .models.maf_engine import MAFEngine, MAFEngineConfig
+        from .parallel.runner import DataParallelRunner
+        from .utils.checkpoint import save_engine
+
+        mc = MAFEngineConfig(dim=cfg.dim, n_layers=cfg.K, hidden=cfg.hidden,
+                             precision=cfg.extra.get("precision", "fp8"))
+        eng = MAFEngine(mc, batch=cfg.batch, device=dev, seed=cfg.seed, rank=info.rank, lr=cfg.lr)
+        run = DataParallelRunner(eng, info)
+        if dev.type == "cuda" and cfg.extra.get("graph", True):
+            run.capture(warmup=1)
+        t0 = time.perf_counter()
+        for t in range(cfg.iters):
+            run.step()
+            if t % cfg.log_every == 0 or t == cfg.iters - 1:
+                el = time.perf_counter() - t0
+                logger.log({"step": t, "nll": float(eng.loss.item()),
+                            "grad_norm": math.sqrt(max(float(eng.gnorm2.item()), 0.0)),
+                            "samples_per_s": (t + 1) * cfg.batch * info.world / el})
+        save_engine(eng, out / "ckpt.pt", info.rank)
+        vdist.barrier()
+        return {"nll": float(eng.loss.item()), "nll_floor_entropy": mc.entropy(),
+                "precision": mc.precision if dev.type == "cuda" else "fp32"}
+
     from .inference.elbo import FreeEnergy
     from .inference.trainer import TrainConfig, Trainer
     from .models.maf_density import MAFConfig, MAFDensity, banana_entropy, banana_samples
 
-    dev = _device(cfg, info)
     model = MAFDensity(MAFConfig(dim=cfg.dim, n_layers=cfg.K, hidden=cfg.hidden,
-                                 n_hidden=cfg.n_hidden)).to(dev)
+                                 n_hidden=cfg.n_hidden,
+                                 precision=cfg.extra.get("precision", "bf16"))).to(dev)
     g = torch.Generator().manual_seed(rank_seed(cfg.seed, info.rank))
 
     def loss_fn(t, beta):

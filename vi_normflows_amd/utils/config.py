@@ -86,7 +86,8 @@ PRESETS: dict[str, RunConfig] = {
                                    dim=3072, hidden=1024, dim_z=256, batch=1024, iters=200,
                                    lr=3e-4),
     "config5_maf64": RunConfig(name="config5_maf64", task="maf_density", device="cuda", K=64,
-                               dim=1024, hidden=1024, n_hidden=1, batch=1024, iters=200, lr=1e-4),
+                               dim=1024, hidden=1024, n_hidden=1, batch=8192, iters=200, lr=1e-4,
+                               extra={"precision": "fp8", "impl": "engine"}),
     "mnist_planar_vae": RunConfig(name="mnist_planar_vae", task="planar_vae", device="auto", K=4,
                                   dim=784, hidden=64, n_hidden=3, dim_z=40, batch=128,
                                   iters=10000, lr=1e-3, schedule="reference"),
