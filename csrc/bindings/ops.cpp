@@ -94,7 +94,8 @@ void coupling_bwd(const at::Tensor& gy, const at::Tensor& s, const at::Tensor& x
   check_2d(dst, "dst");
   check_2d(gx, "gx");
   check_dtype(gy, at::kFloat, "gy");
-  check_dtype(s, at::kFloat, "s");
+  const bool shat = s.scalar_type() == at::kBFloat16;   // s_hat (bf16 conditioner output)
+  TORCH_CHECK(shat || s.scalar_type() == at::kFloat, "s: fp32 s or bf16 s_hat");
   check_dtype(x, at::kFloat, "x");
   check_dtype(gx, at::kFloat, "gx");
   TORCH_CHECK(dst.scalar_type() == at::kBFloat16 || dst.scalar_type() == at::kFloat, "dst dtype");
@@ -106,7 +107,10 @@ void coupling_bwd(const at::Tensor& gy, const at::Tensor& s, const at::Tensor& x
     check_dtype(*c_row, at::kFloat, "c_row");
     TORCH_CHECK(c_row->numel() == B && c_row->is_contiguous(), "c_row");
   }
-  nf_launch_coupling_bwd(gy.data_ptr<float>(), ld_of(gy), s.data_ptr<float>(), ld_of(s),
+  TORCH_CHECK(!shat || (Dh % 4 == 0 && ld_of(s) % 4 == 0 &&
+                        reinterpret_cast<uintptr_t>(s.data_ptr()) % 8 == 0),
+              "s_hat input needs Dh % 4 == 0 and 8-B aligned rows");
+  nf_launch_coupling_bwd(s.data_ptr(), shat, ld_of(s), gy.data_ptr<float>(), ld_of(gy),
                          x.data_ptr<float>(), ld_of(x), (float)c, opt_ptr<float>(c_row),
                          dst.data_ptr(), dst.scalar_type() == at::kBFloat16, ld_of(dst),
                          gx.data_ptr<float>(), ld_of(gx), B, Dh,

@@ -11,10 +11,12 @@ void nf_launch_coupling_fwd(const void* st, int st_is_bf16, long ld_st_, const f
                             float* y, long ld_y, void* ybf, int ybf_is_bf16, long ld_yb,
                             float* ssav, long ld_s, float* ldj, int B, int Dh, float scale,
                             int inverse, int ldj_init, int yb_width, hipStream_t stream);
-void nf_launch_coupling_bwd(const float* gy, long ld_gy, const float* s, long ld_s, const float* x,
-                            long ld_x, float c_scalar, const float* c_row, void* dst,
-                            int dst_is_bf16, long ld_dst, float* gx, long ld_gx, int B, int Dh,
-                            float scale, int gx_accumulate, int dst_pad_to, hipStream_t stream);
+// s: saved fp32 s, or (s_is_shat_bf16) the bf16 conditioner output s_hat (s recomputed)
+void nf_launch_coupling_bwd(const void* s, int s_is_shat_bf16, long ld_s, const float* gy,
+                            long ld_gy, const float* x, long ld_x, float c_scalar,
+                            const float* c_row, void* dst, int dst_is_bf16, long ld_dst, float* gx,
+                            long ld_gx, int B, int Dh, float scale, int gx_accumulate,
+                            int dst_pad_to, hipStream_t stream);
 
 // elbo.hip
 void nf_launch_target_logp_grad(int kind, const float* A, long lda, const float* Bh, long ldb,

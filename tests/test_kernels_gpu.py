@@ -57,6 +57,24 @@ def test_coupling_bwd(gpu, B, Dh, acc, use_row):
     _close(res[0][1], res[1][1], 2e-5)
 
 
+@pytest.mark.parametrize("B,Dh", [(64, 392), (7, 100)])
+def test_coupling_bwd_from_s_hat(gpu, B, Dh):
+    """Backward fed the bf16 conditioner output s_hat (s recomputed in-kernel) == backward fed
+    s = scale * tanh(s_hat)."""
+    torch.manual_seed(4)
+    st = (torch.randn(B, 2 * Dh + 8, device=gpu) * 0.7).to(torch.bfloat16)
+    gy, x = torch.randn(B, Dh, device=gpu), torch.randn(B, Dh, device=gpu)
+    s = 1.3 * torch.tanh(st[:, :Dh].float())
+    out = []
+    for sin in (st[:, :Dh], s):
+        dst = torch.empty(B, 2 * Dh, device=gpu, dtype=torch.bfloat16)
+        gx = torch.empty(B, Dh, device=gpu)
+        torch.ops.vinf.coupling_bwd(gy, sin, x, -0.25, None, dst, gx, 1.3, False)
+        out.append((dst.float(), gx))
+    assert (out[0][0] - out[1][0]).abs().max() <= 1e-2 * out[1][0].abs().max()
+    assert torch.allclose(out[0][1], out[1][1], rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("kind", [0, 1])
 @pytest.mark.parametrize("B,Dh", [(5, 2), (40, 392)])
 def test_target_logp_grad(gpu, kind, B, Dh):

@@ -153,8 +153,10 @@ class RealNVPVI:
         Dp, Np = cfg.half_pad, cfg.out_pad
         self.Hbf = torch.empty(L, B, Dp, dtype=self.cdt, device=dev)    # bf16(h_1 .. h_L), 0-padded
         self.Act = torch.empty(L, cfg.n_hidden, B, H, dtype=self.cdt, device=dev)
-        self.S = torch.empty(L, B, Dh, dtype=f32, device=dev)
-        self.st = torch.empty(B, Np, dtype=self.cdt, device=dev)
+        # per-layer conditioner outputs [s_hat | t] (compute dtype): the backward recomputes
+        # s = scale * tanh(s_hat) from them instead of reading a saved fp32 s
+        self.ST = torch.empty(L, B, Np, dtype=self.cdt, device=dev)
+        self.st = self.ST[0]
         # gradient operands of the weight-gradient GEMMs, double-buffered by layer parity: the
         # grouped weight-gradient launch of layer l runs on a side stream while layer l-1's
         # backward chain (main stream) fills the other buffer set
@@ -260,8 +262,9 @@ class RealNVPVI:
             out = self.Act[l, i]
             gemm.linear_fwd(a, P.c(f"l{l}.W{i}"), P.c(f"l{l}.b{i}"), out, relu=True)
             a = out
-        gemm.linear_fwd(a, P.c(f"l{l}.W{nh}"), P.c(f"l{l}.b{nh}"), self.st, relu=False)
-        return self.st
+        st = self.ST[l]
+        gemm.linear_fwd(a, P.c(f"l{l}.W{nh}"), P.c(f"l{l}.b{nh}"), st, relu=False)
+        return st
 
     def forward(self):
         cfg, P = self.cfg, self.params
@@ -275,7 +278,7 @@ class RealNVPVI:
         for l in range(L):
             st = self._conditioner_fwd(l, self.Hbf[l])
             ybf = self.Hbf[l + 1] if l + 1 < L else None
-            fused.coupling_fwd(st, self.h(l), self.h(l + 2), ybf=ybf, ssav=self.S[l],
+            fused.coupling_fwd(st, self.h(l), self.h(l + 2), ybf=ybf, ssav=None,
                                ldj=self.ldj, scale=cfg.scale_bound, inverse=False,
                                ldj_init=(l == 0))
         A, Bh, ia, ib = self.zK_halves()
@@ -311,8 +314,8 @@ class RealNVPVI:
             if done[par] is not None:
                 main.wait_event(done[par])      # WAR: wgrad(l+2) has read this buffer set
             dst, dH = self.dst2[par], self.dH2[par]
-            fused.coupling_bwd(self.G[l + 2], self.S[l], self.h(l), dst, self.G[l], c=c,
-                               scale=cfg.scale_bound, gx_accumulate=False)
+            fused.coupling_bwd(self.G[l + 2], self.ST[l][:, :cfg.half], self.h(l), dst, self.G[l],
+                               c=c, scale=cfg.scale_bound, gx_accumulate=False, s_is_hat=True)
             d = dst
             wg = []
             for i in range(nh, -1, -1):

@@ -35,7 +35,12 @@ def coupling_fwd(st, x, y, ybf=None, ssav=None, ldj=None, scale=1.0, inverse=Fal
         ref.coupling_fwd(st, x, y, ybf, ssav, ldj, float(scale), bool(inverse), bool(ldj_init))
 
 
-def coupling_bwd(gy, s, x, dst, gx, c=0.0, c_row=None, scale=1.0, gx_accumulate=False):
+def coupling_bwd(gy, s, x, dst, gx, c=0.0, c_row=None, scale=1.0, gx_accumulate=False,
+                 s_is_hat=False):
+    """``s``: the saved s, or with ``s_is_hat`` the conditioner output s_hat (s = scale *
+    tanh(s_hat) is recomputed; bf16 s_hat goes straight to the kernel)."""
+    if s_is_hat and not (_gpu(x) and s.dtype == torch.bfloat16):
+        s = scale * torch.tanh(s.float())
     if _gpu(x):
         native().coupling_bwd(gy, s, x, float(c), c_row, dst, gx, float(scale),
                               bool(gx_accumulate))
