@@ -28,4 +28,9 @@ case "$mode" in
   *) echo "usage: $0 trace|pmc|markers OUT [COUNTERS] -- CMD..."; exit 2 ;;
 esac
 cd "$repo"
-python3 -m vi_normflows_amd.bench.prof_summary "$out" > "$out/summary.txt" 2>/dev/null && cat "$out/summary.txt"
+if [ "$mode" == "pmc" ]; then
+  python3 -m vi_normflows_amd.bench.pmc_summary "$out" > "$out/summary.txt" 2>/dev/null && cat "$out/summary.txt"
+else
+  python3 -m vi_normflows_amd.bench.prof_summary "$out" > "$out/summary.txt" 2>/dev/null && cat "$out/summary.txt"
+fi
+exit 0

@@ -10,7 +10,7 @@
 // Tile: 128x128 output, 128-byte K step - byte-for-byte the LDS image of the bf16 kernel
 // (128 rows x 128 B, 16-B chunks XOR-swizzled by row, filled by LDS-DMA, conflict-free
 // fragment reads by the same argument as gemm.hip's k-major image). Each lane's A/B fragment is 32
-// consecutive k-bytes (two ds_read_b128); the MFMA's k order is a permutation applied
+// k-bytes (two ds_read_b128 of chunks g, g+4); the MFMA's k order is a permutation applied
 // identically to both operands, so the dot products are exact whatever the hardware's
 // internal k interleave (the row/column lane maps and C/D layout are the bf16 ones).
 // MADE tile skipping: per N-tile K ranges (rounded out to 128; columns outside the mask's
@@ -164,10 +164,13 @@ __device__ __forceinline__ void stage(const unsigned char* __restrict__ base, lo
   }
 }
 
+// Lane group g = lane >> 4 takes the 16-B chunks g and g + 4 of its row (32 k-bytes). Reading
+// chunk pairs (2g, 2g+1) instead costs 4 bank-conflict cycles per LDS cycle (PMC,
+// profiles/r1_pmc_gemm256_group_fp8.txt); (g, g+4) is the bf16 kernel's conflict-free pattern.
 __device__ __forceinline__ v8i read_frag(const char* tile, int r0, int lane) {
   const int r = r0 + (lane & 15), g = lane >> 4;
-  const v4i lo = *(const LDS_AS v4i*)(tile + r * 128 + (((2 * g) ^ (r & 7)) << 4));
-  const v4i hi = *(const LDS_AS v4i*)(tile + r * 128 + (((2 * g + 1) ^ (r & 7)) << 4));
+  const v4i lo = *(const LDS_AS v4i*)(tile + r * 128 + ((g ^ (r & 7)) << 4));
+  const v4i hi = *(const LDS_AS v4i*)(tile + r * 128 + (((g + 4) ^ (r & 7)) << 4));
   return (v8i){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 

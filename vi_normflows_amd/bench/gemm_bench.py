@@ -47,6 +47,7 @@ def main():
               ("wgrad_l3", "tn", 800, 1024, B), ("wgrad_l2", "tn", 1024, 1024, B),
               ("wgrad_l1", "tn", 1024, 416, B),
               ("wgrad_group", "tn_group", 0, 0, B),
+              ("fwd_l2_fp8", "nt_fp8", B, 1024, 1024), ("sq4096_fp8", "nt_fp8", 4096, 4096, 4096),
               ("sq4096", "nt", 4096, 4096, 4096), ("fwd_k4096", "nt", B, 1024, 4096),
               ("fwd_k2048", "nt", B, 1024, 2048), ("fwd_m64k", "nt", 65536, 1024, 1024)]
     if a.only:
@@ -73,6 +74,18 @@ def main():
                 y = torch.zeros(M, N, device=dev)
                 mine = lambda: ops.gemm_nn(dy, W, None, y, True)
                 ref = lambda: y.add_(torch.mm(dy, W, out_dtype=torch.float32))
+        elif kind == "nt_fp8":     # e4m3 operands, MX K=128 MFMA (ops.fp8) vs bf16 hipBLASLt
+            from vi_normflows_amd.ops.fp8 import gemm_fp8, quantize_rows
+
+            xf = torch.randn(M, K, device=dev)
+            Wf = torch.randn(N, K, device=dev) * 0.05
+            xq, sx = quantize_rows(xf)
+            wq, sw = quantize_rows(Wf)
+            b = torch.randn(N, device=dev).to(bf)
+            y = torch.empty(M, N, device=dev, dtype=bf)
+            x, W = xf.to(bf), Wf.to(bf)
+            mine = lambda: gemm_fp8(xq, sx, wq, sw, b, True, out=y)
+            ref = lambda: torch.relu_(torch.addmm(b, x, W.t(), out=y))
         elif kind == "tn_group":   # the three weight gradients of one conditioner
             its = []
             for (m_, n_) in [(800, 1024), (1024, 1024), (1024, 416)]:
