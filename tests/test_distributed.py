@@ -49,18 +49,19 @@ def _worker(rank, world, port, eps_all, out_dir, bucket_mb, compress):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bucket_mb,compress", [(0.001, False), (64.0, False), (0.001, True)])
-def test_dp_gradient_equals_single_process(tmp_path, bucket_mb, compress):
-    world = 2
+@pytest.mark.parametrize("world,bucket_mb,compress", [(2, 0.001, False), (2, 64.0, False),
+                                                     (2, 0.001, True), (4, 0.001, False)])
+def test_dp_gradient_equals_single_process(tmp_path, world, bucket_mb, compress):
     torch.manual_seed(0)
     eps_all = torch.randn(world * B, CFG["dim"])
     mp.spawn(_worker, args=(world, _free_port(), eps_all, str(tmp_path), bucket_mb, compress),
              nprocs=world, join=True)
     r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
-    r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
-    # rank 1 started from a different seed but received rank 0's parameters by broadcast
-    assert torch.equal(r0["master"], r1["master"])
-    assert torch.allclose(r0["grad"], r1["grad"])
+    for r in range(1, world):
+        rr = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
+        # rank r started from a different seed but received rank 0's parameters by broadcast
+        assert torch.equal(r0["master"], rr["master"])
+        assert torch.allclose(r0["grad"], rr["grad"])
     single = RealNVPVI(RealNVPConfig(**CFG), batch=world * B, device="cpu", seed=100)
     single.params.master.copy_(r0["master"])
     single.params.sync_compute()

@@ -19,7 +19,7 @@ def _grads(fn, inputs):
 
 
 @pytest.mark.parametrize("N,D,K", [(1000, 2, 8), (257, 1, 3), (300, 5, 4), (64, 16, 2),
-                                   (40, 40, 4), (17, 300, 3), (8, 1024, 2)])
+                                   (40, 40, 4), (17, 300, 3), (8, 1024, 2), (1, 3, 2)])
 @pytest.mark.parametrize("per_sample", [False, True])
 @pytest.mark.parametrize("variant", ["paper", "reference"])
 def test_planar_stack_kernel(gpu, N, D, K, per_sample, variant):
@@ -45,7 +45,7 @@ def test_planar_stack_kernel(gpu, N, D, K, per_sample, variant):
         assert (ga - gb).abs().max() <= 2e-3 * (1 + gb.abs().max()), (ga - gb).abs().max()
 
 
-@pytest.mark.parametrize("N,D,K", [(1000, 2, 6), (100, 9, 3), (33, 128, 2), (5, 700, 2)])
+@pytest.mark.parametrize("N,D,K", [(1000, 2, 6), (100, 9, 3), (33, 128, 2), (5, 700, 2), (1, 2, 3)])
 @pytest.mark.parametrize("per_sample", [False, True])
 def test_radial_stack_kernel(gpu, N, D, K, per_sample):
     torch.manual_seed(N + D)
