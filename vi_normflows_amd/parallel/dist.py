@@ -46,12 +46,15 @@ def init(backend: str | None = None, device_type: str | None = None) -> DistInfo
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if device_type == "cuda":
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        # one process per GPU; more ranks than GPUs (rehearsing a multi-rank run on a smaller
+        # box) wrap around - RCCL refuses two ranks on one GPU, so use VINF_DIST_BACKEND=gloo then
+        idx = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(idx)
+        device = torch.device("cuda", idx)
     else:
         device = torch.device("cpu")
     if backend is None:
-        backend = "nccl" if device_type == "cuda" else "gloo"
+        backend = os.environ.get("VINF_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
@@ -82,7 +85,7 @@ def info() -> DistInfo:
 def barrier() -> None:
     if dist.is_initialized():
         if _INFO.backend == "nccl":
-            dist.barrier(device_ids=[_INFO.local_rank])
+            dist.barrier(device_ids=[_INFO.device.index if _INFO.device.index is not None else _INFO.local_rank])
         else:
             dist.barrier()
 
