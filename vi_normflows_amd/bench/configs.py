@@ -17,7 +17,9 @@ import torch
 
 from ..parallel import dist as vdist
 
-NAMES = {1: "2D two-moons planar-flow VI on CPU (plumbing, no GPU)",
+NAMES = {0: "reference main workload: MNIST-shape planar-flow VAE (784-64x3, dz=40, K=4), "
+            "synthetic binary data",
+         1: "2D two-moons planar-flow VI on CPU (plumbing, no GPU)",
          2: "8-layer RealNVP on 784-dim synthetic (MNIST-shape), bf16, 1xMI355X",
          3: "32-layer RealNVP on 784-dim synthetic, DP over xGMI (see bench.py)",
          4: "IAF-10 amortized VI (VAE encoder) on 3x32x32 synthetic",
@@ -49,6 +51,35 @@ def graphed(step_fn, dev, warmup: int = 3):
 def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: bool = True,
           impl: str = "engine"):
     dev = info.device
+    if cfg_id == 0:
+        # src/learning_mnist.py: K=4, dz=40, 784 -> 64x3 -> 2dz+2dz*K+K, Adam lr 1e-3, batch 128
+        from ..models.vae import PlanarVAE, VAEConfig, synthetic_binary_images
+
+        B = batch or 128
+        model = PlanarVAE(VAEConfig(dim_x=784, dim_z=40, K=4, width=64, hidden_layers=3))
+        model.init_reference(generator=torch.Generator().manual_seed(0))
+        model = model.to(dev)
+        X = synthetic_binary_images(max(2000, 4 * B), 784, seed=info.rank).to(dev)
+        use_graph = graph and dev.type == "cuda" and info.world == 1
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, capturable=use_graph)
+        xs = X[:B].clone()
+        it = [0]
+
+        def compute():
+            F = model.loss(xs, 1.0, with_stats=False).F
+            opt.zero_grad(set_to_none=True)
+            F.backward()
+            opt.step()
+
+        g = graphed(compute, dev) if use_graph else None
+
+        def step():
+            i = it[0] % (X.shape[0] // B)
+            it[0] += 1
+            xs.copy_(X[i * B:(i + 1) * B])
+            g.replay() if g is not None else compute()
+        return step, B, dev, "fp32 (flat-vector MLPs) + fused per-sample planar HIP kernels" + (
+            ", hipGraph" if use_graph else "")
     if cfg_id == 1:
         from ..distributions.base import StdNormal
         from ..distributions.energies import get_target
@@ -185,10 +216,11 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--precision", default="fp8", choices=["fp8", "bf16"], help="config 5 GEMMs")
     ap.add_argument("--graph", default="on", choices=["on", "off"])
+    ap.add_argument("--cpu", action="store_true", help="config 0 on the CPU")
     ap.add_argument("--impl", default="engine", choices=["engine", "module"],
                     help="config 5: explicit-backward MAF engine or the autograd MAFDensity module")
     a = ap.parse_args(argv)
-    info = vdist.init(device_type="cpu" if a.config == 1 else None)
+    info = vdist.init(device_type="cpu" if a.config == 1 or (a.config == 0 and a.cpu) else None)
     step, B, dev, dtype = build(a.config, info, a.batch, a.precision, a.graph == "on", a.impl)
     for _ in range(a.warmup):
         step()

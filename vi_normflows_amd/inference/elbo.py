@@ -59,7 +59,8 @@ def reference_free_energy(flow, density, n_samples: int, dim: int, generator=Non
     return FreeEnergy(F, _stats(lq0.detach(), ldj.detach(), lp.detach(), 1.0))
 
 
-def amortized_free_energy(x, encode, flow, log_joint, beta: float = 1.0, generator=None):
+def amortized_free_energy(x, encode, flow, log_joint, beta: float = 1.0, generator=None,
+                          with_stats: bool = True):
     """Amortized VI: (mu, logvar, flow_params) = encode(x); z0 ~ N(mu, diag(exp(logvar)));
     z_K = flow(z0, flow_params); F = mean(log q0(z0) - ldj - beta log p(x, z_K))."""
     mu, logvar, fparams = encode(x)
@@ -72,7 +73,8 @@ def amortized_free_energy(x, encode, flow, log_joint, beta: float = 1.0, generat
         zK, ldj = z0, torch.zeros(z0.shape[0], device=z0.device)
     lp = log_joint(x, zK)
     F = (lq0 - ldj - beta * lp).mean()
-    return FreeEnergy(F, _stats(lq0.detach(), ldj.detach(), lp.detach(), beta)), zK
+    st = _stats(lq0.detach(), ldj.detach(), lp.detach(), beta) if with_stats else {}
+    return FreeEnergy(F, st), zK
 
 
 def importance_log_likelihood(x, encode, flow, log_joint, n_importance: int = 64):

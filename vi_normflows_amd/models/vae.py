@@ -84,8 +84,9 @@ class PlanarVAE(nn.Module):
     def log_joint(self, x, z):
         return log_bern_logits(x, self.decode_logits(z)) + log_std_norm(z)
 
-    def loss(self, x, beta: float = 1.0, generator=None):
-        res, _ = amortized_free_energy(x, self.encode, self.flow, self.log_joint, beta, generator)
+    def loss(self, x, beta: float = 1.0, generator=None, with_stats: bool = True):
+        res, _ = amortized_free_energy(x, self.encode, self.flow, self.log_joint, beta, generator,
+                                       with_stats)
         return res
 
     @torch.no_grad()
