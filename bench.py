@@ -41,7 +41,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("VINF_BENCH_BATCH", 16384)),
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("VINF_BENCH_BATCH", 32768)),
                     help="per-GPU ELBO samples per step")
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--dim", type=int, default=784)

@@ -80,7 +80,7 @@ PRESETS: dict[str, RunConfig] = {
                                   K=8, dim=784, hidden=1024, batch=16384, iters=200, lr=1e-4,
                                   schedule="reference"),
     "config3_realnvp32_dp8": RunConfig(name="config3_realnvp32_dp8", task="realnvp_vi",
-                                       device="cuda", K=32, dim=784, hidden=1024, batch=16384,
+                                       device="cuda", K=32, dim=784, hidden=1024, batch=32768,
                                        iters=200, lr=1e-4, schedule="reference"),
     "config4_iaf10_vae": RunConfig(name="config4_iaf10_vae", task="iaf_vae", device="cuda", K=10,
                                    dim=3072, hidden=1024, dim_z=256, batch=1024, iters=200,
