@@ -73,6 +73,50 @@ __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ base, long
   }
 }
 
+
+// Per-lane LDS-DMA source pointers of one operand tile at k = k0, without the K clamp: valid
+// for every full tile (k0 + BK <= K), reached by adding `step` per K-tile. The per-tile
+// address arithmetic of stage_tile (row/K clamps, 64-bit multiplies: ~80 VALU per K-tile)
+// then runs once per block; only a tail tile takes the clamped path.
+template <bool KMAJOR>
+struct TilePtrs {
+  const bf16_t* p[4];
+  long step;
+};
+
+template <bool KMAJOR>
+__device__ __forceinline__ void tile_ptrs(TilePtrs<KMAJOR>& t, const bf16_t* __restrict__ base,
+                                          long ld, int row0, int rows_total, int k0, int wave,
+                                          int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wave * 4 + i;
+    if (KMAJOR) {
+      const int r = piece * 8 + (lane >> 3);
+      const int lc = (lane & 7) ^ (r & 7);
+      int gr = row0 + r;
+      gr = gr < rows_total ? gr : rows_total - 1;
+      t.p[i] = base + (long)gr * ld + k0 + lc * 8;
+    } else {
+      const int kr = piece * 4 + (lane >> 4);
+      const int lc = (lane & 15) ^ mn_swz(kr);
+      int gm = row0 + lc * 8;
+      gm = gm < rows_total ? gm : rows_total - 8;
+      t.p[i] = base + (long)(k0 + kr) * ld + gm;
+    }
+  }
+  t.step = KMAJOR ? (long)BK : (long)BK * ld;
+}
+
+template <bool KMAJOR>
+__device__ __forceinline__ void stage_ptrs(const TilePtrs<KMAJOR>& t, long off, char* lds_tile,
+                                           int wave) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    __builtin_amdgcn_global_load_lds((const void*)(t.p[i] + off),
+                                     (LDS_AS void*)(lds_tile + (wave * 4 + i) * 1024), 16, 0, 0);
+}
+
 template <bool A_KMAJOR, bool B_KMAJOR, int EPI>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a, int wg, int split, char* smem) {
   const int lane = threadIdx.x & 63;
@@ -107,9 +151,19 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, int wg, int split, 
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;
 
+  TilePtrs<A_KMAJOR> ta;
+  TilePtrs<B_KMAJOR> tb;
+  tile_ptrs<A_KMAJOR>(ta, a.A, a.lda, m0, a.M, kbeg, wave, lane);
+  tile_ptrs<B_KMAJOR>(tb, a.B, a.ldb, n0, a.N, kbeg, wave, lane);
+  long offa = 0, offb = 0;
   if (nkt > 0) {
-    stage_tile<A_KMAJOR>(a.A, a.lda, m0, a.M, kbeg, a.K, smem, wave, lane);
-    stage_tile<B_KMAJOR>(a.B, a.ldb, n0, a.N, kbeg, a.K, smem + TILE_BYTES, wave, lane);
+    if (kbeg + BK <= a.K) {
+      stage_ptrs<A_KMAJOR>(ta, 0, smem, wave);
+      stage_ptrs<B_KMAJOR>(tb, 0, smem + TILE_BYTES, wave);
+    } else {
+      stage_tile<A_KMAJOR>(a.A, a.lda, m0, a.M, kbeg, a.K, smem, wave, lane);
+      stage_tile<B_KMAJOR>(a.B, a.ldb, n0, a.N, kbeg, a.K, smem + TILE_BYTES, wave, lane);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -118,8 +172,15 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, int wg, int split, 
     if (kt + 1 < nkt) {
       char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
       const int k0 = kbeg + (kt + 1) * BK;
-      stage_tile<A_KMAJOR>(a.A, a.lda, m0, a.M, k0, a.K, nxt, wave, lane);
-      stage_tile<B_KMAJOR>(a.B, a.ldb, n0, a.N, k0, a.K, nxt + TILE_BYTES, wave, lane);
+      offa += ta.step;
+      offb += tb.step;
+      if (k0 + BK <= a.K) {
+        stage_ptrs<A_KMAJOR>(ta, offa, nxt, wave);
+        stage_ptrs<B_KMAJOR>(tb, offb, nxt + TILE_BYTES, wave);
+      } else {
+        stage_tile<A_KMAJOR>(a.A, a.lda, m0, a.M, k0, a.K, nxt, wave, lane);
+        stage_tile<B_KMAJOR>(a.B, a.ldb, n0, a.N, k0, a.K, nxt + TILE_BYTES, wave, lane);
+      }
     }
     const int kvalid = kend - (kbeg + kt * BK);
 #pragma unroll
@@ -528,6 +589,7 @@ static int tn_group_splits(int nprob, const NfTnProblem* pr) {
   int target = (t256 ? 1 : 2) * device_cus();
   if (const char* e = getenv("VINF_TN_TARGET_BLOCKS")) target = atoi(e);
   int S = (int)(target / (tiles > 0 ? tiles : 1));
+  if (const char* e = getenv("VINF_TN_GROUP_SPLITS")) S = atoi(e);   // experiments
   if (S > cap) S = cap;
   return S < 1 ? 1 : S;
 }
