@@ -30,6 +30,7 @@ class IAFVAEConfig:
     context: int = 256
     n_flows: int = 10
     made_hidden: int = 1024
+    compute: str = "bf16"     # GPU matmul precision of the dense encoder/decoder ("bf16" | "fp32")
 
     @property
     def dim_x(self) -> int:
@@ -56,17 +57,31 @@ class IAFVAE(nn.Module):
         o = self.enc_out(self.encoder(x))
         return o[:, :dz], o[:, dz:2 * dz], o[:, 2 * dz:]
 
+    def _amp(self, x):
+        """bf16 autocast for the dense MLP GEMMs on the GPU (fp32 master weights, fp32 loss
+        terms); the MADE layers run their own bf16 MFMA kernels either way."""
+        import contextlib
+
+        if x.is_cuda and self.cfg.compute == "bf16":
+            return torch.autocast("cuda", dtype=torch.bfloat16)
+        return contextlib.nullcontext()
+
     def loss(self, x, beta: float = 1.0, generator=None, with_stats: bool = True) -> FreeEnergy:
         x = x.reshape(x.shape[0], -1)
-        mu, logvar, h = self.encode(x)
+        with self._amp(x):
+            mu, logvar, h = (t.float() for t in self.encode(x))
         eps = torch.randn(mu.shape, device=mu.device, dtype=mu.dtype, generator=generator)
         z = mu + torch.exp(0.5 * logvar) * eps
         lq = -0.5 * mu.shape[1] * LOG2PI - 0.5 * logvar.sum(1) - 0.5 * (eps * eps).sum(1)
         ldj = torch.zeros_like(lq)
         for f in self.flows:
-            z, l = f(z, h)
+            with self._amp(x):
+                z, l = f(z, h)
+            z, l = z.float(), l.float()
             ldj = ldj + l
-        lp = log_bern_logits(x, self.decoder(z)) + log_std_norm(z)
+        with self._amp(x):
+            logits = self.decoder(z).float()
+        lp = log_bern_logits(x, logits) + log_std_norm(z)
         F = (lq - ldj - beta * lp).mean()
         if not with_stats:   # no host syncs (hipGraph capture)
             return FreeEnergy(F, {})
