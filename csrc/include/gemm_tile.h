@@ -8,12 +8,16 @@
 #pragma once
 #include "nf_common.h"
 
+#include <cstdlib>
+
 namespace nf {
 namespace gemm {
 
 typedef short v8s __attribute__((ext_vector_type(8)));
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef float v4f __attribute__((ext_vector_type(4)));
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 #define LDS_AS __attribute__((address_space(3)))
 
 enum Epi : int {
@@ -42,7 +46,28 @@ struct GemmArgs {
   const int* krange;           // [ntn][2] per output N-tile K range [lo, hi) (multiples of 64), or null
   const unsigned char* skip;   // [ntm*ntn] 1 -> tile entirely masked: write zeros, no MFMA, or null
   const unsigned char* cmask;  // [M][N] 0/1 applied to fp32 outputs (masked weight gradients), or null
+  int staged;                  // 1 -> LDS-staged epilogue (set by the launchers, see staged_ok)
 };
+
+// LDS-staged epilogue switch (VINF_GEMM_STAGED_EPI=0 restores the fragment-layout stores) and
+// the alignment its 16-B row accesses need (host side).
+inline bool staged_enabled() {
+  static const int v = [] {
+    const char* e = getenv("VINF_GEMM_STAGED_EPI");
+    return e ? atoi(e) != 0 : 1;
+  }();
+  return v != 0;
+}
+inline bool staged_ok(const GemmArgs& a, int epi) {
+  if (!staged_enabled()) return false;
+  auto al = [](const void* p) { return ((unsigned long)p & 15) == 0; };
+  if (epi == EPI_BF16 || epi == EPI_BF16_RELUMASK) {
+    if (a.N % 8 || a.ldc % 8 || !al(a.C)) return false;
+    if (epi == EPI_BF16_RELUMASK && (a.ld_aux % 8 || !al(a.aux))) return false;
+    return true;
+  }
+  return a.N % 4 == 0 && a.ldc % 4 == 0 && a.c_split_stride % 4 == 0 && al(a.C);
+}
 
 // Grouped launch: up to 4 independent problems (the weight gradients of one conditioner MLP),
 // blocks [start[p], start[p+1]) belong to problem p, split-major inside a problem so the column
@@ -120,6 +145,117 @@ __device__ __forceinline__ void epi_store(const GemmArgs& a, v4f v, int m, int n
     float4 o = *reinterpret_cast<float4*>(cp);
     o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
     *reinterpret_cast<float4*>(cp) = o;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS-staged epilogue. In the fragment layout one store instruction covers 16 rows x 32 B
+// (bf16) or 16 rows x 64 B (fp32): 16 partial cache lines per instruction, which made the
+// output write, not the MFMAs, the per-tile fixed cost at K <= 1024 (~15 us per 256^2 tile).
+// A wave instead parks its WM x 64 sub-tile in its own LDS region (free once the main loop
+// is done) and reads it back as whole rows, so every global store / aux / cmask / accumulate
+// access moves 16 B per lane and full 128-B lines.
+//   bf16 region: [WM rows][64 n] (128 B rows), 16-B chunk q of row r at q ^ (r & 7); the
+//                8-B fragment writes land 2-way at worst, the 16-B reads conflict-free.
+//   fp32 region: [64 rows][64 n] (256 B rows) per pass, chunk q of row r at q ^ (r & 7).
+// acc[i][j]: n = n0 + i*16 + (lane>>4)*4 + r, m = m0 + j*16 + (lane&15)  (m0/n0 = the wave's
+// sub-tile origin), i < 4, j < NJ (WM = 16*NJ). Requires N % 8 == 0, ldc % 8 == 0 (bf16) /
+// ldc % 4 == 0 (fp32) and a 16-B aligned C (checked by the launchers).
+template <int EPI, int NJ>
+__device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&acc)[4][NJ],
+                                                int m0, int n0, int split, char* region,
+                                                int lane) {
+  const int g = lane >> 4, c = lane & 15;
+  if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK) {
+    float bv[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[i][r] = 0.f;
+    if (EPI == EPI_BF16 && a.bias) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = n0 + i * 16 + g * 4;
+        if (n < a.N) {
+          const ushort4 bb = *reinterpret_cast<const ushort4*>(a.bias + n);
+          bv[i][0] = bf2f(bb.x); bv[i][1] = bf2f(bb.y); bv[i][2] = bf2f(bb.z); bv[i][3] = bf2f(bb.w);
+        }
+      }
+    }
+    const bool relu = EPI == EPI_BF16 && a.relu;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int row = j * 16 + c;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v0 = acc[i][j][0] + bv[i][0], v1 = acc[i][j][1] + bv[i][1];
+        float v2 = acc[i][j][2] + bv[i][2], v3 = acc[i][j][3] + bv[i][3];
+        if (relu) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
+        const unsigned lo = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
+        const unsigned hi = (unsigned)f2bf(v2) | ((unsigned)f2bf(v3) << 16);
+        const int slot = i * 4 + g;  // 8-B slot of the 128-B row
+        *(LDS_AS v2u*)(region + row * 128 + (((slot >> 1) ^ (row & 7)) << 4) + (slot & 1) * 8) =
+            (v2u){lo, hi};
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int q = lane & 7;
+#pragma unroll 4
+    for (int it = 0; it < NJ * 2; ++it) {
+      const int row = it * 8 + (lane >> 3);
+      const v4u v = *(const LDS_AS v4u*)(region + row * 128 + ((q ^ (row & 7)) << 4));
+      const int m = m0 + row, n = n0 + q * 8;
+      if (m < a.M && n < a.N) {
+        uint4 o = make_uint4(v[0], v[1], v[2], v[3]);
+        if (EPI == EPI_BF16_RELUMASK) {
+          const uint4 h = *reinterpret_cast<const uint4*>(a.aux + (long)m * a.ld_aux + n);
+          // keep element e iff aux_e > 0 (bf16: sign clear and not +0), per 16-bit half
+          auto keep = [](unsigned hw) {
+            const unsigned lo = (hw & 0xffffu) != 0 && !(hw & 0x8000u) ? 0xffffu : 0u;
+            const unsigned hi = (hw >> 16) != 0 && !(hw & 0x80000000u) ? 0xffff0000u : 0u;
+            return lo | hi;
+          };
+          o.x &= keep(h.x); o.y &= keep(h.y); o.z &= keep(h.z); o.w &= keep(h.w);
+        }
+        *reinterpret_cast<uint4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int hj = 0; hj < NJ / 4; ++hj) {
+      if (hj) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int row = jj * 16 + c;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          *(LDS_AS v4f*)(region + row * 256 + (((i * 4 + g) ^ (row & 7)) << 4)) = acc[i][hj * 4 + jj];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int q = lane & 15;
+#pragma unroll 4
+      for (int it = 0; it < 16; ++it) {
+        const int row = it * 4 + (lane >> 4);
+        v4f v = *(const LDS_AS v4f*)(region + row * 256 + ((q ^ (row & 7)) << 4));
+        const int m = m0 + hj * 64 + row, n = n0 + q * 4;
+        if (m < a.M && n < a.N) {
+          if (EPI == EPI_F32) {
+            if (a.cmask) {
+              const uchar4 mk = *reinterpret_cast<const uchar4*>(a.cmask + (long)m * a.N + n);
+              v[0] = mk.x ? v[0] : 0.f; v[1] = mk.y ? v[1] : 0.f;
+              v[2] = mk.z ? v[2] : 0.f; v[3] = mk.w ? v[3] : 0.f;
+            }
+            float* cp = (float*)a.C + (long)split * a.c_split_stride + (long)m * a.ldc + n;
+            *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+            float* cp = (float*)a.C + (long)m * a.ldc + n;
+            float4 o = *reinterpret_cast<float4*>(cp);
+            o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
+            *reinterpret_cast<float4*>(cp) = o;
+          }
+        }
+      }
+    }
   }
 }
 

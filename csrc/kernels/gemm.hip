@@ -218,6 +218,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, int wg, int split, 
       if (m < a.M) a.dbias[(long)split * a.M + m] = accb[j][0];
     }
   }
+  if (a.staged) {  // main loop ended on a barrier: the whole 64 KiB is free
+    epi_tile_staged<EPI, 4>(a, acc, m0 + wm * 64, n0 + wn * 64, split, smem + wave * 16384, lane);
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int m = m0 + wm * 64 + j * 16 + c;
@@ -335,7 +339,8 @@ __global__ void __launch_bounds__(256) splitk_reduce_group_kernel(ReduceGroup r)
 }
 
 template <bool AK, bool BK_, int EPI>
-static void launch(const GemmArgs& a, int splits, hipStream_t stream) {
+static void launch(GemmArgs a, int splits, hipStream_t stream) {
+  a.staged = staged_ok(a, EPI);
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn, splits), block(NTHR);
   hipLaunchKernelGGL((gemm_kernel<AK, BK_, EPI>), grid, block, 0, stream, a);
@@ -644,6 +649,7 @@ void nf_launch_gemm_tn_group(int nprob, const NfTnProblem* pr, float* work, hipS
     r.istart[p + 1] = r.istart[p] + (long)q.M * (q.N / 4) + (q.db ? q.M : 0);
     wp += (long)S * slab + (q.db ? (long)S * q.M : 0);
   }
+  for (int p = 0; p < nprob; ++p) g.p[p].staged = staged_ok(g.p[p], EPI_F32);
   if (use_256_tn()) {
     nf_launch_gemm256_tn_group(g, stream);
   } else {

@@ -275,6 +275,12 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
       if (g == 0 && m < a.M) a.dbias[(long)split * a.M + m] = v;
     }
   }
+  if (a.staged) {
+    barrier();  // every wave is past its last operand read; each wave reuses 16 KiB of LDS
+    epi_tile_staged<EPI, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, split, smem + wave * 16384,
+                            lane);
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int m = m0 + wr * 128 + j * 16 + c;
@@ -314,7 +320,8 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_group_kernel(GroupArgs g) {
 static int g_depth = 4;
 
 template <bool AK, bool BK_, int EPI, bool DB = false>
-void launch(const GemmArgs& a, int splits, hipStream_t stream) {
+void launch(GemmArgs a, int splits, hipStream_t stream) {
+  a.staged = staged_ok(a, EPI);
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn, splits), block(NTHR);
   if (g_depth == 4)

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--mine-only", action="store_true", help="skip the hipBLASLt reference")
     ap.add_argument("--modes", default=None,
                     help="compare kernel choices, e.g. 128,256d3,256d4 (M = batch products)")
+    ap.add_argument("--custom", default=None,
+                    help="extra shapes 'kind:M:N:K,...' (kind nt | ntplain | nn_mask | tn)")
     a = ap.parse_args()
     ops = native()
     dev = torch.device("cuda")
@@ -53,15 +55,23 @@ def main():
     if a.only:
         keep = set(a.only.split(","))
         shapes = [s for s in shapes if s[0] in keep]
+    if a.custom:
+        for spec in a.custom.split(","):
+            kind, M_, N_, K_ = spec.split(":")
+            shapes.append((f"{kind}_{M_}x{N_}x{K_}", kind, int(M_), int(N_), int(K_)))
     for name, kind, M, N, K in shapes:
         torch.manual_seed(0)
-        if kind == "nt":
+        if kind in ("nt", "ntplain"):
             x = torch.randn(M, K, device=dev).to(bf)
             W = (torch.randn(N, K, device=dev) * 0.05).to(bf)
             b = torch.randn(N, device=dev).to(bf)
             y = torch.empty(M, N, device=dev, dtype=bf)
-            mine = lambda: ops.gemm_nt(x, W, b, y, 1)
-            ref = lambda: torch.relu_(torch.addmm(b, x, W.t(), out=y))
+            if kind == "nt":
+                mine = lambda: ops.gemm_nt(x, W, b, y, 1)
+                ref = lambda: torch.relu_(torch.addmm(b, x, W.t(), out=y))
+            else:
+                mine = lambda: ops.gemm_nt(x, W, None, y, 0)
+                ref = lambda: torch.mm(x, W.t(), out=y)
         elif kind.startswith("nn"):
             dy = torch.randn(M, K, device=dev).to(bf)
             W = (torch.randn(K, N, device=dev) * 0.05).to(bf)
