@@ -198,23 +198,34 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
             (v2u){lo, hi};
       }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // aux rows (ReLU mask) for every readback row, in flight while the LDS writes drain
     const int q = lane & 7;
-#pragma unroll 4
+    uint4 hv[NJ * 2];
+    if constexpr (EPI == EPI_BF16_RELUMASK) {
+#pragma unroll
+      for (int it = 0; it < NJ * 2; ++it) {
+        int m = m0 + it * 8 + (lane >> 3), n = n0 + q * 8;
+        m = m < a.M ? m : a.M - 1;
+        n = n < a.N ? n : a.N - 8;
+        hv[it] = *reinterpret_cast<const uint4*>(a.aux + (long)m * a.ld_aux + n);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
     for (int it = 0; it < NJ * 2; ++it) {
       const int row = it * 8 + (lane >> 3);
       const v4u v = *(const LDS_AS v4u*)(region + row * 128 + ((q ^ (row & 7)) << 4));
       const int m = m0 + row, n = n0 + q * 8;
       if (m < a.M && n < a.N) {
         uint4 o = make_uint4(v[0], v[1], v[2], v[3]);
-        if (EPI == EPI_BF16_RELUMASK) {
-          const uint4 h = *reinterpret_cast<const uint4*>(a.aux + (long)m * a.ld_aux + n);
+        if constexpr (EPI == EPI_BF16_RELUMASK) {
           // keep element e iff aux_e > 0 (bf16: sign clear and not +0), per 16-bit half
           auto keep = [](unsigned hw) {
             const unsigned lo = (hw & 0xffffu) != 0 && !(hw & 0x8000u) ? 0xffffu : 0u;
             const unsigned hi = (hw >> 16) != 0 && !(hw & 0x80000000u) ? 0xffff0000u : 0u;
             return lo | hi;
           };
+          const uint4 h = hv[it];
           o.x &= keep(h.x); o.y &= keep(h.y); o.z &= keep(h.z); o.w &= keep(h.w);
         }
         *reinterpret_cast<uint4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
@@ -231,9 +242,20 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
         for (int i = 0; i < 4; ++i)
           *(LDS_AS v4f*)(region + row * 256 + (((i * 4 + g) ^ (row & 7)) << 4)) = acc[i][hj * 4 + jj];
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // old C (fp32 accumulate) rows, in flight while the LDS writes drain
       const int q = lane & 15;
-#pragma unroll 4
+      float4 cv[16];
+      if constexpr (EPI == EPI_F32_ACC) {
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+          int m = m0 + hj * 64 + it * 4 + (lane >> 4), n = n0 + q * 4;
+          m = m < a.M ? m : a.M - 1;
+          n = n < a.N ? n : a.N - 4;
+          cv[it] = *reinterpret_cast<const float4*>((const float*)a.C + (long)m * a.ldc + n);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
       for (int it = 0; it < 16; ++it) {
         const int row = it * 4 + (lane >> 4);
         v4f v = *(const LDS_AS v4f*)(region + row * 256 + ((q ^ (row & 7)) << 4));
@@ -248,10 +270,9 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
             float* cp = (float*)a.C + (long)split * a.c_split_stride + (long)m * a.ldc + n;
             *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
           } else {
-            float* cp = (float*)a.C + (long)m * a.ldc + n;
-            float4 o = *reinterpret_cast<float4*>(cp);
-            o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
-            *reinterpret_cast<float4*>(cp) = o;
+            const float4 o = cv[it];
+            *reinterpret_cast<float4*>((float*)a.C + (long)m * a.ldc + n) =
+                make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
           }
         }
       }

@@ -577,12 +577,24 @@ void nf_launch_gemm_tn_masked(const void* dy, long lddy, const void* x, long ldx
 }
 
 // ---------------------------------------------------------------- grouped weight gradients
+// Grouped weight gradients: the 256x256 kernel (one block per CU, S = CUs / tiles splits) beats
+// the 128x128 one at long K (235 vs 246 us for the RealNVP conditioner at B = 32768,
+// profiles/r1_wgrad_group_256.jsonl); it has no masked-tile skipping, so MADE groups stay on 128.
+static bool group_use_256(int nprob, const NfTnProblem* pr) {
+  if (g_tile_mode < 0) use_256(1, 1, 1);
+  if (g_tile_mode == 3) return true;
+  if (g_tile_mode != 0) return false;
+  for (int p = 0; p < nprob; ++p)
+    if (pr[p].skip || pr[p].K < 8192) return false;
+  return true;
+}
+
 // All weight gradients of one conditioner MLP in ONE launch: a common split count S chosen so
 // that S x (sum of tiles) fills one wave of resident blocks (2 per CU). Compared with one
 // launch per layer this cuts the split count (3 vs 8-16 at B = 16384), so each block streams a
 // 3x longer K range and the fp32 slab traffic drops by the same factor.
 static int tn_group_splits(int nprob, const NfTnProblem* pr) {
-  const bool t256 = use_256_tn();
+  const bool t256 = group_use_256(nprob, pr);
   const int bm = t256 ? 256 : BM, bn = t256 ? 256 : BN;
   long tiles = 0;
   int cap = 1 << 30;
@@ -610,6 +622,7 @@ long nf_gemm_tn_group_workspace(int nprob, const NfTnProblem* pr) {
 void nf_launch_gemm_tn_group(int nprob, const NfTnProblem* pr, float* work, hipStream_t stream) {
   if (nprob < 1 || nprob > 4) return;
   const int S = tn_group_splits(nprob, pr);
+  const bool t256 = group_use_256(nprob, pr);
   GroupArgs g{};
   ReduceGroup r{};
   g.nprob = nprob;
@@ -630,7 +643,7 @@ void nf_launch_gemm_tn_group(int nprob, const NfTnProblem* pr, float* work, hipS
     a.skip = q.skip;
     a.cmask = q.cmask;
     r.cmask[p] = q.cmask;
-    const int tb = use_256_tn() ? 256 : BM;
+    const int tb = t256 ? 256 : BM;
     const int tiles = ((q.M + tb - 1) / tb) * ((q.N + tb - 1) / tb);
     g.start[p + 1] = g.start[p] + tiles * used;
     if (S == 1 || used == 1) {
@@ -650,7 +663,7 @@ void nf_launch_gemm_tn_group(int nprob, const NfTnProblem* pr, float* work, hipS
     wp += (long)S * slab + (q.db ? (long)S * q.M : 0);
   }
   for (int p = 0; p < nprob; ++p) g.p[p].staged = staged_ok(g.p[p], EPI_F32);
-  if (use_256_tn()) {
+  if (t256) {
     nf_launch_gemm256_tn_group(g, stream);
   } else {
     hipLaunchKernelGGL((gemm_group_kernel<false, false, EPI_F32>), dim3(g.start[nprob]), dim3(NTHR),

@@ -101,14 +101,6 @@ __device__ __forceinline__ void vmwait_count(int cnt) {
   else vmwait<0>();
 }
 
-// sum of the 8 bf16 of a fragment (fp32)
-__device__ __forceinline__ float frag_sum(v8s f) {
-  float s = 0.f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) s += __uint_as_float(((unsigned)(unsigned short)f[e]) << 16);
-  return s;
-}
-
 template <bool A_KMAJOR, bool B_KMAJOR, int EPI, int D, bool DB>
 __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int split, char* smem) {
   const int lane = threadIdx.x & 63;
@@ -128,12 +120,25 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
-  // bias gradient db[m] = sum_k Aop(m,k) (weight-gradient launches): VALU sums of the A
-  // fragments the wc == 0 waves of the tn == 0 blocks already hold, overlapping the MFMAs
-  const bool do_db = DB && a.dbias != nullptr && tn == 0 && wc == 0;
-  float dba[8];
+  // bias gradient db[m] = sum_k Aop(m,k) (weight-gradient launches): an MFMA of a ones
+  // fragment against an A fragment the tn == 0 blocks already hold; wave wc takes row group
+  // j == wc of each A half (4 extra MFMAs per K-tile on every wave of those blocks, instead of
+  // 256 VALU on one wave that the block barriers then wait for)
+  const bool do_db = DB && a.dbias != nullptr && tn == 0;
+  v4f accb[2] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
+  v8s ones;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) dba[j] = 0.f;
+  for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;
+  auto db_mfma = [&](v4f& acc_b, const v8s (&f)[4][2], bool two_) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      if (ks == 1 && !two_) break;
+      if (wc == 0) acc_b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f[0][ks], acc_b, 0, 0, 0);
+      else if (wc == 1) acc_b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f[1][ks], acc_b, 0, 0, 0);
+      else if (wc == 2) acc_b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f[2][ks], acc_b, 0, 0, 0);
+      else acc_b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f[3][ks], acc_b, 0, 0, 0);
+    }
+  };
 
   // issue half j of K-tile t (no-op past the end)
   auto issue = [&](int t, int j) {
@@ -189,9 +194,7 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
             for (int j = 0; j < 4; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbl[i][ks], fa[j][ks], acc[i][j],
                                                                   0, 0, 0);
-      if (do_db)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) dba[j] += frag_sum(fa[j][0]) + (two ? frag_sum(fa[j][1]) : 0.f);
+      if (do_db) db_mfma(accb[0], fa, two);
       __builtin_amdgcn_s_setprio(0);
       barrier();
       // ---- r2: M0-3 x N2-3
@@ -236,10 +239,7 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
             for (int j = 0; j < 4; ++j)
               acc[2 + i][4 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                   fbh[i][ks], fa[j][ks], acc[2 + i][4 + j], 0, 0, 0);
-      if (do_db)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          dba[4 + j] += frag_sum(fa[j][0]) + (two ? frag_sum(fa[j][1]) : 0.f);
+      if (do_db) db_mfma(accb[1], fa, two);
       __builtin_amdgcn_s_setprio(0);
       barrier();
       // ---- r4: M4-7 x N0-1 (no LDS reads)
@@ -265,14 +265,11 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   // ---------------------------------------------------------------- epilogue
   // acc[i][j]: n = n0 + wc*64 + i*16 + (lane>>4)*4 + r, m = m0 + wr*128 + j*16 + (lane&15)
   const int g = lane >> 4, c = lane & 15;
-  if (do_db) {
+  if (do_db && g == 0) {  // accb[h]: m = wr*128 + h*64 + wc*16 + (lane & 15), any of the 4 rows
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = dba[j];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      const int m = m0 + wr * 128 + j * 16 + c;
-      if (g == 0 && m < a.M) a.dbias[(long)split * a.M + m] = v;
+    for (int h = 0; h < 2; ++h) {
+      const int m = m0 + wr * 128 + h * 64 + wc * 16 + c;
+      if (m < a.M) a.dbias[(long)split * a.M + m] = accb[h][0];
     }
   }
   if (a.staged) {

@@ -48,7 +48,7 @@ def main():
               ("dgrad_l1", "nn_f32acc", B, 416, 1024),
               ("wgrad_l3", "tn", 800, 1024, B), ("wgrad_l2", "tn", 1024, 1024, B),
               ("wgrad_l1", "tn", 1024, 416, B),
-              ("wgrad_group", "tn_group", 0, 0, B),
+              ("wgrad_group", "tn_group", 0, 0, B), ("wgrad_group_nodb", "tn_group_nodb", 0, 0, B),
               ("fwd_l2_fp8", "nt_fp8", B, 1024, 1024), ("sq4096_fp8", "nt_fp8", 4096, 4096, 4096),
               ("sq4096", "nt", 4096, 4096, 4096), ("fwd_k4096", "nt", B, 1024, 4096),
               ("fwd_k2048", "nt", B, 1024, 2048), ("fwd_m64k", "nt", 65536, 1024, 1024)]
@@ -96,11 +96,12 @@ def main():
             x, W = xf.to(bf), Wf.to(bf)
             mine = lambda: gemm_fp8(xq, sx, wq, sw, b, True, out=y)
             ref = lambda: torch.relu_(torch.addmm(b, x, W.t(), out=y))
-        elif kind == "tn_group":   # the three weight gradients of one conditioner
+        elif kind.startswith("tn_group"):   # the three weight gradients of one conditioner
             its = []
             for (m_, n_) in [(800, 1024), (1024, 1024), (1024, 416)]:
                 its.append((torch.randn(K, m_, device=dev).to(bf), torch.randn(K, n_, device=dev).to(bf),
-                            torch.empty(m_, n_, device=dev), torch.empty(m_, device=dev)))
+                            torch.empty(m_, n_, device=dev),
+                            None if kind.endswith("nodb") else torch.empty(m_, device=dev)))
             M, N = 1, 800 * 1024 + 1024 * 1024 + 1024 * 416
             mine = lambda: ops.gemm_tn_group([i[0] for i in its], [i[1] for i in its],
                                              [i[2] for i in its], [i[3] for i in its], [], [])
@@ -108,16 +109,19 @@ def main():
             def ref():
                 for i in its:
                     ops.gemm_tn(*i)
+            if kind.endswith("nodb"):
+                ref = mine
         else:
             dy = torch.randn(K, M, device=dev).to(bf)
             x = torch.randn(K, N, device=dev).to(bf)
             dW = torch.empty(M, N, device=dev)
-            db = torch.empty(M, device=dev)
+            db = None if kind == "tnnodb" else torch.empty(M, device=dev)
             mine = lambda: ops.gemm_tn(dy, x, dW, db)
 
             def ref():
                 dW.copy_(torch.mm(dy.t(), x, out_dtype=torch.float32))
-                torch.sum(dy, 0, dtype=torch.float32, out=db)
+                if db is not None:
+                    torch.sum(dy, 0, dtype=torch.float32, out=db)
         flops = 2.0 * M * N * K
         if a.modes:
             res = {m: [] for m in a.modes.split(",")}
