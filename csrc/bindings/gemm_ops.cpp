@@ -32,7 +32,7 @@ void chk_q(const at::Tensor& t, const char* n) {
 
 // y = act(x W^T + b): x [M,K], W [N,K], b [N] (bf16), y [M,N] bf16
 void gemm_nt(const at::Tensor& x, const at::Tensor& W, const c10::optional<at::Tensor>& b,
-             const at::Tensor& y, int64_t relu) {
+             const at::Tensor& y, int64_t relu, const c10::optional<at::Tensor>& mask) {
   chk_mat(x, "x", at::kBFloat16);
   chk_mat(W, "W", at::kBFloat16);
   chk_mat(y, "y", at::kBFloat16);
@@ -46,13 +46,25 @@ void gemm_nt(const at::Tensor& x, const at::Tensor& W, const c10::optional<at::T
     TORCH_CHECK(b->scalar_type() == at::kBFloat16 && b->numel() == N && b->is_contiguous(), "bias");
     bp = b->data_ptr();
   }
+  void* mp = nullptr;
+  long ldm = 0;
+  if (mask && mask->defined()) {  // ReLU bitmask [M][N/8] uint8 for the input-gradient epilogue
+    TORCH_CHECK(mask->is_cuda() && mask->dim() == 2 && mask->scalar_type() == at::kByte &&
+                    mask->stride(1) == 1, "mask must be a 2-D uint8 GPU tensor with unit inner stride");
+    TORCH_CHECK(relu, "the bitmask records 1(y > 0) of a ReLU layer");
+    TORCH_CHECK(mask->size(0) == M && mask->size(1) * 8 == N, "mask shape [M, N/8]");
+    TORCH_CHECK(ld2(y) % 8 == 0 && ((uintptr_t)y.data_ptr() & 15) == 0,
+                "bitmask output needs 16-B aligned y rows");
+    mp = mask->data_ptr();
+    ldm = ld2(*mask);
+  }
   nf_launch_gemm_nt(x.data_ptr(), ld2(x), W.data_ptr(), ld2(W), bp, y.data_ptr(), ld2(y), M, N, K,
-                    (int)relu, cur_stream());
+                    (int)relu, cur_stream(), mp, ldm);
 }
 
 // dx = dy W  [* 1(h > 0)]: dy [M,K], W [K,N] bf16; dx bf16 (mask) or fp32 (+= when accumulate)
 void gemm_nn(const at::Tensor& dy, const at::Tensor& W, const c10::optional<at::Tensor>& h,
-             const at::Tensor& dx, bool accumulate) {
+             const at::Tensor& dx, bool accumulate, const c10::optional<at::Tensor>& hbits) {
   chk_mat(dy, "dy", at::kBFloat16);
   chk_mat(W, "W", at::kBFloat16);
   const bool f32 = dx.scalar_type() == at::kFloat;
@@ -70,9 +82,20 @@ void gemm_nn(const at::Tensor& dy, const at::Tensor& W, const c10::optional<at::
     hp = h->data_ptr();
     ldh = ld2(*h);
   }
+  int bits = 0;
+  if (hbits && hbits->defined()) {  // ReLU bitmask written by gemm_nt(mask=...)
+    TORCH_CHECK(!hp, "pass either h or hbits");
+    TORCH_CHECK(!f32, "ReLU-mask epilogue writes bf16");
+    TORCH_CHECK(hbits->is_cuda() && hbits->dim() == 2 && hbits->scalar_type() == at::kByte &&
+                    hbits->stride(1) == 1, "hbits must be a 2-D uint8 GPU tensor with unit inner stride");
+    TORCH_CHECK(hbits->size(0) == M && hbits->size(1) * 8 == N, "hbits shape [M, N/8]");
+    hp = hbits->data_ptr();
+    ldh = ld2(*hbits);
+    bits = 1;
+  }
   TORCH_CHECK(!accumulate || f32, "accumulate needs an fp32 output");
   nf_launch_gemm_nn(dy.data_ptr(), ld2(dy), W.data_ptr(), ld2(W), hp, ldh, dx.data_ptr(), ld2(dx),
-                    f32, accumulate, M, N, K, cur_stream());
+                    f32, accumulate, M, N, K, cur_stream(), bits);
 }
 
 // dW = dy^T x (fp32), db = colsum(dy) (fp32): dy [K,M], x [K,N] bf16
@@ -378,8 +401,8 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("masked_gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu, Tensor krange) -> ()");
   m.def("masked_gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, Tensor krange, bool accumulate=False) -> ()");
   m.def("masked_gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db, Tensor skip) -> ()");
-  m.def("gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu) -> ()");
-  m.def("gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, bool accumulate) -> ()");
+  m.def("gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu, Tensor(b!)? mask=None) -> ()");
+  m.def("gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, bool accumulate, Tensor? hbits=None) -> ()");
   m.def("gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db) -> ()");
   m.def("gemm_tn_group(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, Tensor?[] skip, Tensor?[] cmask) -> ()");
   m.def("fp8_quant_rows_strided(Tensor x, int layer_stride, int rows_per, int layers, int C, Tensor(a!) q, Tensor(b!) scale) -> ()");

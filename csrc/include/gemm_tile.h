@@ -8,6 +8,7 @@
 #pragma once
 #include "nf_common.h"
 
+#include <cstdio>
 #include <cstdlib>
 
 namespace nf {
@@ -47,6 +48,10 @@ struct GemmArgs {
   const unsigned char* skip;   // [ntm*ntn] 1 -> tile entirely masked: write zeros, no MFMA, or null
   const unsigned char* cmask;  // [M][N] 0/1 applied to fp32 outputs (masked weight gradients), or null
   int staged;                  // 1 -> LDS-staged epilogue (set by the launchers, see staged_ok)
+  // ReLU bitmask (1 bit per output, bit e of byte [m][n/8] <-> column n+e):
+  unsigned char* mask_out;     // EPI_BF16 + relu: also write 1(y > 0) bits (staged path only)
+  long ld_mask;                // bytes per mask row
+  int aux_bits;                // EPI_BF16_RELUMASK: aux is such a bitmask (ld_aux in bytes)
 };
 
 // LDS-staged epilogue switch (VINF_GEMM_STAGED_EPI=0 restores the fragment-layout stores) and
@@ -59,11 +64,11 @@ inline bool staged_enabled() {
   return v != 0;
 }
 inline bool staged_ok(const GemmArgs& a, int epi) {
-  if (!staged_enabled()) return false;
+  if (!staged_enabled() && !a.mask_out) return false;
   auto al = [](const void* p) { return ((unsigned long)p & 15) == 0; };
   if (epi == EPI_BF16 || epi == EPI_BF16_RELUMASK) {
     if (a.N % 8 || a.ldc % 8 || !al(a.C)) return false;
-    if (epi == EPI_BF16_RELUMASK && (a.ld_aux % 8 || !al(a.aux))) return false;
+    if (epi == EPI_BF16_RELUMASK && !a.aux_bits && (a.ld_aux % 8 || !al(a.aux))) return false;
     return true;
   }
   return a.N % 4 == 0 && a.ldc % 4 == 0 && a.c_split_stride % 4 == 0 && al(a.C);
@@ -124,12 +129,18 @@ __device__ __forceinline__ void epi_store(const GemmArgs& a, v4f v, int m, int n
     o.x = f2bf(v[0]); o.y = f2bf(v[1]); o.z = f2bf(v[2]); o.w = f2bf(v[3]);
     *reinterpret_cast<ushort4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
   } else if (EPI == EPI_BF16_RELUMASK) {
-    const ushort4 h = *reinterpret_cast<const ushort4*>(a.aux + (long)m * a.ld_aux + n);
-    // bf16 > 0  <=>  sign bit clear and not +0
-    v[0] = (h.x != 0 && !(h.x & 0x8000)) ? v[0] : 0.f;
-    v[1] = (h.y != 0 && !(h.y & 0x8000)) ? v[1] : 0.f;
-    v[2] = (h.z != 0 && !(h.z & 0x8000)) ? v[2] : 0.f;
-    v[3] = (h.w != 0 && !(h.w & 0x8000)) ? v[3] : 0.f;
+    if (a.aux_bits) {
+      const unsigned b = ((const unsigned char*)a.aux)[(long)m * a.ld_aux + (n >> 3)] >> (n & 4);
+      v[0] = (b & 1u) ? v[0] : 0.f; v[1] = (b & 2u) ? v[1] : 0.f;
+      v[2] = (b & 4u) ? v[2] : 0.f; v[3] = (b & 8u) ? v[3] : 0.f;
+    } else {
+      const ushort4 h = *reinterpret_cast<const ushort4*>(a.aux + (long)m * a.ld_aux + n);
+      // bf16 > 0  <=>  sign bit clear and not +0
+      v[0] = (h.x != 0 && !(h.x & 0x8000)) ? v[0] : 0.f;
+      v[1] = (h.y != 0 && !(h.y & 0x8000)) ? v[1] : 0.f;
+      v[2] = (h.z != 0 && !(h.z & 0x8000)) ? v[2] : 0.f;
+      v[3] = (h.w != 0 && !(h.w & 0x8000)) ? v[3] : 0.f;
+    }
     ushort4 o;
     o.x = f2bf(v[0]); o.y = f2bf(v[1]); o.z = f2bf(v[2]); o.w = f2bf(v[3]);
     *reinterpret_cast<ushort4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
@@ -201,13 +212,24 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
     // aux rows (ReLU mask) for every readback row, in flight while the LDS writes drain
     const int q = lane & 7;
     uint4 hv[NJ * 2];
+    unsigned hb[NJ * 2];
     if constexpr (EPI == EPI_BF16_RELUMASK) {
+      if (a.aux_bits) {
 #pragma unroll
-      for (int it = 0; it < NJ * 2; ++it) {
-        int m = m0 + it * 8 + (lane >> 3), n = n0 + q * 8;
-        m = m < a.M ? m : a.M - 1;
-        n = n < a.N ? n : a.N - 8;
-        hv[it] = *reinterpret_cast<const uint4*>(a.aux + (long)m * a.ld_aux + n);
+        for (int it = 0; it < NJ * 2; ++it) {
+          int m = m0 + it * 8 + (lane >> 3), n = n0 + q * 8;
+          m = m < a.M ? m : a.M - 1;
+          n = n < a.N ? n : a.N - 8;
+          hb[it] = ((const unsigned char*)a.aux)[(long)m * a.ld_aux + (n >> 3)];
+        }
+      } else {
+#pragma unroll
+        for (int it = 0; it < NJ * 2; ++it) {
+          int m = m0 + it * 8 + (lane >> 3), n = n0 + q * 8;
+          m = m < a.M ? m : a.M - 1;
+          n = n < a.N ? n : a.N - 8;
+          hv[it] = *reinterpret_cast<const uint4*>(a.aux + (long)m * a.ld_aux + n);
+        }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -225,8 +247,24 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
             const unsigned hi = (hw >> 16) != 0 && !(hw & 0x80000000u) ? 0xffff0000u : 0u;
             return lo | hi;
           };
-          const uint4 h = hv[it];
-          o.x &= keep(h.x); o.y &= keep(h.y); o.z &= keep(h.z); o.w &= keep(h.w);
+          if (a.aux_bits) {
+            const unsigned b = hb[it];
+            auto kb = [b](int e) {
+              return ((b >> e) & 1u ? 0xffffu : 0u) | ((b >> (e + 1)) & 1u ? 0xffff0000u : 0u);
+            };
+            o.x &= kb(0); o.y &= kb(2); o.z &= kb(4); o.w &= kb(6);
+          } else {
+            const uint4 h = hv[it];
+            o.x &= keep(h.x); o.y &= keep(h.y); o.z &= keep(h.z); o.w &= keep(h.w);
+          }
+        }
+        if (EPI == EPI_BF16 && a.mask_out) {  // 1(y > 0) of the stored bf16, 8 bits per lane
+          auto pos2 = [](unsigned w) {
+            return (((w & 0xffffu) != 0 && !(w & 0x8000u)) ? 1u : 0u) |
+                   (((w >> 16) != 0 && !(w & 0x80000000u)) ? 2u : 0u);
+          };
+          const unsigned bits = pos2(o.x) | (pos2(o.y) << 2) | (pos2(o.z) << 4) | (pos2(o.w) << 6);
+          a.mask_out[(long)m * a.ld_mask + (n >> 3)] = (unsigned char)bits;
         }
         *reinterpret_cast<uint4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
       }

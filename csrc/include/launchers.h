@@ -47,11 +47,14 @@ void nf_launch_sumsq_guard(const float* x, long n, float* partial, int npartial,
                            hipStream_t stream);
 
 // gemm.hip (bf16 MFMA, fp32 accumulate)
+// mask_out: optional ReLU bitmask [M][N/8] bytes (bit e of byte n/8 <-> column n+e) written by
+// the forward epilogue; aux_is_bits: the dgrad's ReLU mask `aux` is such a bitmask (ld in bytes)
 void nf_launch_gemm_nt(const void* x, long ldx, const void* W, long ldw, const void* bias, void* y,
-                       long ldy, int M, int N, int K, int relu, hipStream_t stream);
+                       long ldy, int M, int N, int K, int relu, hipStream_t stream,
+                       void* mask_out = nullptr, long ld_mask = 0);
 void nf_launch_gemm_nn(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                        long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
-                       int N, int K, hipStream_t stream);
+                       int N, int K, hipStream_t stream, int aux_is_bits = 0);
 void nf_launch_gemm_tn(const void* dy, long lddy, const void* x, long ldx, float* dW, long lddw,
                        float* db, int M, int N, int K, int splits, float* work,
                        hipStream_t stream);
@@ -71,10 +74,11 @@ long nf_gemm_tn_group_workspace(int nprob, const NfTnProblem* pr);
 void nf_launch_gemm_tn_group(int nprob, const NfTnProblem* pr, float* work, hipStream_t stream);
 // gemm256.hip: 256x256 8-phase kernel (forward / input-gradient products)
 void nf_launch_gemm256_nt(const void* x, long ldx, const void* W, long ldw, const void* bias,
-                          void* y, long ldy, int M, int N, int K, int relu, hipStream_t stream);
+                          void* y, long ldy, int M, int N, int K, int relu, hipStream_t stream,
+                          void* mask_out = nullptr, long ld_mask = 0);
 void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                           long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
-                          int N, int K, hipStream_t stream);
+                          int N, int K, hipStream_t stream, int aux_is_bits = 0);
 void nf_gemm256_set_depth(int d);
 int nf_launch_gemm256_tn_partials(const void* dy, long lddy, const void* x, long ldx, float* C,
                                   long ldc, long slab_stride, float* dbias, int M, int N, int K,

@@ -341,6 +341,10 @@ __global__ void __launch_bounds__(256) splitk_reduce_group_kernel(ReduceGroup r)
 template <bool AK, bool BK_, int EPI>
 static void launch(GemmArgs a, int splits, hipStream_t stream) {
   a.staged = staged_ok(a, EPI);
+  if (a.mask_out && !a.staged) {
+    fprintf(stderr, "vinf: ReLU bitmask output needs the staged epilogue (N %% 8, 16-B rows)\n");
+    abort();
+  }
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn, splits), block(NTHR);
   hipLaunchKernelGGL((gemm_kernel<AK, BK_, EPI>), grid, block, 0, stream, a);
@@ -397,10 +401,11 @@ static bool use_256_tn() {
 
 // y[M][N] = act(x[M][K] W[N][K]^T + bias)   -> bf16
 void nf_launch_gemm_nt(const void* x, long ldx, const void* W, long ldw, const void* bias, void* y,
-                       long ldy, int M, int N, int K, int relu, hipStream_t stream) {
+                       long ldy, int M, int N, int K, int relu, hipStream_t stream,
+                       void* mask_out, long ld_mask) {
   if (M <= 0 || N <= 0) return;
   if (use_256(M, N, K)) {
-    nf_launch_gemm256_nt(x, ldx, W, ldw, bias, y, ldy, M, N, K, relu, stream);
+    nf_launch_gemm256_nt(x, ldx, W, ldw, bias, y, ldy, M, N, K, relu, stream, mask_out, ld_mask);
     return;
   }
   GemmArgs a{};
@@ -409,17 +414,18 @@ void nf_launch_gemm_nt(const void* x, long ldx, const void* W, long ldw, const v
   a.C = y; a.ldc = ldy;
   a.bias = (const bf16_t*)bias;
   a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + BK - 1) / BK) * BK; a.relu = relu;
+  a.mask_out = (unsigned char*)mask_out; a.ld_mask = ld_mask;
   launch<true, true, EPI_BF16>(a, 1, stream);
 }
 
 // dx[M][N] = dy[M][K] W[K][N]  (* 1(aux>0) -> bf16)  or  (fp32 dx (+)= ...)
 void nf_launch_gemm_nn(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                        long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
-                       int N, int K, hipStream_t stream) {
+                       int N, int K, hipStream_t stream, int aux_is_bits) {
   if (M <= 0 || N <= 0) return;
   if (use_256(M, N, K)) {
     nf_launch_gemm256_nn(dy, lddy, W, ldw, aux, ld_aux, dx, lddx, dx_is_f32, accumulate, M, N, K,
-                         stream);
+                         stream, aux_is_bits);
     return;
   }
   GemmArgs a{};
@@ -427,6 +433,7 @@ void nf_launch_gemm_nn(const void* dy, long lddy, const void* W, long ldw, const
   a.B = (const bf16_t*)W; a.ldb = ldw;
   a.C = dx; a.ldc = lddx;
   a.aux = (const bf16_t*)aux; a.ld_aux = ld_aux;
+  a.aux_bits = aux_is_bits;
   a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + BK - 1) / BK) * BK;
   if (dx_is_f32) {
     if (accumulate) launch<true, false, EPI_F32_ACC>(a, 1, stream);

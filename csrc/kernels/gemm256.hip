@@ -319,6 +319,10 @@ static int g_depth = 4;
 template <bool AK, bool BK_, int EPI, bool DB = false>
 void launch(GemmArgs a, int splits, hipStream_t stream) {
   a.staged = staged_ok(a, EPI);
+  if (a.mask_out && !a.staged) {
+    fprintf(stderr, "vinf: ReLU bitmask output needs the staged epilogue (N %% 8, 16-B rows)\n");
+    abort();
+  }
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn, splits), block(NTHR);
   if (g_depth == 4)
@@ -338,7 +342,8 @@ void nf_gemm256_set_depth(int d) { g256::g_depth = d == 3 ? 3 : 4; }
 
 // y[M][N] = act(x[M][K] W[N][K]^T + bias) -> bf16
 void nf_launch_gemm256_nt(const void* x, long ldx, const void* W, long ldw, const void* bias,
-                          void* y, long ldy, int M, int N, int K, int relu, hipStream_t stream) {
+                          void* y, long ldy, int M, int N, int K, int relu, hipStream_t stream,
+                          void* mask_out, long ld_mask) {
   if (M <= 0 || N <= 0) return;
   GemmArgs a{};
   a.A = (const nf::bf16_t*)x; a.lda = ldx;
@@ -346,19 +351,21 @@ void nf_launch_gemm256_nt(const void* x, long ldx, const void* W, long ldw, cons
   a.C = y; a.ldc = ldy;
   a.bias = (const nf::bf16_t*)bias;
   a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + 63) / 64) * 64; a.relu = relu;
+  a.mask_out = (unsigned char*)mask_out; a.ld_mask = ld_mask;
   g256::launch<true, true, EPI_BF16>(a, 1, stream);
 }
 
 // dx[M][N] = dy[M][K] W[K][N]  (* 1(aux>0) -> bf16)  or  fp32 dx (+)= ...
 void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                           long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
-                          int N, int K, hipStream_t stream) {
+                          int N, int K, hipStream_t stream, int aux_is_bits) {
   if (M <= 0 || N <= 0) return;
   GemmArgs a{};
   a.A = (const nf::bf16_t*)dy; a.lda = lddy;
   a.B = (const nf::bf16_t*)W; a.ldb = ldw;
   a.C = dx; a.ldc = lddx;
   a.aux = (const nf::bf16_t*)aux; a.ld_aux = ld_aux;
+  a.aux_bits = aux_is_bits;
   a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + 63) / 64) * 64;
   if (dx_is_f32) {
     if (accumulate) g256::launch<true, false, EPI_F32_ACC>(a, 1, stream);

@@ -24,16 +24,17 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, eps_all, out_dir):
+def _worker(rank, world, port, eps_all, out_dir, side):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), VINF_DIST_BACKEND="gloo")
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), VINF_DIST_BACKEND="gloo",
+                      VINF_WGRAD_STREAM=side)
     from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI
     from vi_normflows_amd.parallel import dist as vdist
     from vi_normflows_amd.parallel.runner import DataParallelRunner
 
     info = vdist.init()
     eng = RealNVPVI(RealNVPConfig(**CFG), batch=B, device=info.device, seed=100 + rank, rank=rank)
-    assert eng.wgrad_stream is not None
+    assert (eng.wgrad_stream is not None) == (side == "1")
     run = DataParallelRunner(eng, info, bucket_cap_mb=0.05)
     eng.eps_override = eps_all[rank * B:(rank + 1) * B].to(info.device)
     run.reducer.start_step()
@@ -47,13 +48,14 @@ def _worker(rank, world, port, eps_all, out_dir):
     dist.destroy_process_group()
 
 
-def test_dp_gpu_side_stream_gradient_equals_single(tmp_path):
+@pytest.mark.parametrize("side", ["0", "1"], ids=["serial", "side_stream"])
+def test_dp_gpu_side_stream_gradient_equals_single(tmp_path, side):
     from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI
 
     world = 2
     torch.manual_seed(0)
     eps_all = torch.randn(world * B, CFG["dim"])
-    mp.spawn(_worker, args=(world, _port(), eps_all, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _port(), eps_all, str(tmp_path), side), nprocs=world, join=True)
     g0 = torch.load(tmp_path / "g0.pt", weights_only=True)
     g1 = torch.load(tmp_path / "g1.pt", weights_only=True)
     assert g0["n_buckets"] > 2

@@ -134,6 +134,40 @@ def test_gemm256_nn(gpu, tile256, M, N, K):
     _check(dxf, dy.float() @ W.float() + base, 2e-2)
 
 
+def _pack_bits(pos: torch.Tensor) -> torch.Tensor:
+    """[M, N] bool -> [M, N/8] uint8, bit e of byte j <-> column 8j+e."""
+    M, N = pos.shape
+    w = (2 ** torch.arange(8, device=pos.device, dtype=torch.int32))
+    return (pos.view(M, N // 8, 8).to(torch.int32) * w).sum(-1).to(torch.uint8)
+
+
+@pytest.mark.parametrize("mode", [1, 2], ids=["t128", "t256"])
+@pytest.mark.parametrize("M,N,K", [(300, 416, 64), (1000, 1024, 96), (4096, 1024, 1024),
+                                   (520, 8, 32)])
+def test_relu_bitmask_roundtrip(gpu, mode, M, N, K):
+    """The forward epilogue's ReLU bitmask equals 1(y > 0) of the stored bf16 output, and the
+    input-gradient epilogue reading it is bitwise identical to reading the bf16 activation."""
+    torch.ops.vinf.gemm_set_mode(mode, 4)
+    try:
+        torch.manual_seed(M + N)
+        x, W, b = _bf(M, K, device=gpu), _bf(N, K, device=gpu, scale=0.05), _bf(N, device=gpu)
+        y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        mask = torch.full((M, N // 8), 0xAA, device=gpu, dtype=torch.uint8)
+        torch.ops.vinf.gemm_nt(x, W, b, y, 1, mask)
+        _check(y, (x.float() @ W.float().t() + b.float()).clamp_min(0), 1e-2)
+        assert torch.equal(mask, _pack_bits(y > 0))
+        Kd = 64
+        dy, W2 = _bf(M, Kd, device=gpu), _bf(Kd, N, device=gpu, scale=0.05)
+        d_ref = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        d_bit = torch.empty_like(d_ref)
+        torch.ops.vinf.gemm_nn(dy, W2, y, d_ref, False)
+        torch.ops.vinf.gemm_nn(dy, W2, None, d_bit, False, mask)
+        assert torch.equal(d_ref, d_bit)
+        _check(d_bit, (dy.float() @ W2.float()) * (y.float() > 0), 1e-2)
+    finally:
+        torch.ops.vinf.gemm_set_mode(0, 4)
+
+
 def test_gemm256_repeatable(gpu, tile256):
     """Race screen: the same product 20x must be bitwise identical (LDS-DMA RAW/WAR schedule)."""
     torch.manual_seed(5)

@@ -84,13 +84,14 @@ def test_reference_annealing_schedule_on_device():
 
 
 @pytest.mark.gpu
-def test_wgrad_side_stream_matches_serial_and_captures(gpu):
+def test_wgrad_side_stream_matches_serial_and_captures(gpu, monkeypatch):
     """Weight-gradient launches on the side stream (overlapping the next layer's backward) give
     bitwise the same gradients as the serial schedule, eagerly and inside a hipGraph."""
     from vi_normflows_amd.parallel.dist import DistInfo
     from vi_normflows_amd.parallel.runner import DataParallelRunner
 
     cfg = RealNVPConfig(dim=64, n_layers=6, hidden=128, anneal="none", init_out_std=0.1)
+    monkeypatch.setenv("VINF_WGRAD_STREAM", "1")
     a = RealNVPVI(cfg, batch=512, device=gpu, seed=3)
     b = RealNVPVI(cfg, batch=512, device=gpu, seed=3)
     b.wgrad_stream = None

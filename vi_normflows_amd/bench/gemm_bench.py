@@ -49,6 +49,7 @@ def main():
               ("wgrad_l3", "tn", 800, 1024, B), ("wgrad_l2", "tn", 1024, 1024, B),
               ("wgrad_l1", "tn", 1024, 416, B),
               ("wgrad_group", "tn_group", 0, 0, B), ("wgrad_group_nodb", "tn_group_nodb", 0, 0, B),
+              ("wgrad_group_sq", "tn_group_sq", 0, 0, B),
               ("fwd_l2_fp8", "nt_fp8", B, 1024, 1024), ("sq4096_fp8", "nt_fp8", 4096, 4096, 4096),
               ("sq4096", "nt", 4096, 4096, 4096), ("fwd_k4096", "nt", B, 1024, 4096),
               ("fwd_k2048", "nt", B, 1024, 2048), ("fwd_m64k", "nt", 65536, 1024, 1024)]
@@ -98,18 +99,20 @@ def main():
             ref = lambda: torch.relu_(torch.addmm(b, x, W.t(), out=y))
         elif kind.startswith("tn_group"):   # the three weight gradients of one conditioner
             its = []
-            for (m_, n_) in [(800, 1024), (1024, 1024), (1024, 416)]:
+            dims = ([(1024, 1024)] * 3 if kind.endswith("sq") else
+                    [(800, 1024), (1024, 1024), (1024, 416)])
+            for (m_, n_) in dims:
                 its.append((torch.randn(K, m_, device=dev).to(bf), torch.randn(K, n_, device=dev).to(bf),
                             torch.empty(m_, n_, device=dev),
                             None if kind.endswith("nodb") else torch.empty(m_, device=dev)))
-            M, N = 1, 800 * 1024 + 1024 * 1024 + 1024 * 416
+            M, N = 1, sum(m_ * n_ for m_, n_ in dims)
             mine = lambda: ops.gemm_tn_group([i[0] for i in its], [i[1] for i in its],
                                              [i[2] for i in its], [i[3] for i in its], [], [])
 
             def ref():
                 for i in its:
                     ops.gemm_tn(*i)
-            if kind.endswith("nodb"):
+            if kind.endswith("nodb") or kind.endswith("sq"):
                 ref = mine
         else:
             dy = torch.randn(K, M, device=dev).to(bf)

@@ -153,6 +153,11 @@ class RealNVPVI:
         Dp, Np = cfg.half_pad, cfg.out_pad
         self.Hbf = torch.empty(L, B, Dp, dtype=self.cdt, device=dev)    # bf16(h_1 .. h_L), 0-padded
         self.Act = torch.empty(L, cfg.n_hidden, B, H, dtype=self.cdt, device=dev)
+        # ReLU bitmasks of the hidden activations, written by the forward GEMM epilogue and read
+        # by the input-gradient epilogue instead of the bf16 activation (B*H/8 bytes vs 2*B*H)
+        self.Mk = None
+        if dev.type == "cuda" and H % 8 == 0:
+            self.Mk = torch.empty(L, cfg.n_hidden, B, H // 8, dtype=torch.uint8, device=dev)
         # per-layer conditioner outputs [s_hat | t] (compute dtype): the backward recomputes
         # s = scale * tanh(s_hat) from them instead of reading a saved fp32 s
         self.ST = torch.empty(L, B, Np, dtype=self.cdt, device=dev)
@@ -167,7 +172,9 @@ class RealNVPVI:
                      for _ in range(max(cfg.n_hidden, 1))] for _ in range(2)]
         self.dH = self.dH2[0]
         self.wgrad_stream = None
-        if dev.type == "cuda" and os.environ.get("VINF_WGRAD_STREAM", "1") == "1":
+        # off by default: the 256x256 grouped launch holds one block on nearly every CU, so
+        # overlapping it with the backward chain measured 1.2 % slower (on: +2 % with 128x128)
+        if dev.type == "cuda" and os.environ.get("VINF_WGRAD_STREAM", "0") == "1":
             self.wgrad_stream = torch.cuda.Stream(device=dev)
         self._G = torch.zeros(L + 2, B, Dp, dtype=f32, device=dev)   # dL/dh_i, 0-padded rows
         self.G = self._G[:, :, :Dh]
@@ -260,7 +267,8 @@ class RealNVPVI:
         nh = self.cfg.n_hidden
         for i in range(nh):
             out = self.Act[l, i]
-            gemm.linear_fwd(a, P.c(f"l{l}.W{i}"), P.c(f"l{l}.b{i}"), out, relu=True)
+            gemm.linear_fwd(a, P.c(f"l{l}.W{i}"), P.c(f"l{l}.b{i}"), out, relu=True,
+                            mask_out=None if self.Mk is None else self.Mk[l, i])
             a = out
         st = self.ST[l]
         gemm.linear_fwd(a, P.c(f"l{l}.W{nh}"), P.c(f"l{l}.b{nh}"), st, relu=False)
@@ -323,7 +331,8 @@ class RealNVPVI:
                 wg.append((d, inp, P.g(f"l{l}.W{i}"), P.g(f"l{l}.b{i}")))
                 if i > 0:
                     nd = dH[i - 1]
-                    gemm.linear_dgrad(d, P.c(f"l{l}.W{i}"), nd, relu_of=self.Act[l, i - 1])
+                    gemm.linear_dgrad(d, P.c(f"l{l}.W{i}"), nd, relu_of=self.Act[l, i - 1],
+                                      relu_bits=None if self.Mk is None else self.Mk[l, i - 1])
                     d = nd
                 else:
                     gemm.linear_dgrad(d, P.c(f"l{l}.W0"), self._G[l + 1], accumulate=True)

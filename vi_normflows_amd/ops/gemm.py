@@ -41,11 +41,14 @@ def _mfma_ok(*ts) -> bool:
 
 
 def linear_fwd(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, out: torch.Tensor,
-               relu: bool = False) -> torch.Tensor:
+               relu: bool = False, mask_out: torch.Tensor | None = None) -> torch.Tensor:
+    """``mask_out`` (MFMA path, ReLU layers): also write the bitmask 1(out > 0) as uint8
+    [M, N/8] (bit e of byte j <-> column 8j+e) for :func:`linear_dgrad`'s ``relu_bits`` -
+    1/16 of the bytes of re-reading the bf16 activation in the backward. Ignored elsewhere."""
     if _mfma_ok(x) and x.is_cuda:
         from ._ext import native
 
-        native().gemm_nt(x, W, b, out, 1 if relu else 0)
+        native().gemm_nt(x, W, b, out, 1 if relu else 0, mask_out if relu else None)
         return out
     if b is not None:
         torch.addmm(b, x, W.t(), out=out)
@@ -57,12 +60,18 @@ def linear_fwd(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, out: to
 
 
 def linear_dgrad(dy: torch.Tensor, W: torch.Tensor, out: torch.Tensor,
-                 relu_of: torch.Tensor | None = None, accumulate: bool = False) -> torch.Tensor:
-    """out (+)= (dy @ W) * 1(relu_of > 0). ``out`` may be fp32 while dy/W are bf16."""
+                 relu_of: torch.Tensor | None = None, accumulate: bool = False,
+                 relu_bits: torch.Tensor | None = None) -> torch.Tensor:
+    """out (+)= (dy @ W) * 1(relu_of > 0). ``out`` may be fp32 while dy/W are bf16.
+    ``relu_bits`` (MFMA path): the bitmask :func:`linear_fwd` wrote for ``relu_of``, read
+    instead of the bf16 activation; the other paths use ``relu_of``."""
     if _mfma_ok(dy) and dy.is_cuda:
         from ._ext import native
 
-        native().gemm_nn(dy, W, relu_of, out, bool(accumulate))
+        if relu_bits is not None:
+            native().gemm_nn(dy, W, None, out, bool(accumulate), relu_bits)
+        else:
+            native().gemm_nn(dy, W, relu_of, out, bool(accumulate))
         return out
     if dy.is_cuda and out.dtype != dy.dtype:
         r = torch.mm(dy, W, out_dtype=out.dtype)
