@@ -1,4 +1,5 @@
 // TORCH_LIBRARY fragment for the MFMA GEMM family (csrc/kernels/gemm.hip).
+#include <vector>
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
@@ -176,6 +177,40 @@ void gemm_tn_group(at::TensorList dy, at::TensorList x, at::TensorList dW,
     wp = work.data_ptr<float>();
   }
   nf_launch_gemm_tn_group((int)n, pr, wp, cur_stream());
+}
+
+// Many dense weight gradients, one whole 256x256 tile per block, no split-K: computes the
+// tiles [tile0, tile0 + ntiles) of the problem list (tiles numbered problem after problem).
+void gemm_tn_multi(at::TensorList dy, at::TensorList x, at::TensorList dW,
+                   const c10::List<c10::optional<at::Tensor>>& db, int64_t tile0, int64_t ntiles) {
+  const size_t n = dy.size();
+  TORCH_CHECK(n >= 1 && n <= 48 && x.size() == n && dW.size() == n && db.size() == n,
+              "gemm_tn_multi: 1..48 problems with matching lists");
+  std::vector<NfTnProblem> pr(n);
+  long total = 0;
+  for (size_t p = 0; p < n; ++p) {
+    chk_mat(dy[p], "dy", at::kBFloat16);
+    chk_mat(x[p], "x", at::kBFloat16);
+    chk_mat(dW[p], "dW", at::kFloat);
+    const int K = dy[p].size(0), M = dy[p].size(1), N = x[p].size(1);
+    TORCH_CHECK(x[p].size(0) == K, "batch mismatch");
+    TORCH_CHECK(dW[p].size(0) == M && dW[p].size(1) == N, "dW shape");
+    TORCH_CHECK(K % 32 == 0 && M % 8 == 0 && N % 8 == 0, "K % 32, M % 8, N % 8 required");
+    TORCH_CHECK(ld2(dy[p]) < (1L << 31) && ld2(x[p]) < (1L << 31) && ld2(dW[p]) < (1L << 31),
+                "leading dimensions must fit in int32");
+    float* dbp = nullptr;
+    const c10::optional<at::Tensor> b = db.get(p);
+    if (b && b->defined()) {
+      TORCH_CHECK(b->scalar_type() == at::kFloat && b->numel() == M && b->is_contiguous(), "db");
+      dbp = b->data_ptr<float>();
+    }
+    pr[p] = NfTnProblem{dy[p].data_ptr(), ld2(dy[p]), x[p].data_ptr(), ld2(x[p]),
+                        dW[p].data_ptr<float>(), ld2(dW[p]), dbp, M, N, K};
+    total += nf_gemm256_tiles(M, N);
+  }
+  TORCH_CHECK(tile0 >= 0 && ntiles >= 1 && tile0 + ntiles <= total, "tile range outside the ",
+              total, " tiles of the problem list");
+  nf_launch_gemm256_tn_multi((int)n, pr.data(), (int)tile0, (int)ntiles, cur_stream());
 }
 
 // all `layers` weights of one kind (rows_per x C each, layer_stride elements apart in the flat
@@ -405,6 +440,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, bool accumulate, Tensor? hbits=None) -> ()");
   m.def("gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db) -> ()");
   m.def("gemm_tn_group(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, Tensor?[] skip, Tensor?[] cmask) -> ()");
+  m.def("gemm_tn_multi(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles) -> ()");
   m.def("fp8_quant_rows_strided(Tensor x, int layer_stride, int rows_per, int layers, int C, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("maf_fwd(Tensor x, Tensor o, float bound, Tensor(a!) u, Tensor(b!)? ubf, Tensor(c!)? uq, Tensor? amax_prev, Tensor(d!)? scale, Tensor(e!)? amax_cur, Tensor(f!) ldj, bool ldj_init) -> ()");
   m.def("maf_bwd(Tensor gu, Tensor u, Tensor o, float bound, float c_ldj, Tensor(a!) dout, Tensor(b!) gx) -> ()");
@@ -418,6 +454,7 @@ TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
   m.impl("gemm_nn", &gemm_nn);
   m.impl("gemm_tn", &gemm_tn);
   m.impl("gemm_tn_group", &gemm_tn_group);
+  m.impl("gemm_tn_multi", &gemm_tn_multi);
   m.impl("fp8_quant_rows", &fp8_quant_rows);
   m.impl("fp8_quant_rows_strided", &fp8_quant_rows_strided);
   m.impl("maf_fwd", &maf_fwd);

@@ -83,6 +83,11 @@ void nf_gemm256_set_depth(int d);
 int nf_launch_gemm256_tn_partials(const void* dy, long lddy, const void* x, long ldx, float* C,
                                   long ldc, long slab_stride, float* dbias, int M, int N, int K,
                                   int splits, hipStream_t stream);
+// many dense weight gradients (no split-K, one 256x256 tile per block): tiles numbered problem
+// after problem, one launch computes [tile0, tile0 + ntiles)
+int nf_gemm256_tiles(int M, int N);
+void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int ntiles,
+                                hipStream_t stream);
 // mode: 0 auto, 1 force 128x128, 2 force 256x256; depth: half-tiles in flight (3 or 4)
 void nf_gemm_set_mode(int mode, int depth);
 // fp8.hip (OCP e4m3): per-row quantisation and the MX-scaled K=128 MFMA GEMM

@@ -314,6 +314,43 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_group_kernel(GroupArgs g) {
   gemm256_body<false, false, EPI_F32, D, true>(a, local % tiles, local / tiles, smem);
 }
 
+// Weight gradients of MANY layers per launch, no split-K. A launch covers the global tile range
+// [tile0, tile0 + ntiles) of a problem list; every block owns one whole 256x256 output tile and
+// streams the full K (= batch) range, so there are no fp32 slabs and no reduce launch, and the
+// launch size is chosen by the caller (a multiple of the CU count: 40 tiles per RealNVP layer x
+// 32 layers = 1280 = 5 x 256). The descriptors travel in the kernarg segment (scalar loads).
+struct TnDesc {
+  const bf16_t* A;
+  const bf16_t* B;
+  float* C;
+  float* db;
+  int lda, ldb, ldc, M, N, K, start, staged;
+};
+constexpr int TN_MULTI_MAX = 48;
+struct TnMulti {
+  TnDesc d[TN_MULTI_MAX];
+  int n, tile0, ntiles;
+};
+
+template <int D>
+__global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+  const int id = t.tile0 + xcd_remap(blockIdx.x, t.ntiles);
+  int p = 0;
+  for (int q = 1; q < t.n; ++q)
+    if (id >= t.d[q].start) p = q;
+  const TnDesc& d = t.d[p];
+  GemmArgs a{};
+  a.A = d.A; a.lda = d.lda;
+  a.B = d.B; a.ldb = d.ldb;
+  a.C = d.C; a.ldc = d.ldc;
+  a.dbias = d.db;
+  a.M = d.M; a.N = d.N; a.K = d.K;
+  a.k_per_split = ((d.K + BK - 1) / BK) * BK;
+  a.staged = d.staged;
+  gemm256_body<false, false, EPI_F32, D, true>(a, id - d.start, 0, smem);
+}
+
 static int g_depth = 4;
 
 template <bool AK, bool BK_, int EPI, bool DB = false>
@@ -395,6 +432,57 @@ int nf_launch_gemm256_tn_partials(const void* dy, long lddy, const void* x, long
   a.M = M; a.N = N; a.K = K; a.k_per_split = kts * 64;
   g256::launch<false, false, EPI_F32, true>(a, used, stream);
   return used;
+}
+
+int nf_gemm256_tiles(int M, int N) {
+  return ((M + g256::BM - 1) / g256::BM) * ((N + g256::BN - 1) / g256::BN);
+}
+
+// tiles are numbered problem after problem (row-major tiles inside a problem); the launch
+// computes tiles [tile0, tile0 + ntiles) and may start or end inside a problem
+void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int ntiles,
+                                hipStream_t stream) {
+  if (ntiles <= 0) return;
+  g256::TnMulti t{};
+  int base = 0;
+  for (int p = 0; p < nprob; ++p) {
+    const NfTnProblem& q = pr[p];
+    const int tiles = nf_gemm256_tiles(q.M, q.N);
+    if (base + tiles > tile0 && base < tile0 + ntiles) {
+      if (t.n >= g256::TN_MULTI_MAX) {
+        fprintf(stderr, "vinf: gemm256_tn_multi: more than %d problems in one launch\n",
+                g256::TN_MULTI_MAX);
+        abort();
+      }
+      if (q.skip || q.cmask || q.K % 32 || q.M % 8 || q.N % 8) {
+        fprintf(stderr, "vinf: gemm256_tn_multi: dense problems with K %% 32, M/N %% 8 only\n");
+        abort();
+      }
+      g256::TnDesc& d = t.d[t.n++];
+      d.A = (const nf::bf16_t*)q.dy; d.lda = (int)q.lddy;
+      d.B = (const nf::bf16_t*)q.x; d.ldb = (int)q.ldx;
+      d.C = q.dW; d.ldc = (int)q.lddw;
+      d.db = q.db;
+      d.M = q.M; d.N = q.N; d.K = q.K;
+      d.start = base;
+      GemmArgs a{};
+      a.C = q.dW; a.ldc = q.lddw; a.N = q.N;
+      d.staged = staged_ok(a, EPI_F32);
+    }
+    base += tiles;
+  }
+  if (tile0 + ntiles > base || t.n == 0) {
+    fprintf(stderr, "vinf: gemm256_tn_multi: tile range [%d, %d) outside the %d tiles\n", tile0,
+            tile0 + ntiles, base);
+    abort();
+  }
+  t.tile0 = tile0;
+  t.ntiles = ntiles;
+  if (g256::g_depth == 3)
+    hipLaunchKernelGGL(g256::gemm256_multi_kernel<3>, dim3(ntiles), dim3(g256::NTHR), 0, stream, t);
+  else
+    hipLaunchKernelGGL(g256::gemm256_multi_kernel<4>, dim3(ntiles), dim3(g256::NTHR), 0, stream, t);
+  NF_HIP_CHECK(hipGetLastError());
 }
 
 void nf_launch_gemm256_tn_group(const GroupArgs& g, hipStream_t stream) {

@@ -1,4 +1,5 @@
-"""Data parallelism on the GPU code path (side-stream weight gradients + bucketed all-reduce
+"""Data parallelism on the GPU code path (per-layer, side-stream or cross-layer deferred weight
+gradients + bucketed all-reduce
 issued from backward hooks + graph-free eager DP step): two ranks share one MI355X over gloo
 (RCCL refuses two ranks per GPU); the DP gradient must equal the single-process gradient on
 the concatenated batch."""
@@ -27,7 +28,8 @@ def _port():
 def _worker(rank, world, port, eps_all, out_dir, side):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), VINF_DIST_BACKEND="gloo",
-                      VINF_WGRAD_STREAM=side)
+                      VINF_WGRAD_STREAM="1" if side == "1" else "0",
+                      VINF_WGRAD_DEFER="1" if side == "defer" else "0")
     from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI
     from vi_normflows_amd.parallel import dist as vdist
     from vi_normflows_amd.parallel.runner import DataParallelRunner
@@ -35,6 +37,7 @@ def _worker(rank, world, port, eps_all, out_dir, side):
     info = vdist.init()
     eng = RealNVPVI(RealNVPConfig(**CFG), batch=B, device=info.device, seed=100 + rank, rank=rank)
     assert (eng.wgrad_stream is not None) == (side == "1")
+    assert eng.wgrad_defer == (side == "defer")
     run = DataParallelRunner(eng, info, bucket_cap_mb=0.05)
     eng.eps_override = eps_all[rank * B:(rank + 1) * B].to(info.device)
     run.reducer.start_step()
@@ -48,7 +51,7 @@ def _worker(rank, world, port, eps_all, out_dir, side):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("side", ["0", "1"], ids=["serial", "side_stream"])
+@pytest.mark.parametrize("side", ["0", "1", "defer"], ids=["serial", "side_stream", "deferred"])
 def test_dp_gpu_side_stream_gradient_equals_single(tmp_path, side):
     from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI
 

@@ -221,3 +221,32 @@ def test_gemm_tn_group(gpu, B, mode):
         _check(dW, rW, 1e-4)
         if db is not None:
             _check(db, rb, 1e-4)
+
+
+@pytest.mark.parametrize("B", [4096, 96])
+@pytest.mark.parametrize("ranges", [[(0, None)], [(0, 7), (7, 20), (20, None)], [(0, 1), (1, 39), (39, None)]],
+                         ids=["one", "three", "edges"])
+def test_gemm_tn_multi(gpu, B, ranges):
+    """Many-problem weight-gradient launch (whole 256x256 tiles, no split-K): any partition of
+    the global tile range into launches == per-problem fp32 references (with/without db)."""
+    from vi_normflows_amd.ops.gemm import WgradPlan
+
+    torch.manual_seed(5)
+    shapes = [(800, 1024), (1024, 1024), (1024, 416), (264, 40), (520, 1024)]
+    items, refs = [], []
+    for p, (M, N) in enumerate(shapes):
+        dy, x = _bf(B, M, device=gpu), _bf(B, N, device=gpu)
+        dW = torch.full((M, N), 3.0, device=gpu)
+        db = torch.full((M,), 3.0, device=gpu) if p % 2 == 0 else None
+        items.append((dy, x, dW, db))
+        refs.append((dy.float().t() @ x.float(), dy.float().sum(0)))
+    plan = WgradPlan(items)
+    assert plan.total == 16 + 16 + 8 + 2 + 12
+    for t0, t1 in ranges:
+        t1 = plan.total if t1 is None else t1
+        plan.run(t0, t1 - t0)
+    torch.cuda.synchronize()
+    for (dy, x, dW, db), (rW, rb) in zip(items, refs):
+        _check(dW, rW, 1e-4)
+        if db is not None:
+            _check(db, rb, 1e-4)

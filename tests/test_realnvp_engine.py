@@ -92,6 +92,7 @@ def test_wgrad_side_stream_matches_serial_and_captures(gpu, monkeypatch):
 
     cfg = RealNVPConfig(dim=64, n_layers=6, hidden=128, anneal="none", init_out_std=0.1)
     monkeypatch.setenv("VINF_WGRAD_STREAM", "1")
+    monkeypatch.setenv("VINF_WGRAD_DEFER", "0")
     a = RealNVPVI(cfg, batch=512, device=gpu, seed=3)
     b = RealNVPVI(cfg, batch=512, device=gpu, seed=3)
     b.wgrad_stream = None
@@ -110,3 +111,39 @@ def test_wgrad_side_stream_matches_serial_and_captures(gpu, monkeypatch):
         rb.step()
     torch.cuda.synchronize()
     assert torch.equal(a.params.master, b.params.master)
+
+
+@pytest.mark.gpu
+def test_deferred_wgrad_matches_per_layer_and_captures(gpu, monkeypatch):
+    """Weight gradients batched across layers (whole-tile launches, full-batch K) == the
+    per-layer split-K schedule, for launch chunks that split layers mid-way; replayable in a
+    hipGraph with the DP hooks firing once per unit."""
+    from vi_normflows_amd.parallel.dist import DistInfo
+    from vi_normflows_amd.parallel.runner import DataParallelRunner
+
+    cfg = RealNVPConfig(dim=784, n_layers=5, hidden=512, anneal="none", init_out_std=0.1)
+    a = RealNVPVI(cfg, batch=1024, device=gpu, seed=3)
+    monkeypatch.setenv("VINF_WGRAD_DEFER", "0")
+    b = RealNVPVI(cfg, batch=1024, device=gpu, seed=3)
+    assert a.wgrad_defer and not b.wgrad_defer
+    a._wchunk = 7                          # 8+4+4 = 16 tiles per layer: chunks straddle layers
+    fired = []
+    a.unit_ready_hook = fired.append
+    for e in (a, b):
+        e._update_schedule()
+        e.forward()
+        e.backward()
+    torch.cuda.synchronize()
+    assert fired == [5, 4, 3, 2, 1, 0]
+    ga, gb = a.params.grad, b.params.grad
+    assert torch.isfinite(ga).all()
+    err = (ga - gb).abs().max().item()
+    assert err <= 1e-4 * gb.abs().max().item(), err
+    a.unit_ready_hook = None
+    a._wchunk = 256
+    ra = DataParallelRunner(a, DistInfo(device=torch.device(gpu)))
+    assert ra.capture(warmup=1)
+    for _ in range(3):
+        ra.step()
+    torch.cuda.synchronize()
+    assert torch.isfinite(a.params.master).all()

@@ -171,6 +171,17 @@ class RealNVPVI:
         self.dH2 = [[torch.empty(B, H, dtype=self.cdt, device=dev)
                      for _ in range(max(cfg.n_hidden, 1))] for _ in range(2)]
         self.dH = self.dH2[0]
+        # deferred weight gradients (MFMA path): every layer keeps its own gradient operands
+        # (dst, dH: ~6 GB at B = 32768 - nothing next to 288 GB of HBM) so the weight gradients
+        # of several layers run as ONE launch of whole 256x256 tiles with the full batch as K
+        # (ops.gemm.WgradPlan) instead of a split-K launch + reduce per layer
+        self.wgrad_defer = dev.type == "cuda" and os.environ.get("VINF_WGRAD_DEFER", "1") != "0"
+        self.dstL = self.dHL = None
+        self._wplan = None
+        if self.wgrad_defer:
+            self.dstL = torch.empty(L, B, Np, dtype=self.cdt, device=dev)
+            self.dHL = torch.empty(L, max(cfg.n_hidden, 1), B, H, dtype=self.cdt, device=dev)
+            self._wchunk = torch.cuda.get_device_properties(dev).multi_processor_count
         self.wgrad_stream = None
         # off by default: the 256x256 grouped launch holds one block on nearly every CU, so
         # overlapping it with the backward chain measured 1.2 % slower (on: +2 % with 128x128)
@@ -310,7 +321,67 @@ class RealNVPVI:
                          - 0.5 * (eps * eps).sum(1))
 
     # ------------------------------------------------------------------ backward
+    def _wgrad_plan(self):
+        """Weight-gradient problems of every layer in backward order (layer L-1 first, last
+        linear first), with the 1-based unit index each layer's gradients belong to."""
+        if self._wplan is None:
+            cfg, P = self.cfg, self.params
+            L, nh = cfg.n_layers, cfg.n_hidden
+            items, layer_last = [], {}
+            for l in range(L - 1, -1, -1):
+                d = self.dstL[l]
+                for i in range(nh, -1, -1):
+                    inp = self.Act[l, i - 1] if i > 0 else self.Hbf[l]
+                    items.append((d, inp, P.g(f"l{l}.W{i}"), P.g(f"l{l}.b{i}")))
+                    if i > 0:
+                        d = self.dHL[l, i - 1]
+                layer_last[l] = len(items) - 1
+            plan = gemm.WgradPlan(items)
+            plan.layer_end = {l: plan.end_of(k) for l, k in layer_last.items()}
+            self._wplan = plan
+        return self._wplan
+
+    def _backward_deferred(self):
+        """Backward with the weight gradients batched across layers (see ``wgrad_defer``):
+        the input-gradient chain runs layer by layer; whenever a CU-count worth of weight-
+        gradient tiles is ready it is launched (5 launches of 256 tiles for RealNVP-32 on
+        MI355X), and each layer's unit is handed to the DP reducer once its tiles are issued."""
+        cfg, P = self.cfg, self.params
+        L, nh = cfg.n_layers, cfg.n_hidden
+        c = -1.0 / self.B
+        plan = self._wgrad_plan()
+        chunk = self._wchunk
+        launched, next_unit = 0, L - 1
+        for l in range(L - 1, -1, -1):
+            dst = self.dstL[l]
+            fused.coupling_bwd(self.G[l + 2], self.ST[l][:, :cfg.half], self.h(l), dst, self.G[l],
+                               c=c, scale=cfg.scale_bound, gx_accumulate=False, s_is_hat=True)
+            d = dst
+            for i in range(nh, -1, -1):
+                if i > 0:
+                    nd = self.dHL[l, i - 1]
+                    gemm.linear_dgrad(d, P.c(f"l{l}.W{i}"), nd, relu_of=self.Act[l, i - 1],
+                                      relu_bits=None if self.Mk is None else self.Mk[l, i - 1])
+                    d = nd
+                else:
+                    gemm.linear_dgrad(d, P.c(f"l{l}.W0"), self._G[l + 1], accumulate=True)
+            avail = plan.layer_end[l]
+            while avail - launched >= chunk or (l == 0 and launched < avail):
+                n = min(chunk, avail - launched)
+                plan.run(launched, n)
+                launched += n
+                while next_unit >= 0 and plan.layer_end[next_unit] <= launched:
+                    if self.unit_ready_hook is not None:
+                        self.unit_ready_hook(next_unit + 1)
+                    next_unit -= 1
+        self._base_backward()
+        if self.unit_ready_hook is not None:
+            self.unit_ready_hook(0)
+
     def backward(self):
+        if (self.wgrad_defer and self.wgrad_stream is None and gemm.backend() == "mfma"
+                and self.cdt == torch.bfloat16):
+            return self._backward_deferred()
         cfg, P = self.cfg, self.params
         L, nh = cfg.n_layers, cfg.n_hidden
         c = -1.0 / self.B

@@ -121,3 +121,63 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dW: torch.Tensor,
         torch.mm(dy.t(), x, out=dW)
     if db is not None:
         torch.sum(dy, 0, dtype=db.dtype, out=db)
+
+
+def wgrad_tiles(M: int, N: int) -> int:
+    """256x256 output tiles of an [M, N] weight gradient (the unit of :class:`WgradPlan`)."""
+    return ((M + 255) // 256) * ((N + 255) // 256)
+
+
+class WgradPlan:
+    """Weight gradients of many layers, computed in launches of whole 256x256 tiles.
+
+    ``items`` = [(dy, x, dW, db), ...] in the order they become ready. Tiles are numbered
+    problem after problem; :meth:`run` computes the tile range [tile0, tile0 + ntiles) in ONE
+    launch of ``csrc/kernels/gemm256.hip`` ``gemm256_multi_kernel`` (no split-K: every block
+    streams the full batch for its tile and writes fp32 dW / db directly - no slabs, no reduce
+    launch). The caller picks ranges that are multiples of the CU count, so a RealNVP-32 step's
+    1280 weight-gradient tiles run as 5 launches of exactly one tile per CU.
+
+    Off the MFMA path (CPU, fp32, blas backend) a problem is computed by :func:`linear_wgrad`
+    when the range covering its LAST tile is run, so every problem is done exactly once.
+    """
+
+    MAX_PROBLEMS = 48   # kernarg descriptor table of one launch
+
+    def __init__(self, items):
+        self.items = list(items)
+        self.tiles = [wgrad_tiles(dy.shape[1], x.shape[1]) for dy, x, _, _ in self.items]
+        self.starts = [0]
+        for t in self.tiles:
+            self.starts.append(self.starts[-1] + t)
+        self.total = self.starts[-1]
+
+    def end_of(self, idx: int) -> int:
+        """Global tile index one past problem ``idx``."""
+        return self.starts[idx + 1]
+
+    def run(self, tile0: int, ntiles: int) -> None:
+        import bisect
+
+        if ntiles <= 0:
+            return
+        end = tile0 + ntiles
+        assert 0 <= tile0 and end <= self.total, (tile0, ntiles, self.total)
+        first = bisect.bisect_right(self.starts, tile0) - 1
+        last = bisect.bisect_left(self.starts, end) - 1        # problem holding tile end-1
+        if not all(_mfma_ok(dy) and dy.is_cuda for dy, _, _, _ in self.items[first:last + 1]):
+            for p in range(first, last + 1):
+                if tile0 < self.starts[p + 1] <= end:
+                    linear_wgrad(*self.items[p])
+            return
+        from ._ext import native
+
+        t = tile0
+        while t < end:
+            p0 = bisect.bisect_right(self.starts, t) - 1
+            p1 = min(last, p0 + self.MAX_PROBLEMS - 1)
+            stop = min(end, self.starts[p1 + 1])
+            ch = self.items[p0:p1 + 1]
+            native().gemm_tn_multi([i[0] for i in ch], [i[1] for i in ch], [i[2] for i in ch],
+                                   [i[3] for i in ch], t - self.starts[p0], stop - t)
+            t = stop
