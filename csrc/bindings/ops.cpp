@@ -259,6 +259,8 @@ void sumsq_guard(const at::Tensor& x, const at::Tensor& partial,
 
 }  // namespace
 
+void cu_hold(int64_t blocks, double usec) { nf_launch_cu_hold((int)blocks, (float)usec, cur_stream()); }
+
 TORCH_LIBRARY(vinf, m) {
   m.def("coupling_fwd(Tensor st, Tensor x, Tensor(a!) y, Tensor(b!)? ybf, Tensor(c!)? ssav, "
         "Tensor(d!) ldj, float scale, bool inverse, bool ldj_init) -> ()");
@@ -277,6 +279,7 @@ TORCH_LIBRARY(vinf, m) {
   m.def("flat_optimizer(int kind, Tensor(a!) p, Tensor g, Tensor(b!)? m, Tensor(c!)? v, "
         "Tensor(d!)? pbf, float lr, float b1, float b2, float eps, float wd, Tensor? step, "
         "float step_host, Tensor? gscale, float gscale_host, Tensor? skip) -> ()");
+  m.def("cu_hold(int blocks, float usec) -> ()", &cu_hold);
   m.def("sumsq_guard(Tensor x, Tensor(a!) partial, Tensor(b!)? out_sumsq, Tensor(c!)? skip, "
         "Tensor(d!)? scale, float max_norm, float base_scale) -> ()");
 }

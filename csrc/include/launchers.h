@@ -42,6 +42,8 @@ void nf_launch_flat_optimizer(int kind, float* p, const float* g, float* m, floa
                               long n, float lr, float b1, float b2, float eps, float wd,
                               const float* step_ptr, float step_host, const float* gscale_ptr,
                               float gscale_host, const float* skip_ptr, hipStream_t stream);
+// diagnostics: hold `blocks` CU slots for `usec` us (collective-occupancy emulation)
+void nf_launch_cu_hold(int blocks, float usec, hipStream_t stream);
 void nf_launch_sumsq_guard(const float* x, long n, float* partial, int npartial, float* out_sumsq,
                            float* out_skip, float* out_scale, float max_norm, float base_scale,
                            hipStream_t stream);

@@ -173,3 +173,28 @@ void nf_launch_sumsq_guard(const float* x, long n, float* partial, int npartial,
                      out_sumsq, out_skip, out_scale, max_norm, base_scale);
   NF_HIP_CHECK(hipGetLastError());
 }
+
+// ---------------------------------------------------------------------------------------------
+// Collective-occupancy emulator (diagnostics only): `blocks` workgroups of 256 threads that each
+// hold a CU slot for `usec` microseconds (s_memrealtime is a 100 MHz clock), launched on a side
+// stream where a DP gradient bucket's all-reduce would run. Lets a 1-GPU box measure how the
+// compute kernels behave when RCCL's channel blocks occupy CUs mid-backward. Every wave exits
+// on the time bound.
+namespace nf {
+__global__ void __launch_bounds__(256) cu_hold_kernel(long long ticks, int* sink) {
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  int n = 0;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+    __builtin_amdgcn_s_sleep(2);
+    ++n;
+  }
+  if (n < 0 && sink) sink[threadIdx.x] = n;  // never taken: keeps the loop observable
+}
+}  // namespace nf
+
+void nf_launch_cu_hold(int blocks, float usec, hipStream_t stream) {
+  if (blocks <= 0 || usec <= 0.f) return;
+  const long long ticks = (long long)(usec * 100.0f);
+  hipLaunchKernelGGL(nf::cu_hold_kernel, dim3(blocks), dim3(256), 0, stream, ticks, (int*)nullptr);
+  NF_HIP_CHECK(hipGetLastError());
+}
