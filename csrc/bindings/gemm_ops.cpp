@@ -213,6 +213,32 @@ void gemm_tn_multi(at::TensorList dy, at::TensorList x, at::TensorList dW,
   nf_launch_gemm256_tn_multi((int)n, pr.data(), (int)tile0, (int)ntiles, cur_stream());
 }
 
+// Conditioner input gradient of coupling layer l (gy = G + dy W, fp32, not stored) fused with the
+// backward of coupling layer l-1: dst = [dS_hat | dT | 0] (bf16), gx = gy e^s (fp32).
+void gemm_nn_cpl(const at::Tensor& dy, const at::Tensor& W, const at::Tensor& G,
+                 const at::Tensor& s_hat, const at::Tensor& x, const at::Tensor& dst,
+                 const at::Tensor& gx, double scale, double c) {
+  chk_mat(dy, "dy", at::kBFloat16);
+  chk_mat(W, "W", at::kBFloat16);
+  const int M = dy.size(0), K = dy.size(1), N = W.size(1);
+  TORCH_CHECK(W.size(0) == K, "W rows must equal dy cols");
+  TORCH_CHECK(K % 32 == 0 && N % 8 == 0, "K % 32 and N % 8 required");
+  for (const at::Tensor* t : {&G, &s_hat, &x, &dst, &gx})
+    TORCH_CHECK(t->is_cuda() && t->dim() == 2 && t->stride(1) == 1 && t->size(0) == M,
+                "gemm_nn_cpl: 2-D GPU operands with unit inner stride and M rows");
+  TORCH_CHECK(G.scalar_type() == at::kFloat && G.size(1) == N, "G: fp32 [M, N]");
+  const int Dh = x.size(1);
+  TORCH_CHECK(x.scalar_type() == at::kFloat && gx.scalar_type() == at::kFloat && gx.size(1) == Dh,
+              "x, gx: fp32 [M, Dh]");
+  TORCH_CHECK(s_hat.scalar_type() == at::kBFloat16 && s_hat.size(1) >= Dh, "s_hat: bf16 [M, >= Dh]");
+  TORCH_CHECK(dst.scalar_type() == at::kBFloat16 && dst.size(1) >= 2 * Dh && dst.size(1) <= Dh + N,
+              "dst: bf16 [M, 2 Dh .. Dh + N]");
+  nf_launch_gemm256_nn_cpl(dy.data_ptr(), ld2(dy), W.data_ptr(), ld2(W), G.data_ptr<float>(),
+                           ld2(G), M, N, K, s_hat.data_ptr(), ld2(s_hat), x.data_ptr<float>(),
+                           ld2(x), dst.data_ptr(), ld2(dst), (int)dst.size(1),
+                           gx.data_ptr<float>(), ld2(gx), Dh, (float)scale, (float)c, cur_stream());
+}
+
 // all `layers` weights of one kind (rows_per x C each, layer_stride elements apart in the flat
 // fp32 buffer starting at x) quantised per row in one launch
 void fp8_quant_rows_strided(const at::Tensor& x, int64_t layer_stride, int64_t rows_per,
@@ -441,6 +467,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db) -> ()");
   m.def("gemm_tn_group(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, Tensor?[] skip, Tensor?[] cmask) -> ()");
   m.def("gemm_tn_multi(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles) -> ()");
+  m.def("gemm_nn_cpl(Tensor dy, Tensor W, Tensor G, Tensor s_hat, Tensor x, Tensor(a!) dst, Tensor(b!) gx, float scale, float c) -> ()");
   m.def("fp8_quant_rows_strided(Tensor x, int layer_stride, int rows_per, int layers, int C, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("maf_fwd(Tensor x, Tensor o, float bound, Tensor(a!) u, Tensor(b!)? ubf, Tensor(c!)? uq, Tensor? amax_prev, Tensor(d!)? scale, Tensor(e!)? amax_cur, Tensor(f!) ldj, bool ldj_init) -> ()");
   m.def("maf_bwd(Tensor gu, Tensor u, Tensor o, float bound, float c_ldj, Tensor(a!) dout, Tensor(b!) gx) -> ()");
@@ -455,6 +482,7 @@ TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
   m.impl("gemm_tn", &gemm_tn);
   m.impl("gemm_tn_group", &gemm_tn_group);
   m.impl("gemm_tn_multi", &gemm_tn_multi);
+  m.impl("gemm_nn_cpl", &gemm_nn_cpl);
   m.impl("fp8_quant_rows", &fp8_quant_rows);
   m.impl("fp8_quant_rows_strided", &fp8_quant_rows_strided);
   m.impl("maf_fwd", &maf_fwd);

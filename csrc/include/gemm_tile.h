@@ -26,6 +26,8 @@ enum Epi : int {
   EPI_F32 = 1,           // C(fp32) = acc  (split-K slab when gridDim.y > 1)
   EPI_BF16_RELUMASK = 2, // C(bf16) = acc * 1(aux > 0)
   EPI_F32_ACC = 3,       // C(fp32) += acc
+  EPI_CPL_BWD = 4,       // gy = C(fp32) + acc, then the affine-coupling backward of the previous
+                         // flow layer (staged path only; see GemmArgs::cpl_*)
 };
 
 struct GemmArgs {
@@ -52,6 +54,17 @@ struct GemmArgs {
   unsigned char* mask_out;     // EPI_BF16 + relu: also write 1(y > 0) bits (staged path only)
   long ld_mask;                // bytes per mask row
   int aux_bits;                // EPI_BF16_RELUMASK: aux is such a bitmask (ld_aux in bytes)
+  // EPI_CPL_BWD: the input gradient of coupling layer l's conditioner completes
+  // gy = dL/dh_{l+1}, which is exactly the output gradient coupling layer l-1 needs. The
+  // epilogue finishes gy (= old C + acc, never stored) and applies layer l-1's backward
+  //   s = cpl_scale * tanh(s_hat)      (s_hat = aux, bf16, [M][ld_aux])
+  //   dS_hat = (gy x e^s + cpl_c) (cpl_scale - s^2 / cpl_scale),  dT = gy,  gx = gy e^s
+  // writing dst = [dS_hat | dT | 0-pad to cpl_pad] (bf16) and gx (fp32) for n < cpl_dh.
+  const float* cpl_x; long ld_cpl_x;   // x = h_{l-1} (fp32)
+  float* cpl_gx; long ld_cpl_gx;       // dL/dh_{l-1} (fp32, written)
+  bf16_t* cpl_dst; long ld_cpl_dst;    // conditioner output gradient of layer l-1
+  int cpl_dh, cpl_pad;
+  float cpl_scale, cpl_c;
 };
 
 // LDS-staged epilogue switch (VINF_GEMM_STAGED_EPI=0 restores the fragment-layout stores) and
@@ -70,6 +83,11 @@ inline bool staged_ok(const GemmArgs& a, int epi) {
     if (a.N % 8 || a.ldc % 8 || !al(a.C)) return false;
     if (epi == EPI_BF16_RELUMASK && !a.aux_bits && (a.ld_aux % 8 || !al(a.aux))) return false;
     return true;
+  }
+  if (epi == EPI_CPL_BWD) {
+    if (a.cpl_dh % 4 || a.ld_cpl_x % 4 || a.ld_cpl_gx % 4 || a.ld_cpl_dst % 4 || a.ld_aux % 4 ||
+        !al(a.cpl_x) || !al(a.cpl_gx) || ((unsigned long)a.cpl_dst & 7) || ((unsigned long)a.aux & 7))
+      return false;
   }
   return a.N % 4 == 0 && a.ldc % 4 == 0 && a.c_split_stride % 4 == 0 && al(a.C);
 }
@@ -283,7 +301,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
       // old C (fp32 accumulate) rows, in flight while the LDS writes drain
       const int q = lane & 15;
       float4 cv[16];
-      if constexpr (EPI == EPI_F32_ACC) {
+      if constexpr (EPI == EPI_F32_ACC || EPI == EPI_CPL_BWD) {
 #pragma unroll
         for (int it = 0; it < 16; ++it) {
           int m = m0 + hj * 64 + it * 4 + (lane >> 4), n = n0 + q * 4;
@@ -299,7 +317,36 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
         v4f v = *(const LDS_AS v4f*)(region + row * 256 + ((q ^ (row & 7)) << 4));
         const int m = m0 + hj * 64 + row, n = n0 + q * 4;
         if (m < a.M && n < a.N) {
-          if (EPI == EPI_F32) {
+          if constexpr (EPI == EPI_CPL_BWD) {
+            const float4 o = cv[it];
+            const float gy[4] = {o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]};
+            bf16_t* drow = a.cpl_dst + (long)m * a.ld_cpl_dst;
+            if (n < a.cpl_dh) {
+              const ushort4 sh = *reinterpret_cast<const ushort4*>(a.aux + (long)m * a.ld_aux + n);
+              const float4 xv = *reinterpret_cast<const float4*>(a.cpl_x + (long)m * a.ld_cpl_x + n);
+              const float shv[4] = {bf2f(sh.x), bf2f(sh.y), bf2f(sh.z), bf2f(sh.w)};
+              const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+              const float inv = 1.0f / a.cpl_scale;
+              float gx[4], dsh[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float sv = a.cpl_scale * tanhf(shv[e]);
+                const float es = __expf(sv);
+                const float ds = fmaf(gy[e] * xs[e], es, a.cpl_c);
+                dsh[e] = ds * (a.cpl_scale - sv * sv * inv);
+                gx[e] = gy[e] * es;
+              }
+              *reinterpret_cast<float4*>(a.cpl_gx + (long)m * a.ld_cpl_gx + n) =
+                  make_float4(gx[0], gx[1], gx[2], gx[3]);
+              ushort4 d0, d1;
+              d0.x = f2bf(dsh[0]); d0.y = f2bf(dsh[1]); d0.z = f2bf(dsh[2]); d0.w = f2bf(dsh[3]);
+              d1.x = f2bf(gy[0]); d1.y = f2bf(gy[1]); d1.z = f2bf(gy[2]); d1.w = f2bf(gy[3]);
+              *reinterpret_cast<ushort4*>(drow + n) = d0;
+              *reinterpret_cast<ushort4*>(drow + a.cpl_dh + n) = d1;
+            } else if (a.cpl_dh + n < a.cpl_pad) {   // zero the dst pad columns [2 Dh, pad)
+              *reinterpret_cast<ushort4*>(drow + a.cpl_dh + n) = make_ushort4(0, 0, 0, 0);
+            }
+          } else if (EPI == EPI_F32) {
             if (a.cmask) {
               const uchar4 mk = *reinterpret_cast<const uchar4*>(a.cmask + (long)m * a.N + n);
               v[0] = mk.x ? v[0] : 0.f; v[1] = mk.y ? v[1] : 0.f;

@@ -82,6 +82,13 @@ void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, co
                           long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
                           int N, int K, hipStream_t stream, int aux_is_bits = 0);
 void nf_gemm256_set_depth(int d);
+// input gradient of coupling layer l's conditioner (fp32, + G) fused with coupling layer l-1's
+// backward: writes dst (bf16 [dS_hat | dT | 0]) and gx; G itself is not written
+void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw, const float* G,
+                              long ldg, int M, int N, int K, const void* s_hat, long ld_s,
+                              const float* x, long ld_x, void* dst, long ld_dst, int dst_pad,
+                              float* gx, long ld_gx, int Dh, float scale, float c,
+                              hipStream_t stream);
 int nf_launch_gemm256_tn_partials(const void* dy, long lddy, const void* x, long ldx, float* C,
                                   long ldc, long slab_stride, float* dbias, int M, int N, int K,
                                   int splits, hipStream_t stream);

@@ -414,6 +414,35 @@ void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, co
   }
 }
 
+// Conditioner input gradient of coupling layer l fused with the backward of coupling layer l-1
+// (EPI_CPL_BWD, gemm_tile.h): gy = G[M][N] + dy[M][K] W[K][N] is consumed in the epilogue and
+// never stored; dst/gx of layer l-1 are written instead.
+void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw, const float* G,
+                              long ldg, int M, int N, int K, const void* s_hat, long ld_s,
+                              const float* x, long ld_x, void* dst, long ld_dst, int dst_pad,
+                              float* gx, long ld_gx, int Dh, float scale, float c,
+                              hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  GemmArgs a{};
+  a.A = (const nf::bf16_t*)dy; a.lda = lddy;
+  a.B = (const nf::bf16_t*)W; a.ldb = ldw;
+  a.C = (void*)G; a.ldc = ldg;
+  a.aux = (const nf::bf16_t*)s_hat; a.ld_aux = ld_s;
+  a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + 63) / 64) * 64;
+  a.cpl_x = x; a.ld_cpl_x = ld_x;
+  a.cpl_gx = gx; a.ld_cpl_gx = ld_gx;
+  a.cpl_dst = (nf::bf16_t*)dst; a.ld_cpl_dst = ld_dst;
+  a.cpl_dh = Dh; a.cpl_pad = dst_pad;
+  a.cpl_scale = scale; a.cpl_c = c;
+  if (Dh > N || dst_pad < 2 * Dh || dst_pad > Dh + N || !staged_ok(a, EPI_CPL_BWD) ||
+      !staged_enabled()) {
+    fprintf(stderr, "vinf: fused coupling-backward GEMM needs Dh <= N, 2 Dh <= pad <= Dh + N, "
+                    "4-element aligned rows and the staged epilogue\n");
+    abort();
+  }
+  g256::launch<true, false, EPI_CPL_BWD>(a, 1, stream);
+}
+
 // dW[M][N] (+ db[M]) = split-K partials of dy[K][M]^T x[K][N] written to `work` slabs (or
 // straight to dW/db when splits == 1); the caller reduces them (gemm.hip).
 int nf_launch_gemm256_tn_partials(const void* dy, long lddy, const void* x, long ldx, float* C,

@@ -176,6 +176,9 @@ class RealNVPVI:
         # of several layers run as ONE launch of whole 256x256 tiles with the full batch as K
         # (ops.gemm.WgradPlan) instead of a split-K launch + reduce per layer
         self.wgrad_defer = dev.type == "cuda" and os.environ.get("VINF_WGRAD_DEFER", "1") != "0"
+        # fuse coupling layer l-1's backward into the epilogue of layer l's last input-gradient
+        # GEMM (gemm_tile.h EPI_CPL_BWD): dL/dh_{l+1} is finished there and consumed at once
+        self.cpl_fuse = self.wgrad_defer and os.environ.get("VINF_CPL_FUSE", "1") != "0"
         self.dstL = self.dHL = None
         self._wplan = None
         if self.wgrad_defer:
@@ -352,17 +355,32 @@ class RealNVPVI:
         plan = self._wgrad_plan()
         chunk = self._wchunk
         launched, next_unit = 0, L - 1
+        fuse = self.cpl_fuse
+
+        def cpl_bwd(l):
+            fused.coupling_bwd(self.G[l + 2], self.ST[l][:, :cfg.half], self.h(l), self.dstL[l],
+                               self.G[l], c=c, scale=cfg.scale_bound, gx_accumulate=False,
+                               s_is_hat=True)
+
+        if fuse:
+            cpl_bwd(L - 1)
         for l in range(L - 1, -1, -1):
-            dst = self.dstL[l]
-            fused.coupling_bwd(self.G[l + 2], self.ST[l][:, :cfg.half], self.h(l), dst, self.G[l],
-                               c=c, scale=cfg.scale_bound, gx_accumulate=False, s_is_hat=True)
-            d = dst
+            if not fuse:
+                cpl_bwd(l)
+            d = self.dstL[l]
             for i in range(nh, -1, -1):
                 if i > 0:
                     nd = self.dHL[l, i - 1]
                     gemm.linear_dgrad(d, P.c(f"l{l}.W{i}"), nd, relu_of=self.Act[l, i - 1],
                                       relu_bits=None if self.Mk is None else self.Mk[l, i - 1])
                     d = nd
+                elif fuse and l > 0:
+                    # dL/dh_{l+1} = G[l+1] + d W0 is finished and consumed by layer l-1's
+                    # coupling backward in the same epilogue (writes dstL[l-1], G[l-1])
+                    gemm.linear_dgrad_coupling(d, P.c(f"l{l}.W0"), self._G[l + 1],
+                                               s_hat=self.ST[l - 1][:, :cfg.half],
+                                               x=self.h(l - 1), dst=self.dstL[l - 1],
+                                               gx=self.G[l - 1], scale=cfg.scale_bound, c=c)
                 else:
                     gemm.linear_dgrad(d, P.c(f"l{l}.W0"), self._G[l + 1], accumulate=True)
             avail = plan.layer_end[l]

@@ -86,6 +86,33 @@ def linear_dgrad(dy: torch.Tensor, W: torch.Tensor, out: torch.Tensor,
     return out
 
 
+def linear_dgrad_coupling(dy: torch.Tensor, W: torch.Tensor, G: torch.Tensor, s_hat: torch.Tensor,
+                          x: torch.Tensor, dst: torch.Tensor, gx: torch.Tensor, scale: float,
+                          c: float) -> None:
+    """Input gradient of a coupling conditioner fused with the PREVIOUS coupling layer's
+    backward (MFMA path: one GEMM whose epilogue does both, ``EPI_CPL_BWD``):
+
+        gy = G + dy @ W                       (dL/d h_{l+1}; G itself is left untouched)
+        s = scale * tanh(s_hat);  dst = [ (gy x e^s + c)(scale - s^2/scale) | gy | 0-pad ]
+        gx = gy e^s
+
+    Elsewhere: the two steps through torch (same math as ``ops.fused.coupling_bwd``)."""
+    if _mfma_ok(dy) and dy.is_cuda:
+        from ._ext import native
+
+        native().gemm_nn_cpl(dy, W, G, s_hat, x, dst, gx, float(scale), float(c))
+        return
+    Dh = x.shape[1]
+    gy = (G.float() + (dy.float() @ W.float()))[:, :Dh]
+    s = scale * torch.tanh(s_hat[:, :Dh].float())
+    es = torch.exp(s)
+    ds = (gy * x * es + c) * (scale - s * s / scale)
+    dst[:, :Dh].copy_(ds)
+    dst[:, Dh:2 * Dh].copy_(gy)
+    dst[:, 2 * Dh:].zero_()
+    gx.copy_(gy * es)
+
+
 def linear_wgrad_group(items) -> None:
     """Several weight gradients at once: ``items`` = [(dy, x, dW, db), ...] (<= 4).
 
