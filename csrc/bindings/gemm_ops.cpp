@@ -182,10 +182,14 @@ void gemm_tn_group(at::TensorList dy, at::TensorList x, at::TensorList dW,
 // Many dense weight gradients, one whole 256x256 tile per block, no split-K: computes the
 // tiles [tile0, tile0 + ntiles) of the problem list (tiles numbered problem after problem).
 void gemm_tn_multi(at::TensorList dy, at::TensorList x, at::TensorList dW,
-                   const c10::List<c10::optional<at::Tensor>>& db, int64_t tile0, int64_t ntiles) {
+                   const c10::List<c10::optional<at::Tensor>>& db, int64_t tile0, int64_t ntiles,
+                   const c10::List<c10::optional<at::Tensor>>& tiles,
+                   const c10::List<c10::optional<at::Tensor>>& cmask) {
   const size_t n = dy.size();
-  TORCH_CHECK(n >= 1 && n <= 48 && x.size() == n && dW.size() == n && db.size() == n,
-              "gemm_tn_multi: 1..48 problems with matching lists");
+  TORCH_CHECK(n >= 1 && n <= 40 && x.size() == n && dW.size() == n && db.size() == n,
+              "gemm_tn_multi: 1..40 problems with matching lists");
+  TORCH_CHECK((tiles.size() == 0 || tiles.size() == n) && (cmask.size() == 0 || cmask.size() == n),
+              "gemm_tn_multi: tiles / cmask lists must be empty or one entry per problem");
   std::vector<NfTnProblem> pr(n);
   long total = 0;
   for (size_t p = 0; p < n; ++p) {
@@ -206,7 +210,26 @@ void gemm_tn_multi(at::TensorList dy, at::TensorList x, at::TensorList dW,
     }
     pr[p] = NfTnProblem{dy[p].data_ptr(), ld2(dy[p]), x[p].data_ptr(), ld2(x[p]),
                         dW[p].data_ptr<float>(), ld2(dW[p]), dbp, M, N, K};
-    total += nf_gemm256_tiles(M, N);
+    int nt = nf_gemm256_tiles(M, N);
+    if (tiles.size() == n) {
+      const c10::optional<at::Tensor> tl = tiles.get(p);
+      if (tl && tl->defined()) {
+        TORCH_CHECK(tl->is_cuda() && tl->scalar_type() == at::kShort && tl->is_contiguous() &&
+                        tl->numel() >= 1 && tl->numel() <= nt,
+                    "tiles: int16 GPU list of active 256x256 tile ids");
+        pr[p].tiles = reinterpret_cast<const unsigned short*>(tl->data_ptr<int16_t>());
+        pr[p].ntiles_active = nt = (int)tl->numel();
+      }
+    }
+    if (cmask.size() == n) {
+      const c10::optional<at::Tensor> cm = cmask.get(p);
+      if (cm && cm->defined()) {
+        TORCH_CHECK(cm->is_cuda() && cm->scalar_type() == at::kByte && cm->is_contiguous() &&
+                        cm->numel() == (long)M * N && ld2(dW[p]) == N, "cmask [M,N] uint8, dense dW");
+        pr[p].cmask = cm->data_ptr<uint8_t>();
+      }
+    }
+    total += nt;
   }
   TORCH_CHECK(tile0 >= 0 && ntiles >= 1 && tile0 + ntiles <= total, "tile range outside the ",
               total, " tiles of the problem list");
@@ -314,7 +337,8 @@ void chk_ranges(const at::Tensor& r, long ntiles, const char* n) {
 }
 
 void masked_gemm_nt(const at::Tensor& x, const at::Tensor& W, const c10::optional<at::Tensor>& b,
-                    const at::Tensor& y, int64_t relu, const at::Tensor& krange) {
+                    const at::Tensor& y, int64_t relu, const at::Tensor& krange,
+                    const c10::optional<at::Tensor>& krange256) {
   chk_mat(x, "x", at::kBFloat16);
   chk_mat(W, "W", at::kBFloat16);
   chk_mat(y, "y", at::kBFloat16);
@@ -323,12 +347,18 @@ void masked_gemm_nt(const at::Tensor& x, const at::Tensor& W, const c10::optiona
   TORCH_CHECK(K % 32 == 0 && N % 8 == 0, "K % 32 and N % 8 required");
   chk_ranges(krange, (N + 127) / 128, "krange");
   const void* bp = (b && b->defined()) ? b->data_ptr() : nullptr;
+  const int* k256 = nullptr;
+  if (krange256 && krange256->defined()) {
+    chk_ranges(*krange256, (N + 255) / 256, "krange256");
+    k256 = krange256->data_ptr<int>();
+  }
   nf_launch_gemm_nt_masked(x.data_ptr(), ld2(x), W.data_ptr(), ld2(W), bp, y.data_ptr(), ld2(y), M,
-                           N, K, (int)relu, krange.data_ptr<int>(), cur_stream());
+                           N, K, (int)relu, krange.data_ptr<int>(), cur_stream(), k256);
 }
 
 void masked_gemm_nn(const at::Tensor& dy, const at::Tensor& W, const c10::optional<at::Tensor>& h,
-                    const at::Tensor& dx, const at::Tensor& krange, bool accumulate) {
+                    const at::Tensor& dx, const at::Tensor& krange, bool accumulate,
+                    const c10::optional<at::Tensor>& krange256) {
   chk_mat(dy, "dy", at::kBFloat16);
   chk_mat(W, "W", at::kBFloat16);
   const bool f32 = dx.scalar_type() == at::kFloat;
@@ -345,8 +375,16 @@ void masked_gemm_nn(const at::Tensor& dy, const at::Tensor& W, const c10::option
     ldh = ld2(*h);
   }
   TORCH_CHECK(!accumulate || f32, "accumulate needs an fp32 dx");
+  const int* k256 = nullptr;
+  if (krange256 && krange256->defined()) {
+    chk_ranges(*krange256, (N + 255) / 256, "krange256");
+    TORCH_CHECK(!hp || (ld2(*h) % 8 == 0 && ((uintptr_t)hp & 15) == 0),
+                "ReLU-mask operand rows must be 16-B aligned for the 256x256 kernel");
+    k256 = krange256->data_ptr<int>();
+  }
   nf_launch_gemm_nn_masked(dy.data_ptr(), ld2(dy), W.data_ptr(), ld2(W), hp, ldh, dx.data_ptr(),
-                           ld2(dx), f32, accumulate, M, N, K, krange.data_ptr<int>(), cur_stream());
+                           ld2(dx), f32, accumulate, M, N, K, krange.data_ptr<int>(), cur_stream(),
+                           k256);
 }
 
 void masked_gemm_tn(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dW,
@@ -459,14 +497,14 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("fp8_quant_rows(Tensor x, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("fp8_quant_tensor(Tensor x, Tensor(a!) q, Tensor amax_prev, Tensor(b!) scale, Tensor(c!) amax_cur) -> ()");
   m.def("gemm_fp8_nt(Tensor xq, Tensor sx, Tensor wq, Tensor sw, Tensor? b, Tensor(a!) y, int relu, Tensor? krange, Tensor(b!)? yq=None, Tensor? q_amax_prev=None, Tensor(c!)? q_scale=None, Tensor(d!)? q_amax_cur=None) -> ()");
-  m.def("masked_gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu, Tensor krange) -> ()");
-  m.def("masked_gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, Tensor krange, bool accumulate=False) -> ()");
+  m.def("masked_gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu, Tensor krange, Tensor? krange256=None) -> ()");
+  m.def("masked_gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, Tensor krange, bool accumulate=False, Tensor? krange256=None) -> ()");
   m.def("masked_gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db, Tensor skip) -> ()");
   m.def("gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu, Tensor(b!)? mask=None) -> ()");
   m.def("gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, bool accumulate, Tensor? hbits=None) -> ()");
   m.def("gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db) -> ()");
   m.def("gemm_tn_group(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, Tensor?[] skip, Tensor?[] cmask) -> ()");
-  m.def("gemm_tn_multi(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles) -> ()");
+  m.def("gemm_tn_multi(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles, Tensor?[] tiles, Tensor?[] cmask) -> ()");
   m.def("gemm_nn_cpl(Tensor dy, Tensor W, Tensor G, Tensor s_hat, Tensor x, Tensor(a!) dst, Tensor(b!) gx, float scale, float c) -> ()");
   m.def("fp8_quant_rows_strided(Tensor x, int layer_stride, int rows_per, int layers, int C, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("maf_fwd(Tensor x, Tensor o, float bound, Tensor(a!) u, Tensor(b!)? ubf, Tensor(c!)? uq, Tensor? amax_prev, Tensor(d!)? scale, Tensor(e!)? amax_cur, Tensor(f!) ldj, bool ldj_init) -> ()");

@@ -71,16 +71,23 @@ struct NfTnProblem {
   int M, N, K;
   const unsigned char* skip = nullptr;   // masked (MADE) weights: all-zero 128x128 tiles of dW
   const unsigned char* cmask = nullptr;  // [M][N] 0/1: zero the masked entries of dW
+  // gemm256_tn_multi only: the 256x256 tiles to compute (all-masked tiles are left out of the
+  // numbering and never written), ntiles_active of them; -1 = every tile
+  const unsigned short* tiles = nullptr;
+  int ntiles_active = -1;
 };
 long nf_gemm_tn_group_workspace(int nprob, const NfTnProblem* pr);
 void nf_launch_gemm_tn_group(int nprob, const NfTnProblem* pr, float* work, hipStream_t stream);
 // gemm256.hip: 256x256 8-phase kernel (forward / input-gradient products)
+// krange: optional per-256-column-tile K ranges [lo, hi) of a MADE-masked weight
 void nf_launch_gemm256_nt(const void* x, long ldx, const void* W, long ldw, const void* bias,
                           void* y, long ldy, int M, int N, int K, int relu, hipStream_t stream,
-                          void* mask_out = nullptr, long ld_mask = 0);
+                          void* mask_out = nullptr, long ld_mask = 0,
+                          const int* krange = nullptr);
 void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                           long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
-                          int N, int K, hipStream_t stream, int aux_is_bits = 0);
+                          int N, int K, hipStream_t stream, int aux_is_bits = 0,
+                          const int* krange = nullptr);
 void nf_gemm256_set_depth(int d);
 // input gradient of coupling layer l's conditioner (fp32, + G) fused with coupling layer l-1's
 // backward: writes dst (bf16 [dS_hat | dT | 0]) and gx; G itself is not written
@@ -130,10 +137,11 @@ void nf_launch_radial_bwd(const float* saved, const float* Z0, const float* AL, 
 // masked (MADE) GEMMs: per-N-tile K ranges [ntn][2] / per-tile skip flags [ntm*ntn] (128x128 tiles)
 void nf_launch_gemm_nt_masked(const void* x, long ldx, const void* W, long ldw, const void* bias,
                               void* y, long ldy, int M, int N, int K, int relu, const int* krange,
-                              hipStream_t stream);
+                              hipStream_t stream, const int* krange256 = nullptr);
 void nf_launch_gemm_nn_masked(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                               long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
-                              int N, int K, const int* krange, hipStream_t stream);
+                              int N, int K, const int* krange, hipStream_t stream,
+                              const int* krange256 = nullptr);
 void nf_launch_gemm_tn_masked(const void* dy, long lddy, const void* x, long ldx, float* dW,
                               long lddw, float* db, int M, int N, int K, int splits, float* work,
                               const unsigned char* skip, hipStream_t stream);

@@ -520,10 +520,17 @@ void nf_launch_gemm_tn(const void* dy, long lddy, const void* x, long ldx, float
 }
 
 // Masked variants (MADE): same kernels, with per-N-tile K ranges / per-tile skip flags.
+// krange256 (optional): the same K ranges for 256-column tiles; when given and the 256x256 kernel
+// is the better fit (use_256), the product runs there.
 void nf_launch_gemm_nt_masked(const void* x, long ldx, const void* W, long ldw, const void* bias,
                               void* y, long ldy, int M, int N, int K, int relu, const int* krange,
-                              hipStream_t stream) {
+                              hipStream_t stream, const int* krange256) {
   if (M <= 0 || N <= 0) return;
+  if (krange256 && use_256(M, N, K)) {
+    nf_launch_gemm256_nt(x, ldx, W, ldw, bias, y, ldy, M, N, K, relu, stream, nullptr, 0,
+                         krange256);
+    return;
+  }
   GemmArgs a{};
   a.A = (const bf16_t*)x; a.lda = ldx;
   a.B = (const bf16_t*)W; a.ldb = ldw;
@@ -536,8 +543,14 @@ void nf_launch_gemm_nt_masked(const void* x, long ldx, const void* W, long ldw, 
 
 void nf_launch_gemm_nn_masked(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                               long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
-                              int N, int K, const int* krange, hipStream_t stream) {
+                              int N, int K, const int* krange, hipStream_t stream,
+                              const int* krange256) {
   if (M <= 0 || N <= 0) return;
+  if (krange256 && use_256(M, N, K)) {
+    nf_launch_gemm256_nn(dy, lddy, W, ldw, aux, ld_aux, dx, lddx, dx_is_f32, accumulate, M, N, K,
+                         stream, 0, krange256);
+    return;
+  }
   GemmArgs a{};
   a.A = (const bf16_t*)dy; a.lda = lddy;
   a.B = (const bf16_t*)W; a.ldb = ldw;

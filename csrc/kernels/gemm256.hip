@@ -113,7 +113,13 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   int kbeg = split * a.k_per_split;
   int kend = kbeg + a.k_per_split;
   kend = kend < a.K ? kend : a.K;
-  const int nkt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (a.krange) {  // MADE weights: stream only the K-tiles where this N-tile's mask is non-zero
+    const int lo = a.krange[2 * tn], hi = a.krange[2 * tn + 1];
+    kbeg = kbeg > lo ? kbeg : lo;
+    kend = kend < hi ? kend : hi;
+  }
+  int nkt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (a.skip && a.skip[tm * ntn + tn] && !(DB && a.dbias != nullptr && tn == 0)) nkt = 0;
 
   v4f acc[4][8];
 #pragma unroll
@@ -324,9 +330,11 @@ struct TnDesc {
   const bf16_t* B;
   float* C;
   float* db;
+  const unsigned short* tiles;   // active tile ids of a masked problem (others never launched)
+  const unsigned char* cmask;    // [M][N] 0/1 applied to dW (MADE), or null
   int lda, ldb, ldc, M, N, K, start, staged;
 };
-constexpr int TN_MULTI_MAX = 48;
+constexpr int TN_MULTI_MAX = 40;   // 80-B descriptors: the table stays inside the 4 KiB kernarg
 struct TnMulti {
   TnDesc d[TN_MULTI_MAX];
   int n, tile0, ntiles;
@@ -348,7 +356,9 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
   a.M = d.M; a.N = d.N; a.K = d.K;
   a.k_per_split = ((d.K + BK - 1) / BK) * BK;
   a.staged = d.staged;
-  gemm256_body<false, false, EPI_F32, D, true>(a, id - d.start, 0, smem);
+  a.cmask = d.cmask;
+  const int local = d.tiles ? (int)d.tiles[id - d.start] : id - d.start;
+  gemm256_body<false, false, EPI_F32, D, true>(a, local, 0, smem);
 }
 
 static int g_depth = 4;
@@ -380,7 +390,7 @@ void nf_gemm256_set_depth(int d) { g256::g_depth = d == 3 ? 3 : 4; }
 // y[M][N] = act(x[M][K] W[N][K]^T + bias) -> bf16
 void nf_launch_gemm256_nt(const void* x, long ldx, const void* W, long ldw, const void* bias,
                           void* y, long ldy, int M, int N, int K, int relu, hipStream_t stream,
-                          void* mask_out, long ld_mask) {
+                          void* mask_out, long ld_mask, const int* krange) {
   if (M <= 0 || N <= 0) return;
   GemmArgs a{};
   a.A = (const nf::bf16_t*)x; a.lda = ldx;
@@ -389,15 +399,17 @@ void nf_launch_gemm256_nt(const void* x, long ldx, const void* W, long ldw, cons
   a.bias = (const nf::bf16_t*)bias;
   a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + 63) / 64) * 64; a.relu = relu;
   a.mask_out = (unsigned char*)mask_out; a.ld_mask = ld_mask;
+  a.krange = krange;
   g256::launch<true, true, EPI_BF16>(a, 1, stream);
 }
 
 // dx[M][N] = dy[M][K] W[K][N]  (* 1(aux>0) -> bf16)  or  fp32 dx (+)= ...
 void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                           long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
-                          int N, int K, hipStream_t stream, int aux_is_bits) {
+                          int N, int K, hipStream_t stream, int aux_is_bits, const int* krange) {
   if (M <= 0 || N <= 0) return;
   GemmArgs a{};
+  a.krange = krange;
   a.A = (const nf::bf16_t*)dy; a.lda = lddy;
   a.B = (const nf::bf16_t*)W; a.ldb = ldw;
   a.C = dx; a.ldc = lddx;
@@ -476,15 +488,16 @@ void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int
   int base = 0;
   for (int p = 0; p < nprob; ++p) {
     const NfTnProblem& q = pr[p];
-    const int tiles = nf_gemm256_tiles(q.M, q.N);
+    const int tiles = q.ntiles_active >= 0 ? q.ntiles_active : nf_gemm256_tiles(q.M, q.N);
     if (base + tiles > tile0 && base < tile0 + ntiles) {
       if (t.n >= g256::TN_MULTI_MAX) {
         fprintf(stderr, "vinf: gemm256_tn_multi: more than %d problems in one launch\n",
                 g256::TN_MULTI_MAX);
         abort();
       }
-      if (q.skip || q.cmask || q.K % 32 || q.M % 8 || q.N % 8) {
-        fprintf(stderr, "vinf: gemm256_tn_multi: dense problems with K %% 32, M/N %% 8 only\n");
+      if (q.skip || q.K % 32 || q.M % 8 || q.N % 8 || (q.cmask && q.lddw != q.N)) {
+        fprintf(stderr, "vinf: gemm256_tn_multi: K %% 32, M/N %% 8, active-tile lists instead of "
+                        "skip flags, dense dW with a cmask\n");
         abort();
       }
       g256::TnDesc& d = t.d[t.n++];
@@ -492,6 +505,8 @@ void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int
       d.B = (const nf::bf16_t*)q.x; d.ldb = (int)q.ldx;
       d.C = q.dW; d.ldc = (int)q.lddw;
       d.db = q.db;
+      d.tiles = q.tiles;
+      d.cmask = q.cmask;
       d.M = q.M; d.N = q.N; d.K = q.K;
       d.start = base;
       GemmArgs a{};

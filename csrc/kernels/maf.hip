@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(256) maf_fwd_kernel(const float* __restrict__ 
     if (blockIdx.x == 0 && threadIdx.x == 0) *scale_out = sc;
   }
   float amax = 0.f;
-  // grid-stride over rows (<= 256 blocks): one amax atomic per block, not per row
+  // grid-stride over rows: one amax atomic (at most) per block, not per row
   for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < B; row += gridDim.x * 4) {
     float sa = 0.f;
     const float* xr = x + (long)row * ldx;
@@ -86,9 +86,13 @@ __global__ void __launch_bounds__(256) maf_fwd_kernel(const float* __restrict__ 
     for (int off = 32; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
     if (lane == 0) red[threadIdx.x >> 6] = amax;
     __syncthreads();
-    if (threadIdx.x == 0)
-      atomicMax(reinterpret_cast<int*>(amax_cur),
-                __float_as_int(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+    if (threadIdx.x == 0) {
+      // amax >= 0, so int ordering == float ordering; a plain read first skips the atomic for
+      // most blocks once the running max has settled (the grid has up to 2048 blocks)
+      const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      if (bm > __hip_atomic_load(amax_cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(reinterpret_cast<int*>(amax_cur), __float_as_int(bm));
+    }
   }
 }
 
@@ -142,8 +146,11 @@ void nf_launch_maf_fwd(const float* x, long ldx, const void* o, long ldo, int B,
                        const float* amax_prev, float* scale_out, float* amax_cur, float* ldj,
                        int ldj_init, hipStream_t stream) {
   if (B <= 0) return;
+  // a memory-bound pass: >= 8 waves per SIMD (2048 blocks); with the e4m3 output each block
+  // folds its rows' amax into one (mostly skipped) atomic, so the grid is capped there
   const int nb = (B + 3) / 4;
-  hipLaunchKernelGGL(maf_fwd_kernel, dim3(nb < 256 ? nb : 256), dim3(256), 0, stream, x, ldx,
+  const int grid = uq ? (nb < 2048 ? nb : 2048) : nb;
+  hipLaunchKernelGGL(maf_fwd_kernel, dim3(grid), dim3(256), 0, stream, x, ldx,
                      (const bf16_t*)o, ldo, B, D, bound, u, ldu, (bf16_t*)ubf, ldub,
                      (unsigned char*)uq, lduq, amax_prev, scale_out, amax_cur, ldj, ldj_init);
   NF_HIP_CHECK(hipGetLastError());

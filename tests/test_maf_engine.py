@@ -94,3 +94,39 @@ def test_engine_gpu_matches_cpu_and_trains(gpu, precision):
         run.step()
     assert eg.loss.item() < sum(l0) / 5
     assert torch.isfinite(eg.params.master).all() and eg.n_skipped.item() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", [0, 2], ids=["auto", "force256"])
+def test_engine_deferred_masked_wgrad_and_256_kernels(gpu, tile, monkeypatch):
+    """Masked products on the 256x256 kernels (per-tile K ranges) and the deferred multi-layer
+    weight gradients (entirely-masked tiles never launched, dense mask in the epilogue) ==
+    the per-layer 128x128 split-K schedule; masked gradient entries exactly zero."""
+    cfg = MAFEngineConfig(dim=512, n_layers=3, hidden=768, init_out_std=0.3, precision="bf16")
+    x = torch.randn(512, 512, generator=torch.Generator().manual_seed(3)).to(gpu)
+    torch.ops.vinf.gemm_set_mode(tile, 4)
+    try:
+        a = MAFEngine(cfg, batch=512, device=gpu, seed=7)
+        a._wchunk = 5                       # chunks straddle problems and layers
+        monkeypatch.setenv("VINF_WGRAD_DEFER", "0")
+        torch.ops.vinf.gemm_set_mode(1 if tile == 0 else tile, 4)
+        b = MAFEngine(cfg, batch=512, device=gpu, seed=7)
+        assert a.wgrad_defer and not b.wgrad_defer
+        fired = []
+        a.unit_ready_hook = fired.append
+        for e in (a, b):
+            e.data_override = x
+            e._update_schedule()
+            e.forward()
+            e.backward()
+        torch.cuda.synchronize()
+    finally:
+        torch.ops.vinf.gemm_set_mode(0, 4)
+    assert fired == [2, 1, 0]
+    ga, gb = a.params.grad, b.params.grad
+    assert torch.isfinite(ga).all()
+    assert (ga - gb).norm() / gb.norm() < 2e-2
+    for l in range(cfg.n_layers):
+        mk = a._mask(l)
+        assert (a.params.g(f"l{l}.W1")[mk["M1"] == 0] == 0).all()
+        assert (a.params.g(f"l{l}.W2")[mk["M2"] == 0] == 0).all()

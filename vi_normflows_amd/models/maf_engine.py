@@ -146,6 +146,18 @@ class MAFEngine:
         self.dO = torch.empty(B, 2 * D, dtype=self.cdt, device=dev)
         self.dH = torch.empty(B, H, dtype=self.cdt, device=dev)
         self.noise = torch.empty(B, D, dtype=f32, device=dev)
+        # deferred weight gradients (GPU): every layer keeps its gradient operands so the masked
+        # weight gradients of several layers run as one launch of whole 256x256 tiles with the
+        # full batch as K, entirely-masked tiles left out (ops.gemm.WgradPlan) - 13 GB at
+        # B = 32768, nothing next to 288 GB of HBM
+        import os
+
+        self.wgrad_defer = dev.type == "cuda" and os.environ.get("VINF_WGRAD_DEFER", "1") != "0"
+        self._wplan = None
+        if self.wgrad_defer:
+            self.dOL = torch.empty(L, B, 2 * D, dtype=self.cdt, device=dev)
+            self.dHL = torch.empty(L, B, H, dtype=self.cdt, device=dev)
+            self._wchunk = torch.cuda.get_device_properties(dev).multi_processor_count
         if self.fp8:
             from ..ops.fp8 import DelayedScale
 
@@ -247,8 +259,10 @@ class MAFEngine:
             elif self.device.type == "cuda":
                 from ..ops._ext import native
 
-                native().masked_gemm_nt(self.Xbf[l], P.c(f"l{l}.W1"), b1, self.Hbf[l], 1, mk["P1"].fwd)
-                native().masked_gemm_nt(self.Hbf[l], P.c(f"l{l}.W2"), b2, self.O[l], 0, mk["P2"].fwd)
+                native().masked_gemm_nt(self.Xbf[l], P.c(f"l{l}.W1"), b1, self.Hbf[l], 1,
+                                        mk["P1"].fwd, mk["P1"].fwd256)
+                native().masked_gemm_nt(self.Hbf[l], P.c(f"l{l}.W2"), b2, self.O[l], 0,
+                                        mk["P2"].fwd, mk["P2"].fwd256)
             else:
                 gemm.linear_fwd(self.Xbf[l], P.c(f"l{l}.W1"), b1, self.Hbf[l], relu=True)
                 gemm.linear_fwd(self.Hbf[l], P.c(f"l{l}.W2"), b2, self.O[l], relu=False)
@@ -267,7 +281,50 @@ class MAFEngine:
         torch.mul(uL, 1.0 / self.B, out=self.gU)
 
     # ------------------------------------------------------------------ backward
+    def _wgrad_plan(self):
+        if self._wplan is None:
+            P, L = self.params, self.cfg.n_layers
+            items, ends = [], []
+            for l in range(L - 1, -1, -1):
+                mk = self._mask(l)
+                items.append((self.dOL[l], self.Hbf[l], P.g(f"l{l}.W2"), P.g(f"l{l}.b2"),
+                              mk["P2"].wtiles256, mk["M2u"]))
+                items.append((self.dHL[l], self.Xbf[l], P.g(f"l{l}.W1"), P.g(f"l{l}.b1"),
+                              mk["P1"].wtiles256, mk["M1u"]))
+                ends.append(len(items) - 1)
+            plan = gemm.WgradPlan(items)
+            plan.unit_ends = [(l, plan.end_of(k)) for l, k in zip(range(L - 1, -1, -1), ends)]
+            # tiles left out of the plan are never written: their (masked) gradients stay 0
+            P.grad.zero_()
+            self._wplan = plan
+        return self._wplan
+
+    def _backward_deferred(self):
+        """Input-gradient chain layer by layer; the masked weight gradients of all layers
+        in CU-count chunks of whole tiles (ops.gemm.WgradScheduler), the DP hook firing per
+        layer once its tiles are issued."""
+        from ..ops._ext import native
+
+        cfg, P = self.cfg, self.params
+        L = cfg.n_layers
+        plan = self._wgrad_plan()
+        sched = gemm.WgradScheduler(plan, plan.unit_ends, self._wchunk, self.unit_ready_hook)
+        gu, gx = self.gU, self.gX
+        for k, l in enumerate(range(L - 1, -1, -1)):
+            mk = self._mask(l)
+            dO, dH = self.dOL[l], self.dHL[l]
+            fused.maf_bwd(gu, self.X[l + 1], self.O[l], dO, gx, bound=cfg.alpha_bound,
+                          c_ldj=1.0 / self.B)
+            native().masked_gemm_nn(dO, P.c(f"l{l}.W2"), self.Hbf[l], dH, mk["P2"].bwd, False,
+                                    mk["P2"].bwd256)
+            native().masked_gemm_nn(dH, P.c(f"l{l}.W1"), None, gx, mk["P1"].bwd, True,
+                                    mk["P1"].bwd256)
+            sched.ready(plan.unit_ends[k][1], final=(l == 0))
+            gu, gx = gx, gu
+
     def backward(self):
+        if self.wgrad_defer and self.cdt == torch.bfloat16:
+            return self._backward_deferred()
         cfg, P = self.cfg, self.params
         L = cfg.n_layers
         gpu = self.device.type == "cuda"

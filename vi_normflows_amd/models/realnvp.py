@@ -353,8 +353,8 @@ class RealNVPVI:
         L, nh = cfg.n_layers, cfg.n_hidden
         c = -1.0 / self.B
         plan = self._wgrad_plan()
-        chunk = self._wchunk
-        launched, next_unit = 0, L - 1
+        sched = gemm.WgradScheduler(plan, [(l + 1, plan.layer_end[l]) for l in range(L - 1, -1, -1)],
+                                    self._wchunk, self.unit_ready_hook)
         fuse = self.cpl_fuse
 
         def cpl_bwd(l):
@@ -383,15 +383,7 @@ class RealNVPVI:
                                                gx=self.G[l - 1], scale=cfg.scale_bound, c=c)
                 else:
                     gemm.linear_dgrad(d, P.c(f"l{l}.W0"), self._G[l + 1], accumulate=True)
-            avail = plan.layer_end[l]
-            while avail - launched >= chunk or (l == 0 and launched < avail):
-                n = min(chunk, avail - launched)
-                plan.run(launched, n)
-                launched += n
-                while next_unit >= 0 and plan.layer_end[next_unit] <= launched:
-                    if self.unit_ready_hook is not None:
-                        self.unit_ready_hook(next_unit + 1)
-                    next_unit -= 1
+            sched.ready(plan.layer_end[l], final=(l == 0))
         self._base_backward()
         if self.unit_ready_hook is not None:
             self.unit_ready_hook(0)

@@ -169,11 +169,15 @@ class WgradPlan:
     when the range covering its LAST tile is run, so every problem is done exactly once.
     """
 
-    MAX_PROBLEMS = 48   # kernarg descriptor table of one launch
+    MAX_PROBLEMS = 40   # kernarg descriptor table of one launch
 
     def __init__(self, items):
-        self.items = list(items)
-        self.tiles = [wgrad_tiles(dy.shape[1], x.shape[1]) for dy, x, _, _ in self.items]
+        # (dy, x, dW, db) or (dy, x, dW, db, active_tiles, cmask): a masked (MADE) problem lists
+        # its not-entirely-masked 256x256 tiles (int16, ops.masked.MaskPlan.wtiles256) and the
+        # dense uint8 mask applied to dW; its other tiles are never computed nor written
+        self.items = [tuple(i) + (None, None) if len(i) == 4 else tuple(i) for i in items]
+        self.tiles = [wgrad_tiles(it[0].shape[1], it[1].shape[1]) if it[4] is None else
+                      int(it[4].numel()) for it in self.items]
         self.starts = [0]
         for t in self.tiles:
             self.starts.append(self.starts[-1] + t)
@@ -192,10 +196,13 @@ class WgradPlan:
         assert 0 <= tile0 and end <= self.total, (tile0, ntiles, self.total)
         first = bisect.bisect_right(self.starts, tile0) - 1
         last = bisect.bisect_left(self.starts, end) - 1        # problem holding tile end-1
-        if not all(_mfma_ok(dy) and dy.is_cuda for dy, _, _, _ in self.items[first:last + 1]):
+        if not all(_mfma_ok(it[0]) and it[0].is_cuda for it in self.items[first:last + 1]):
             for p in range(first, last + 1):
                 if tile0 < self.starts[p + 1] <= end:
-                    linear_wgrad(*self.items[p])
+                    dy, x, dW, db, _, cm = self.items[p]
+                    linear_wgrad(dy, x, dW, db)
+                    if cm is not None:
+                        dW.mul_(cm)
             return
         from ._ext import native
 
@@ -205,6 +212,35 @@ class WgradPlan:
             p1 = min(last, p0 + self.MAX_PROBLEMS - 1)
             stop = min(end, self.starts[p1 + 1])
             ch = self.items[p0:p1 + 1]
+            masked = any(i[4] is not None or i[5] is not None for i in ch)
             native().gemm_tn_multi([i[0] for i in ch], [i[1] for i in ch], [i[2] for i in ch],
-                                   [i[3] for i in ch], t - self.starts[p0], stop - t)
+                                   [i[3] for i in ch], t - self.starts[p0], stop - t,
+                                   [i[4] for i in ch] if masked else [],
+                                   [i[5] for i in ch] if masked else [])
             t = stop
+
+
+class WgradScheduler:
+    """Issues a :class:`WgradPlan` as the backward produces its operands.
+
+    ``unit_ends`` = [(unit, end_tile), ...] in backward order: ``unit``'s weight gradients are
+    the plan's tiles below ``end_tile``. :meth:`ready` (call after a layer's input-gradient
+    chain) launches every full chunk of ``chunk`` tiles now available (the CU count: one tile
+    per CU per launch), with ``final=True`` the rest as well; ``hook(unit)`` fires once all of
+    a unit's tiles are issued (the DP reducer's bucket trigger)."""
+
+    def __init__(self, plan: WgradPlan, unit_ends, chunk: int, hook=None):
+        self.plan, self.unit_ends, self.chunk, self.hook = plan, list(unit_ends), int(chunk), hook
+        self.launched = 0
+        self._next = 0
+
+    def ready(self, avail_end: int, final: bool = False) -> None:
+        while avail_end - self.launched >= self.chunk or (final and self.launched < avail_end):
+            n = min(self.chunk, avail_end - self.launched)
+            self.plan.run(self.launched, n)
+            self.launched += n
+            while (self._next < len(self.unit_ends)
+                   and self.unit_ends[self._next][1] <= self.launched):
+                if self.hook is not None:
+                    self.hook(self.unit_ends[self._next][0])
+                self._next += 1

@@ -67,6 +67,16 @@ class MaskPlan:
         self.bwd = tile_ranges(m.t()).to(dev).contiguous()      # dx = dy (W*M) : tiles over in
         self.wskip = skip_flags(m).to(dev).contiguous()         # dW tiles that are all masked
         self.skipped_fraction = masked_fraction(m)
+        # the same metadata for the 256x256 kernels (gemm256.hip): K ranges per 256-wide output
+        # tile, and the weight-gradient tiles that are NOT entirely masked (tile id = row-major
+        # over 256x256 tiles; the first tile column is kept for the bias gradient), which the
+        # multi-layer weight-gradient launch computes - the others are never launched
+        self.fwd256 = tile_ranges(m, 256).to(dev).contiguous()
+        self.bwd256 = tile_ranges(m.t(), 256).to(dev).contiguous()
+        sk = skip_flags(m, 256)
+        tn = (m.shape[1] + 255) // 256
+        act = [t for t in range(sk.numel()) if not sk[t] or t % tn == 0]
+        self.wtiles256 = torch.tensor(act, dtype=torch.int16).to(dev)
 
 
 _PLANS: dict = {}
