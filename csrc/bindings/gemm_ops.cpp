@@ -449,7 +449,8 @@ void gemm_fp8_nt(const at::Tensor& xq, const at::Tensor& sx, const at::Tensor& w
                  const at::Tensor& sw, const c10::optional<at::Tensor>& b, const at::Tensor& y,
                  int64_t relu, const c10::optional<at::Tensor>& krange,
                  const c10::optional<at::Tensor>& yq, const c10::optional<at::Tensor>& q_amax_prev,
-                 const c10::optional<at::Tensor>& q_scale, const c10::optional<at::Tensor>& q_amax_cur) {
+                 const c10::optional<at::Tensor>& q_scale, const c10::optional<at::Tensor>& q_amax_cur,
+                 const c10::optional<at::Tensor>& krange256) {
   chk_q(xq, "xq");
   chk_q(wq, "wq");
   chk_mat(y, "y", at::kBFloat16);
@@ -484,6 +485,23 @@ void gemm_fp8_nt(const at::Tensor& xq, const at::Tensor& sx, const at::Tensor& w
     qs = q_scale->data_ptr<float>();
     qac = q_amax_cur->data_ptr<float>();
   }
+  // the 256x256 kernel when the caller supplies its K ranges (or the weight is dense) and the
+  // product has a tile per CU (same rule as the bf16 products)
+  const bool dense = !(krange && krange->defined());
+  const bool has256 = krange256 && krange256->defined();
+  if ((dense || has256) && nf_gemm_prefer_256(M, N, K) && ld2(xq) % 16 == 0 && ld2(wq) % 16 == 0 &&
+      ld2(y) % 8 == 0 && (!qp || ldq % 8 == 0)) {
+    const int* k256 = nullptr;
+    if (has256) {
+      chk_ranges(*krange256, (N + 255) / 256, "krange256");
+      k256 = krange256->data_ptr<int>();
+    }
+    nf_launch_gemm256_fp8_nt(xq.data_ptr(), ld2(xq), sx.data_ptr<float>(),
+                             sx.numel() == M && M > 1, wq.data_ptr(), ld2(wq), sw.data_ptr<float>(),
+                             bp, y.data_ptr(), ld2(y), M, N, K, (int)relu, k256, qp, ldq, qap, qs,
+                             qac, cur_stream());
+    return;
+  }
   nf_launch_gemm_fp8_nt(xq.data_ptr(), ld2(xq), sx.data_ptr<float>(), sx.numel() == M && M > 1,
                         wq.data_ptr(), ld2(wq),
                         sw.data_ptr<float>(), bp, y.data_ptr(), ld2(y), M, N, K, (int)relu, kr,
@@ -496,7 +514,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("gemm_set_mode(int mode, int depth) -> ()", &gemm_set_mode);
   m.def("fp8_quant_rows(Tensor x, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("fp8_quant_tensor(Tensor x, Tensor(a!) q, Tensor amax_prev, Tensor(b!) scale, Tensor(c!) amax_cur) -> ()");
-  m.def("gemm_fp8_nt(Tensor xq, Tensor sx, Tensor wq, Tensor sw, Tensor? b, Tensor(a!) y, int relu, Tensor? krange, Tensor(b!)? yq=None, Tensor? q_amax_prev=None, Tensor(c!)? q_scale=None, Tensor(d!)? q_amax_cur=None) -> ()");
+  m.def("gemm_fp8_nt(Tensor xq, Tensor sx, Tensor wq, Tensor sw, Tensor? b, Tensor(a!) y, int relu, Tensor? krange, Tensor(b!)? yq=None, Tensor? q_amax_prev=None, Tensor(c!)? q_scale=None, Tensor(d!)? q_amax_cur=None, Tensor? krange256=None) -> ()");
   m.def("masked_gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu, Tensor krange, Tensor? krange256=None) -> ()");
   m.def("masked_gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, Tensor krange, bool accumulate=False, Tensor? krange256=None) -> ()");
   m.def("masked_gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db, Tensor skip) -> ()");

@@ -65,6 +65,17 @@ struct GemmArgs {
   bf16_t* cpl_dst; long ld_cpl_dst;    // conditioner output gradient of layer l-1
   int cpl_dh, cpl_pad;
   float cpl_scale, cpl_c;
+  // e4m3 operands (gemm256.hip FP8 instantiation, EPI_BF16): y = acc * f8_sa[m | 0] * f8_sb[n]
+  // + bias, and optionally an e4m3 copy of the stored bf16 y with a delayed per-tensor scale
+  // (q = e4m3(sat(y / s)), s = amax_prev / 448, amax_cur = max |y|) - the next fp8 GEMM's operand
+  const float* f8_sa;
+  int f8_sa_per_row;
+  const float* f8_sb;
+  unsigned char* f8_cq;
+  long ld_f8_cq;
+  const float* f8_q_amax_prev;
+  float* f8_q_scale_out;
+  float* f8_q_amax_cur;
 };
 
 // LDS-staged epilogue switch (VINF_GEMM_STAGED_EPI=0 restores the fragment-layout stores) and
@@ -190,7 +201,7 @@ __device__ __forceinline__ void epi_store(const GemmArgs& a, v4f v, int m, int n
 // acc[i][j]: n = n0 + i*16 + (lane>>4)*4 + r, m = m0 + j*16 + (lane&15)  (m0/n0 = the wave's
 // sub-tile origin), i < 4, j < NJ (WM = 16*NJ). Requires N % 8 == 0, ldc % 8 == 0 (bf16) /
 // ldc % 4 == 0 (fp32) and a 16-B aligned C (checked by the launchers).
-template <int EPI, int NJ>
+template <int EPI, int NJ, bool F8 = false>
 __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&acc)[4][NJ],
                                                 int m0, int n0, int split, char* region,
                                                 int lane) {
@@ -212,13 +223,39 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
       }
     }
     const bool relu = EPI == EPI_BF16 && a.relu;
+    // fp8 operands: rank-1 dequantisation factor sa[m] * sb[n] (1 for bf16 operands)
+    float sn[4][4], smj[NJ];
+    constexpr bool f8 = F8 && EPI == EPI_BF16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sn[i][r] = 1.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) smj[j] = 1.f;
+    if constexpr (f8) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int n = n0 + i * 16 + g * 4;
+        n = n < a.N ? n : a.N - 4;
+        const float4 t = *reinterpret_cast<const float4*>(a.f8_sb + n);
+        sn[i][0] = t.x; sn[i][1] = t.y; sn[i][2] = t.z; sn[i][3] = t.w;
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        int m = m0 + j * 16 + c;
+        m = m < a.M ? m : a.M - 1;
+        smj[j] = a.f8_sa_per_row ? a.f8_sa[m] : a.f8_sa[0];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int row = j * 16 + c;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float v0 = acc[i][j][0] + bv[i][0], v1 = acc[i][j][1] + bv[i][1];
-        float v2 = acc[i][j][2] + bv[i][2], v3 = acc[i][j][3] + bv[i][3];
+        float v0 = fmaf(acc[i][j][0], smj[j] * sn[i][0], bv[i][0]);
+        float v1 = fmaf(acc[i][j][1], smj[j] * sn[i][1], bv[i][1]);
+        float v2 = fmaf(acc[i][j][2], smj[j] * sn[i][2], bv[i][2]);
+        float v3 = fmaf(acc[i][j][3], smj[j] * sn[i][3], bv[i][3]);
         if (relu) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
         const unsigned lo = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
         const unsigned hi = (unsigned)f2bf(v2) | ((unsigned)f2bf(v3) << 16);
@@ -249,6 +286,14 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
           hv[it] = *reinterpret_cast<const uint4*>(a.aux + (long)m * a.ld_aux + n);
         }
       }
+    }
+    float qinv = 1.f, qamax = 0.f;
+    const bool f8out = F8 && EPI == EPI_BF16 && a.f8_cq != nullptr;
+    if (f8out) {
+      const float ap = *a.f8_q_amax_prev;
+      const float qs = ap > 0.f ? ap / 448.f : 1.f;
+      qinv = 1.f / qs;
+      if (blockIdx.x == 0 && threadIdx.x == 0) *a.f8_q_scale_out = qs;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -285,7 +330,35 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
           a.mask_out[(long)m * a.ld_mask + (n >> 3)] = (unsigned char)bits;
         }
         *reinterpret_cast<uint4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
+        if (f8out) {
+          const unsigned w4[4] = {o.x, o.y, o.z, o.w};
+          float f[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            f[2 * e] = __uint_as_float(w4[e] << 16);
+            f[2 * e + 1] = __uint_as_float(w4[e] & 0xffff0000u);
+          }
+          int q0 = 0, q1 = 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            qamax = fmaxf(qamax, fabsf(f[e]));
+            f[e] = fminf(fmaxf(f[e] * qinv, -448.f), 448.f);
+          }
+          q0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], q0, false);
+          q0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], q0, true);
+          q1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], q1, false);
+          q1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], q1, true);
+          *reinterpret_cast<uint2*>(a.f8_cq + (long)m * a.ld_f8_cq + n) =
+              make_uint2((unsigned)q0, (unsigned)q1);
+        }
       }
+    }
+    if (f8out) {  // one (mostly skipped) atomic per wave: amax >= 0, int order == float order
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) qamax = fmaxf(qamax, __shfl_xor(qamax, off));
+      if (lane == 0 &&
+          qamax > __hip_atomic_load(a.f8_q_amax_cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(reinterpret_cast<int*>(a.f8_q_amax_cur), __float_as_int(qamax));
     }
   } else {
 #pragma unroll

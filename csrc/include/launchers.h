@@ -118,6 +118,15 @@ void nf_launch_gemm_fp8_nt(const void* xq, long ldx, const float* sx, int sx_per
                            void* yq, long ldyq, const float* q_amax_prev, float* q_scale_out,
                            float* q_amax_cur, hipStream_t stream);
 int nf_gemm_tn_splits(int M, int N, int K);
+// the 256x256 kernels' auto rule (a tile per CU, K >= 256; VINF_GEMM_TILE / gemm_set_mode)
+bool nf_gemm_prefer_256(int M, int N, int K);
+// gemm256.hip F8 instantiation: same contract as nf_launch_gemm_fp8_nt on 256x256 tiles
+// (krange per 256-column tile)
+void nf_launch_gemm256_fp8_nt(const void* xq, long ldx, const float* sx, int sx_per_row,
+                              const void* wq, long ldw, const float* sw, const void* bias, void* y,
+                              long ldy, int M, int N, int K, int relu, const int* krange,
+                              void* yq, long ldyq, const float* q_amax_prev, float* q_scale_out,
+                              float* q_amax_cur, hipStream_t stream);
 
 // planar.hip / radial.hip (fused K-layer stacks; per-row parameter gradients)
 void nf_launch_planar_fwd(const float* z, const float* W, const float* U, const float* B, float* zK,

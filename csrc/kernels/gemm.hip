@@ -394,6 +394,8 @@ static bool use_256(int M, int N, int K) {
   return tiles >= device_cus() && K >= 256;
 }
 
+bool nf_gemm_prefer_256(int M, int N, int K) { return use_256(M, N, K); }
+
 static bool use_256_tn() {
   if (g_tile_mode < 0) use_256(1, 1, 1);  // resolve the env default
   return g_tile_mode == 3;

@@ -46,10 +46,40 @@ __device__ __forceinline__ int half_row(bool is_a, bool hi, int lr) {
               : ((lr >> 5) << 6) + (lr & 31) + (hi ? 32 : 0);
 }
 
-template <bool KMAJOR>
+// one 64x32 output quadrant x one K-tile: 16 bf16 16x16x32 MFMAs (8 without the tail's
+// second k-step) or 8 e4m3 16x16x128 scaled MFMAs
+#define NF_G256_QUAD(IO, JO, FB)                                                                  \
+  do {                                                                                            \
+    if constexpr (F8) {                                                                           \
+      _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                             \
+        const v8i fbi = cat16(FB[i][0], FB[i][1]);                                                \
+        _Pragma("unroll") for (int j = 0; j < 4; ++j)                                             \
+          acc[IO + i][JO + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(                 \
+              fbi, cat16(fa[j][0], fa[j][1]), acc[IO + i][JO + j], 0, 0, 0, 127, 0, 127);          \
+      }                                                                                           \
+    } else {                                                                                      \
+      _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) if (ks == 0 || two)                        \
+        _Pragma("unroll") for (int i = 0; i < 2; ++i)                                             \
+          _Pragma("unroll") for (int j = 0; j < 4; ++j)                                           \
+            acc[IO + i][JO + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                        \
+                FB[i][ks], fa[j][ks], acc[IO + i][JO + j], 0, 0, 0);                              \
+    }                                                                                             \
+  } while (0)
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef int v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v8i cat16(v8s lo, v8s hi) {
+  const v4i l = __builtin_bit_cast(v4i, lo), h = __builtin_bit_cast(v4i, hi);
+  return __builtin_shufflevector(l, h, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// EB: bytes per element (2 = bf16, 1 = e4m3); ld, k0, K in elements. A half-tile is 128 rows x
+// 128 bytes either way (64 bf16 or 128 e4m3 k-values per row).
+template <bool KMAJOR, int EB = 2>
 __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long ld, int row0,
                                            int rows_total, int k0, int K, bool is_a, bool hi,
                                            char* dst, int wave, int lane) {
+  constexpr int CE = 16 / EB;  // elements per 16-B chunk
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int piece = wave * 2 + i;  // 16 x 1 KiB
@@ -59,9 +89,9 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long
       const int lc = (lane & 7) ^ (r & 7);
       int gr = row0 + half_row(is_a, hi, r);
       gr = gr < rows_total ? gr : rows_total - 1;
-      int gk = k0 + lc * 8;
-      gk = gk < K ? gk : K - 8;
-      src = base + (long)gr * ld + gk;
+      int gk = k0 + lc * CE;
+      gk = gk < K ? gk : K - CE;
+      src = (const bf16_t*)((const char*)base + ((long)gr * ld + gk) * EB);
     } else {
       const int kr = piece * 4 + (lane >> 4);
       const int lc = (lane & 15) ^ mn_swz(kr);
@@ -101,8 +131,14 @@ __device__ __forceinline__ void vmwait_count(int cnt) {
   else vmwait<0>();
 }
 
-template <bool A_KMAJOR, bool B_KMAJOR, int EPI, int D, bool DB>
+// F8: e4m3 operands (both k-major), one v_mfma_scale_f32_16x16x128_f8f6f4 per (i, j) and K-tile
+// of 128 bytes in place of the two bf16 16x16x32 steps - the same LDS image and fragment reads
+// (a lane's 32 k-bytes are the chunks g and g + 4 the bf16 steps read), 2x the FLOPs per
+// MFMA cycle; block scales fixed at 2^0, the per-row / per-tensor scales applied in the epilogue.
+template <bool A_KMAJOR, bool B_KMAJOR, int EPI, int D, bool DB, bool F8 = false>
 __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int split, char* smem) {
+  constexpr int BKE = F8 ? 2 * BK : BK;  // K-tile in elements
+  constexpr int EB = F8 ? 1 : 2;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -114,11 +150,15 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   int kend = kbeg + a.k_per_split;
   kend = kend < a.K ? kend : a.K;
   if (a.krange) {  // MADE weights: stream only the K-tiles where this N-tile's mask is non-zero
-    const int lo = a.krange[2 * tn], hi = a.krange[2 * tn + 1];
+    const int lo = (a.krange[2 * tn] / BKE) * BKE, hi = a.krange[2 * tn + 1];
     kbeg = kbeg > lo ? kbeg : lo;
     kend = kend < hi ? kend : hi;
+    if (F8 && kend > kbeg) {  // whole 128-byte K-tiles (the extra columns hold zero weights)
+      kend = kbeg + ((kend - kbeg + BKE - 1) / BKE) * BKE;
+      kend = kend < a.K ? kend : a.K;
+    }
   }
-  int nkt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  int nkt = kend > kbeg ? (kend - kbeg + BKE - 1) / BKE : 0;
   if (a.skip && a.skip[tm * ntn + tn] && !(DB && a.dbias != nullptr && tn == 0)) nkt = 0;
 
   v4f acc[4][8];
@@ -150,11 +190,11 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   auto issue = [&](int t, int j) {
     if (t >= nkt) return;
     char* dst = smem + (t & 1) * BUF_BYTES + j * HALF_BYTES;
-    const int k0 = kbeg + t * BK;
+    const int k0 = kbeg + t * BKE;
     if (j == H_ALO || j == H_AHI)
-      stage_half<A_KMAJOR>(a.A, a.lda, m0, a.M, k0, kend, true, j == H_AHI, dst, wave, lane);
+      stage_half<A_KMAJOR, EB>(a.A, a.lda, m0, a.M, k0, kend, true, j == H_AHI, dst, wave, lane);
     else
-      stage_half<B_KMAJOR>(a.B, a.ldb, n0, a.N, k0, kend, false, j == H_BHI, dst, wave, lane);
+      stage_half<B_KMAJOR, EB>(a.B, a.ldb, n0, a.N, k0, kend, false, j == H_BHI, dst, wave, lane);
   };
   // valid halves issued at global phases (P - D, P]; half (t, j) is issued at 4t - 5 + j
   auto outstanding = [&](int P) {
@@ -173,7 +213,7 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
     v8s fa[4][2], fbl[2][2], fbh[2][2];
     for (int t = 0; t < nkt; ++t) {
       const char* buf = smem + (t & 1) * BUF_BYTES;
-      const bool two = (kend - (kbeg + t * BK)) > 32;
+      const bool two = F8 || (kend - (kbeg + t * BK)) > 32;
       const int P = 4 * t;
       // ---- r1: M0-3 x N0-1
 #pragma unroll
@@ -191,15 +231,7 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        if (ks == 0 || two)
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbl[i][ks], fa[j][ks], acc[i][j],
-                                                                  0, 0, 0);
+      NF_G256_QUAD(0, 0, fbl);
       if (do_db) db_mfma(accb[0], fa, two);
       __builtin_amdgcn_s_setprio(0);
       barrier();
@@ -214,15 +246,7 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        if (ks == 0 || two)
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[2 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbh[i][ks], fa[j][ks],
-                                                                      acc[2 + i][j], 0, 0, 0);
+      NF_G256_QUAD(2, 0, fbh);
       __builtin_amdgcn_s_setprio(0);
       barrier();
       // ---- r3: M4-7 x N2-3
@@ -236,15 +260,7 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        if (ks == 0 || two)
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[2 + i][4 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  fbh[i][ks], fa[j][ks], acc[2 + i][4 + j], 0, 0, 0);
+      NF_G256_QUAD(2, 4, fbh);
       if (do_db) db_mfma(accb[1], fa, two);
       __builtin_amdgcn_s_setprio(0);
       barrier();
@@ -253,15 +269,7 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
       vmwait_count<D>(outstanding(P + 4));
       barrier();
       __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        if (ks == 0 || two)
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[i][4 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbl[i][ks], fa[j][ks],
-                                                                      acc[i][4 + j], 0, 0, 0);
+      NF_G256_QUAD(0, 4, fbl);
       __builtin_amdgcn_s_setprio(0);
       barrier();
     }
@@ -280,8 +288,8 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   }
   if (a.staged) {
     barrier();  // every wave is past its last operand read; each wave reuses 16 KiB of LDS
-    epi_tile_staged<EPI, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, split, smem + wave * 16384,
-                            lane);
+    epi_tile_staged<EPI, 8, F8>(a, acc, m0 + wr * 128, n0 + wc * 64, split,
+                                smem + wave * 16384, lane);
     return;
   }
 #pragma unroll
@@ -297,12 +305,12 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   }
 }
 
-template <bool A_KMAJOR, bool B_KMAJOR, int EPI, int D, bool DB>
+template <bool A_KMAJOR, bool B_KMAJOR, int EPI, int D, bool DB, bool F8 = false>
 __global__ void __launch_bounds__(NTHR, 1) gemm256_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
-  gemm256_body<A_KMAJOR, B_KMAJOR, EPI, D, DB>(a, xcd_remap(blockIdx.x, ntm * ntn), blockIdx.y,
-                                                smem);
+  gemm256_body<A_KMAJOR, B_KMAJOR, EPI, D, DB, F8>(a, xcd_remap(blockIdx.x, ntm * ntn),
+                                                    blockIdx.y, smem);
 }
 
 // grouped weight gradients (same block layout as gemm.hip's gemm_group_kernel)
@@ -473,6 +481,40 @@ int nf_launch_gemm256_tn_partials(const void* dy, long lddy, const void* x, long
   a.M = M; a.N = N; a.K = K; a.k_per_split = kts * 64;
   g256::launch<false, false, EPI_F32, true>(a, used, stream);
   return used;
+}
+
+// y[M][N] = act((qx * sx) (qw * sw)^T + bias) -> bf16 (+ optional e4m3 copy of y), e4m3 operands
+// with K (bytes) % 128 == 0; krange: per-256-column-tile K ranges of a MADE-masked weight
+void nf_launch_gemm256_fp8_nt(const void* xq, long ldx, const float* sx, int sx_per_row,
+                              const void* wq, long ldw, const float* sw, const void* bias, void* y,
+                              long ldy, int M, int N, int K, int relu, const int* krange,
+                              void* yq, long ldyq, const float* q_amax_prev, float* q_scale_out,
+                              float* q_amax_cur, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  GemmArgs a{};
+  a.A = (const nf::bf16_t*)xq; a.lda = ldx;
+  a.B = (const nf::bf16_t*)wq; a.ldb = ldw;
+  a.C = y; a.ldc = ldy;
+  a.bias = (const nf::bf16_t*)bias;
+  a.M = M; a.N = N; a.K = K; a.k_per_split = K; a.relu = relu;
+  a.krange = krange;
+  a.f8_sa = sx; a.f8_sa_per_row = sx_per_row; a.f8_sb = sw;
+  a.f8_cq = (unsigned char*)yq; a.ld_f8_cq = ldyq;
+  a.f8_q_amax_prev = q_amax_prev; a.f8_q_scale_out = q_scale_out; a.f8_q_amax_cur = q_amax_cur;
+  a.staged = staged_ok(a, EPI_BF16);
+  if (K % 128 || ldx % 16 || ldw % 16 || N % 8 || !a.staged || (yq && ldyq % 8)) {
+    fprintf(stderr, "vinf: gemm256_fp8_nt needs K %% 128 == 0, 16-B rows, N %% 8 == 0 and the "
+                    "staged epilogue\n");
+    abort();
+  }
+  const int ntm = (M + g256::BM - 1) / g256::BM, ntn = (N + g256::BN - 1) / g256::BN;
+  if (g256::g_depth == 3)
+    hipLaunchKernelGGL((g256::gemm256_kernel<true, true, EPI_BF16, 3, false, true>),
+                       dim3(ntm * ntn), dim3(g256::NTHR), 0, stream, a);
+  else
+    hipLaunchKernelGGL((g256::gemm256_kernel<true, true, EPI_BF16, 4, false, true>),
+                       dim3(ntm * ntn), dim3(g256::NTHR), 0, stream, a);
+  NF_HIP_CHECK(hipGetLastError());
 }
 
 int nf_gemm256_tiles(int M, int N) {

@@ -108,3 +108,54 @@ def test_gemm_fp8_fused_output_quantisation(gpu):
     ref = (y.float() / s).clamp(-448, 448).to(torch.float8_e4m3fn)
     assert (yq.view(torch.uint8) != ref.view(torch.uint8)).float().mean() < 1e-3
     assert abs(st.amax[1].item() - y.float().abs().max().item()) < 1e-6
+
+
+@pytest.fixture
+def force256():
+    torch.ops.vinf.gemm_set_mode(2, 4)
+    yield
+    torch.ops.vinf.gemm_set_mode(0, 4)
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 512, 256), (1000, 272, 384), (2048, 1024, 1024)])
+def test_gemm256_fp8_matches_dequantised_product(gpu, force256, M, N, K):
+    """e4m3 instantiation of the 256x256 8-phase kernel (one scaled 16x16x128 MFMA per K-tile
+    of 128 bytes): per-row scales, bias, ReLU, fused e4m3 output and its amax."""
+    from vi_normflows_amd.ops.fp8 import DelayedScale, dequantize, gemm_fp8, quantize_rows
+
+    torch.manual_seed(M + K)
+    x, W = torch.randn(M, K, device=gpu), torch.randn(N, K, device=gpu) * 0.05
+    b = torch.randn(N, device=gpu)
+    xq, sx = quantize_rows(x)
+    wq, sw = quantize_rows(W)
+    st = DelayedScale(gpu)
+    st.amax[1] = 2.0
+    yq = torch.empty(M, N, device=gpu, dtype=torch.float8_e4m3fn)
+    y, s = gemm_fp8(xq, sx, wq, sw, b, True, out_q=yq, out_scale=st)
+    ref = (dequantize(xq, sx) @ dequantize(wq, sw).t() + b.to(torch.bfloat16).float()).clamp_min(0)
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 8e-3 * ref.abs().max().item(), err
+    refq = (y.float() / s).clamp(-448, 448).to(torch.float8_e4m3fn)
+    assert (yq.view(torch.uint8) != refq.view(torch.uint8)).float().mean() < 1e-3
+    assert abs(st.amax[1].item() - y.float().abs().max().item()) < 1e-6
+
+
+def test_gemm256_fp8_masked_k_ranges(gpu, force256):
+    """MADE-masked fp8 product with per-256-tile K ranges == the dense product of the masked
+    (zero) weights: the skipped K-tiles hold only zeros."""
+    from vi_normflows_amd.flows.made import made_degrees, made_masks
+    from vi_normflows_amd.ops.fp8 import gemm_fp8, quantize_rows
+    from vi_normflows_amd.ops.masked import MaskPlan
+
+    torch.manual_seed(4)
+    D, H = 512, 768
+    for order in (None, torch.arange(D, 0, -1)):
+        m1, _ = made_masks(*made_degrees(D, H, 1, order), 2)
+        m1 = m1.float().to(gpu)
+        plan = MaskPlan(m1)
+        x, W = torch.randn(1024, D, device=gpu), torch.randn(H, D, device=gpu) * 0.05 * m1
+        xq, sx = quantize_rows(x)
+        wq, sw = quantize_rows(W)
+        y = gemm_fp8(xq, sx, wq, sw, None, False, krange=plan.fwd, krange256=plan.fwd256)
+        yd = gemm_fp8(xq, sx, wq, sw, None, False)
+        assert torch.equal(y, yd)

@@ -252,10 +252,11 @@ class MAFEngine:
                 # h (bf16, kept for backward) and its e4m3 copy from one epilogue
                 _, sh = gemm_fp8(self.Xq, sxs, self.W1q[l * H:(l + 1) * H],
                                  self.s1[l * H:(l + 1) * H], b1, relu=True, krange=mk["P1"].fwd,
-                                 out=self.Hbf[l], out_q=self.Hq, out_scale=self.sh[l])
+                                 out=self.Hbf[l], out_q=self.Hq, out_scale=self.sh[l],
+                                 krange256=mk["P1"].fwd256)
                 gemm_fp8(self.Hq, sh, self.W2q[l * 2 * D:(l + 1) * 2 * D],
                          self.s2[l * 2 * D:(l + 1) * 2 * D], b2, relu=False,
-                         krange=mk["P2"].fwd, out=self.O[l])
+                         krange=mk["P2"].fwd, out=self.O[l], krange256=mk["P2"].fwd256)
             elif self.device.type == "cuda":
                 from ..ops._ext import native
 

@@ -83,10 +83,12 @@ class DelayedScale:
 
 
 def gemm_fp8(xq, sx, wq, sw, bias=None, relu=False, krange=None, out=None, out_q=None,
-             out_scale: "DelayedScale | None" = None):
+             out_scale: "DelayedScale | None" = None, krange256=None):
     """y = act((xq*sx) (wq*sw)^T + bias) in bf16 (GPU kernel). With ``out_q``/``out_scale``
     the epilogue also writes the e4m3 copy of y under ``out_scale``'s delayed scale (the next
-    fp8 GEMM's operand, no separate quantisation pass); returns (y, scale) then."""
+    fp8 GEMM's operand, no separate quantisation pass); returns (y, scale) then.
+    A dense product, or a masked one given its 256-tile K ranges ``krange256``, runs on the
+    256x256 8-phase kernel (gemm256.hip, e4m3 instantiation) when it has a tile per CU."""
     from ._ext import native
 
     M, N = xq.shape[0], wq.shape[0]
@@ -97,9 +99,10 @@ def gemm_fp8(xq, sx, wq, sw, bias=None, relu=False, krange=None, out=None, out_q
         st.amax[0].copy_(st.amax[1])
         st.amax[1].zero_()
         native().gemm_fp8_nt(xq, sx, wq, sw, b, y, int(relu), krange, out_q, st.amax[0:1],
-                             st.scale, st.amax[1:2])
+                             st.scale, st.amax[1:2], krange256)
         return y, st.scale
-    native().gemm_fp8_nt(xq, sx, wq, sw, b, y, int(relu), krange)
+    native().gemm_fp8_nt(xq, sx, wq, sw, b, y, int(relu), krange, None, None, None, None,
+                         krange256)
     return y
 
 
