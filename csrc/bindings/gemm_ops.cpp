@@ -376,15 +376,19 @@ void masked_gemm_nn(const at::Tensor& dy, const at::Tensor& W, const c10::option
   }
   TORCH_CHECK(!accumulate || f32, "accumulate needs an fp32 dx");
   const int* k256 = nullptr;
+  int segs = 1;
   if (krange256 && krange256->defined()) {
-    chk_ranges(*krange256, (N + 255) / 256, "krange256");
+    // [tiles, 2] (one K range per 256-column tile) or [tiles, 4] (two ranges)
+    const long nt = (N + 255) / 256;
+    segs = krange256->numel() == 4 * nt ? 2 : 1;
+    chk_ranges(*krange256, segs * nt, "krange256");
     TORCH_CHECK(!hp || (ld2(*h) % 8 == 0 && ((uintptr_t)hp & 15) == 0),
                 "ReLU-mask operand rows must be 16-B aligned for the 256x256 kernel");
     k256 = krange256->data_ptr<int>();
   }
   nf_launch_gemm_nn_masked(dy.data_ptr(), ld2(dy), W.data_ptr(), ld2(W), hp, ldh, dx.data_ptr(),
                            ld2(dx), f32, accumulate, M, N, K, krange.data_ptr<int>(), cur_stream(),
-                           k256);
+                           k256, segs);
 }
 
 void masked_gemm_tn(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dW,

@@ -87,7 +87,7 @@ void nf_launch_gemm256_nt(const void* x, long ldx, const void* W, long ldw, cons
 void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                           long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
                           int N, int K, hipStream_t stream, int aux_is_bits = 0,
-                          const int* krange = nullptr);
+                          const int* krange = nullptr, int krange_segs = 1);
 void nf_gemm256_set_depth(int d);
 // input gradient of coupling layer l's conditioner (fp32, + G) fused with coupling layer l-1's
 // backward: writes dst (bf16 [dS_hat | dT | 0]) and gx; G itself is not written
@@ -150,7 +150,7 @@ void nf_launch_gemm_nt_masked(const void* x, long ldx, const void* W, long ldw, 
 void nf_launch_gemm_nn_masked(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                               long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
                               int N, int K, const int* krange, hipStream_t stream,
-                              const int* krange256 = nullptr);
+                              const int* krange256 = nullptr, int krange256_segs = 1);
 void nf_launch_gemm_tn_masked(const void* dy, long lddy, const void* x, long ldx, float* dW,
                               long lddw, float* db, int M, int N, int K, int splits, float* work,
                               const unsigned char* skip, hipStream_t stream);

@@ -149,16 +149,31 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   int kbeg = split * a.k_per_split;
   int kend = kbeg + a.k_per_split;
   kend = kend < a.K ? kend : a.K;
+  // optional second K segment [kbeg2, kend2) streamed after the first (K-tiles n1 .. nkt-1):
+  // a MADE mask over a [mu | s] output pair is non-zero on one range in EACH half
+  int kbeg2 = 0, kend2 = 0, n2 = 0;
   if (a.krange) {  // MADE weights: stream only the K-tiles where this N-tile's mask is non-zero
-    const int lo = (a.krange[2 * tn] / BKE) * BKE, hi = a.krange[2 * tn + 1];
+    const int segs = a.krange_segs == 2 ? 2 : 1;
+    const int* r = a.krange + 2 * segs * tn;
+    const int lo = (r[0] / BKE) * BKE, hi = r[1];
     kbeg = kbeg > lo ? kbeg : lo;
     kend = kend < hi ? kend : hi;
     if (F8 && kend > kbeg) {  // whole 128-byte K-tiles (the extra columns hold zero weights)
       kend = kbeg + ((kend - kbeg + BKE - 1) / BKE) * BKE;
       kend = kend < a.K ? kend : a.K;
     }
+    if (segs == 2 && r[3] > r[2]) {  // (split-K is not combined with two segments)
+      kbeg2 = (r[2] / BKE) * BKE;
+      kend2 = r[3] < a.K ? r[3] : a.K;
+      if (F8) {
+        kend2 = kbeg2 + ((kend2 - kbeg2 + BKE - 1) / BKE) * BKE;
+        kend2 = kend2 < a.K ? kend2 : a.K;
+      }
+      n2 = (kend2 - kbeg2 + BKE - 1) / BKE;
+    }
   }
-  int nkt = kend > kbeg ? (kend - kbeg + BKE - 1) / BKE : 0;
+  const int n1 = kend > kbeg ? (kend - kbeg + BKE - 1) / BKE : 0;
+  int nkt = n1 + n2;
   if (a.skip && a.skip[tm * ntn + tn] && !(DB && a.dbias != nullptr && tn == 0)) nkt = 0;
 
   v4f acc[4][8];
@@ -190,11 +205,13 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   auto issue = [&](int t, int j) {
     if (t >= nkt) return;
     char* dst = smem + (t & 1) * BUF_BYTES + j * HALF_BYTES;
-    const int k0 = kbeg + t * BKE;
+    const bool s2 = t >= n1;
+    const int k0 = s2 ? kbeg2 + (t - n1) * BKE : kbeg + t * BKE;
+    const int ke = s2 ? kend2 : kend;
     if (j == H_ALO || j == H_AHI)
-      stage_half<A_KMAJOR, EB>(a.A, a.lda, m0, a.M, k0, kend, true, j == H_AHI, dst, wave, lane);
+      stage_half<A_KMAJOR, EB>(a.A, a.lda, m0, a.M, k0, ke, true, j == H_AHI, dst, wave, lane);
     else
-      stage_half<B_KMAJOR, EB>(a.B, a.ldb, n0, a.N, k0, kend, false, j == H_BHI, dst, wave, lane);
+      stage_half<B_KMAJOR, EB>(a.B, a.ldb, n0, a.N, k0, ke, false, j == H_BHI, dst, wave, lane);
   };
   // valid halves issued at global phases (P - D, P]; half (t, j) is issued at 4t - 5 + j
   auto outstanding = [&](int P) {
@@ -213,7 +230,8 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
     v8s fa[4][2], fbl[2][2], fbh[2][2];
     for (int t = 0; t < nkt; ++t) {
       const char* buf = smem + (t & 1) * BUF_BYTES;
-      const bool two = F8 || (kend - (kbeg + t * BK)) > 32;
+      const bool two = F8 || (t >= n1 ? (kend2 - (kbeg2 + (t - n1) * BK)) > 32
+                                       : (kend - (kbeg + t * BK)) > 32);
       const int P = 4 * t;
       // ---- r1: M0-3 x N0-1
 #pragma unroll
@@ -305,12 +323,46 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   }
 }
 
+// Streamed K-tiles of column tile tn under a MADE K-range plan (one or two ranges).
+__device__ __forceinline__ int krange_len(const GemmArgs& a, int tn) {
+  const int segs = a.krange_segs == 2 ? 2 : 1;
+  const int* r = a.krange + 2 * segs * tn;
+  int len = r[1] > r[0] ? r[1] - r[0] : 0;
+  if (segs == 2 && r[3] > r[2]) len += r[3] - r[2];
+  return len;
+}
+
 template <bool A_KMAJOR, bool B_KMAJOR, int EPI, int D, bool DB, bool F8 = false>
 __global__ void __launch_bounds__(NTHR, 1) gemm256_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
-  gemm256_body<A_KMAJOR, B_KMAJOR, EPI, D, DB, F8>(a, xcd_remap(blockIdx.x, ntm * ntn),
-                                                    blockIdx.y, smem);
+  if (!a.pair_tiles) {
+    gemm256_body<A_KMAJOR, B_KMAJOR, EPI, D, DB, F8>(a, xcd_remap(blockIdx.x, ntm * ntn),
+                                                      blockIdx.y, smem);
+    return;
+  }
+  // MADE-masked products: column tiles stream very different K lengths (a triangular mask:
+  // 1:2:3:4), and one tile per block leaves the launch waiting on the CUs that drew two long
+  // tiles. Each block instead takes, for one row tile tm, the column tiles of rank p and
+  // ntn-1-p in descending K length (equal sums for a triangular plan): one balanced round,
+  // and the two tiles share the A row panel.
+  const int half = ntn >> 1;
+  const int b = xcd_remap(blockIdx.x, ntm * half);
+  const int tm = b / half, p = b % half;
+  int tn_a = 0, tn_b = 0;
+  for (int c = 0; c < ntn; ++c) {  // rank by (length desc, index asc); uniform scalar loop
+    const int lc = krange_len(a, c);
+    int rank = 0;
+    for (int o = 0; o < ntn; ++o) {
+      const int lo = krange_len(a, o);
+      rank += (lo > lc || (lo == lc && o < c)) ? 1 : 0;
+    }
+    if (rank == p) tn_a = c;
+    if (rank == ntn - 1 - p) tn_b = c;
+  }
+  gemm256_body<A_KMAJOR, B_KMAJOR, EPI, D, DB, F8>(a, tm * ntn + tn_a, 0, smem);
+  __syncthreads();  // the second tile's LDS-DMA reuses what the first tile's epilogue staged
+  gemm256_body<A_KMAJOR, B_KMAJOR, EPI, D, DB, F8>(a, tm * ntn + tn_b, 0, smem);
 }
 
 // grouped weight gradients (same block layout as gemm.hip's gemm_group_kernel)
@@ -371,6 +423,16 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
 
 static int g_depth = 4;
 
+int device_cus_256() {
+  static const int n = [] {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return cus;
+  }();
+  return n;
+}
+
 template <bool AK, bool BK_, int EPI, bool DB = false>
 void launch(GemmArgs a, int splits, hipStream_t stream) {
   a.staged = staged_ok(a, EPI);
@@ -379,7 +441,15 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
     abort();
   }
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
-  dim3 grid(ntm * ntn, splits), block(NTHR);
+  // pair the column tiles of MADE-masked products (see gemm256_kernel) when that still gives
+  // every CU a block; VINF_GEMM_PAIR=0 disables, =2 forces (tests)
+  static const int pair_env = [] {
+    const char* e = getenv("VINF_GEMM_PAIR");
+    return e ? atoi(e) : 1;
+  }();
+  a.pair_tiles = pair_env && a.krange && splits == 1 && ntn % 2 == 0 &&
+                 (pair_env == 2 || (long)ntm * (ntn / 2) >= device_cus_256());
+  dim3 grid(a.pair_tiles ? ntm * (ntn / 2) : ntm * ntn, splits), block(NTHR);
   if (g_depth == 4)
     hipLaunchKernelGGL((gemm256_kernel<AK, BK_, EPI, 4, DB>), grid, block, 0, stream, a);
   else
@@ -414,10 +484,12 @@ void nf_launch_gemm256_nt(const void* x, long ldx, const void* W, long ldw, cons
 // dx[M][N] = dy[M][K] W[K][N]  (* 1(aux>0) -> bf16)  or  fp32 dx (+)= ...
 void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                           long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
-                          int N, int K, hipStream_t stream, int aux_is_bits, const int* krange) {
+                          int N, int K, hipStream_t stream, int aux_is_bits, const int* krange,
+                          int krange_segs) {
   if (M <= 0 || N <= 0) return;
   GemmArgs a{};
   a.krange = krange;
+  a.krange_segs = krange_segs;
   a.A = (const nf::bf16_t*)dy; a.lda = lddy;
   a.B = (const nf::bf16_t*)W; a.ldb = ldw;
   a.C = dx; a.ldc = lddx;
@@ -508,12 +580,17 @@ void nf_launch_gemm256_fp8_nt(const void* xq, long ldx, const float* sx, int sx_
     abort();
   }
   const int ntm = (M + g256::BM - 1) / g256::BM, ntn = (N + g256::BN - 1) / g256::BN;
+  const char* pe = getenv("VINF_GEMM_PAIR");
+  const int pv = pe ? atoi(pe) : 1;   // 0 off, 1 auto, 2 always (tests)
+  a.pair_tiles = pv && krange && ntn % 2 == 0 &&
+                 (pv == 2 || (long)ntm * (ntn / 2) >= g256::device_cus_256());
+  const int nblk = a.pair_tiles ? ntm * (ntn / 2) : ntm * ntn;
   if (g256::g_depth == 3)
     hipLaunchKernelGGL((g256::gemm256_kernel<true, true, EPI_BF16, 3, false, true>),
-                       dim3(ntm * ntn), dim3(g256::NTHR), 0, stream, a);
+                       dim3(nblk), dim3(g256::NTHR), 0, stream, a);
   else
     hipLaunchKernelGGL((g256::gemm256_kernel<true, true, EPI_BF16, 4, false, true>),
-                       dim3(ntm * ntn), dim3(g256::NTHR), 0, stream, a);
+                       dim3(nblk), dim3(g256::NTHR), 0, stream, a);
   NF_HIP_CHECK(hipGetLastError());
 }
 

@@ -146,10 +146,10 @@ void nf_launch_maf_fwd(const float* x, long ldx, const void* o, long ldo, int B,
                        const float* amax_prev, float* scale_out, float* amax_cur, float* ldj,
                        int ldj_init, hipStream_t stream) {
   if (B <= 0) return;
-  // a memory-bound pass: >= 8 waves per SIMD (2048 blocks); with the e4m3 output each block
-  // folds its rows' amax into one (mostly skipped) atomic, so the grid is capped there
+  // a memory-bound pass: one wave per row, full grid; with the e4m3 output each block folds its
+  // rows' amax into one atomic that a plain read skips once the running max has settled
   const int nb = (B + 3) / 4;
-  const int grid = uq ? (nb < 2048 ? nb : 2048) : nb;
+  const int grid = nb;
   hipLaunchKernelGGL(maf_fwd_kernel, dim3(grid), dim3(256), 0, stream, x, ldx,
                      (const bf16_t*)o, ldo, B, D, bound, u, ldu, (bf16_t*)ubf, ldub,
                      (unsigned char*)uq, lduq, amax_prev, scale_out, amax_cur, ldj, ldj_init);

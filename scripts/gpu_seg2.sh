@@ -1,0 +1,13 @@
+#!/bin/bash
+# Two K ranges per tile for MADE [mu | s] input gradients: tests, MAF sweep, headline check.
+set -o pipefail
+mkdir -p gpurun_out
+cd "$GRAFT_REPO_ROOT" || exit 1
+timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+  tests/test_masked_gpu.py tests/test_maf_engine.py tests/test_fp8_gpu.py tests/test_gemm_gpu.py > gpurun_out/seg2_tests.log 2>&1 || { tail -40 gpurun_out/seg2_tests.log; exit 1; }
+tail -2 gpurun_out/seg2_tests.log
+rm -f gpurun_out/seg2.jsonl
+for args in "--precision fp8 --batch 32768" "--precision bf16 --batch 32768"; do
+  timeout -k 10 300 python -m vi_normflows_amd.bench.configs --config 5 $args --steps 10 --warmup 3 >> gpurun_out/seg2.jsonl 2> gpurun_out/seg2.err || { tail -20 gpurun_out/seg2.err; exit 1; }
+done
+cat gpurun_out/seg2.jsonl

@@ -52,3 +52,85 @@ def test_iaf_maf_gpu_kernel_path(gpu):
             y, l = f.inverse(x)
         assert torch.isfinite(y).all() and torch.isfinite(l).all()
         (y.sum() + l.sum()).backward()
+
+
+@pytest.mark.parametrize("order", ["natural", "reversed"])
+def test_masked_dgrad_two_k_ranges_256(gpu, order):
+    """[mu | s] MADE output mask: the 256x256 input-gradient kernel streams two K ranges per
+    tile (ops.masked.tile_ranges2) and equals the dense product of the masked weights."""
+    from vi_normflows_amd.ops.masked import MaskPlan
+
+    torch.manual_seed(6)
+    D, H, B = 512, 512, 512
+    o = torch.arange(D, 0, -1) if order == "reversed" else None
+    _, m2 = made_masks(*made_degrees(D, H, 1, o), 2)        # [2D, H]
+    m2 = m2.float().to(gpu)
+    plan = MaskPlan(m2)
+    assert plan.bwd256.shape[1] == 4                          # two ranges chosen
+    W = (torch.randn(2 * D, H, device=gpu) * 0.05 * m2).to(torch.bfloat16)
+    dy = torch.randn(B, 2 * D, device=gpu).to(torch.bfloat16)
+    h = torch.randn(B, H, device=gpu).to(torch.bfloat16)
+    ref = (dy.float() @ W.float()) * (h.float() > 0)
+    torch.ops.vinf.gemm_set_mode(2, 4)
+    try:
+        out = torch.empty(B, H, device=gpu, dtype=torch.bfloat16)
+        torch.ops.vinf.masked_gemm_nn(dy, W, h, out, plan.bwd, False, plan.bwd256)
+        acc = torch.full((B, H), 1.0, device=gpu)
+        torch.ops.vinf.masked_gemm_nn(dy, W, None, acc, plan.bwd, True, plan.bwd256)
+    finally:
+        torch.ops.vinf.gemm_set_mode(0, 4)
+    err = (out.float() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item(), err
+    ref2 = dy.float() @ W.float() + 1.0
+    assert (acc - ref2).abs().max().item() <= 1e-4 * ref2.abs().max().item()
+
+
+def _pair_env_subprocess(code: str):
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, VINF_GEMM_PAIR="2", VINF_GEMM_TILE="256")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "OK" in r.stdout, r.stdout
+
+
+def test_masked_paired_column_tiles_256(gpu):
+    """Paired column tiles per block (descending K-length rank p with ntn-1-p; forced on
+    through VINF_GEMM_PAIR=2, read once per process): masked fwd (bf16 and e4m3) and two-range
+    dgrad equal the dense products of the masked weights."""
+    _pair_env_subprocess('''
+import torch
+from vi_normflows_amd.flows.made import made_degrees, made_masks
+from vi_normflows_amd.ops._ext import native
+from vi_normflows_amd.ops.masked import MaskPlan
+from vi_normflows_amd.ops.fp8 import gemm_fp8, quantize_rows
+native()
+dev = "cuda"
+torch.manual_seed(3)
+D, H, B = 512, 1024, 768
+for o in (None, torch.arange(D, 0, -1)):
+    m1, m2 = made_masks(*made_degrees(D, H, 1, o), 2)
+    m1, m2 = m1.float().to(dev), m2.float().to(dev)
+    p1, p2 = MaskPlan(m1), MaskPlan(m2)
+    x = torch.randn(B, D, device=dev).to(torch.bfloat16)
+    W1 = (torch.randn(H, D, device=dev) * 0.05 * m1).to(torch.bfloat16)
+    y = torch.empty(B, H, device=dev, dtype=torch.bfloat16)
+    native().masked_gemm_nt(x, W1, None, y, 0, p1.fwd, p1.fwd256)
+    ref = x.float() @ W1.float().t()
+    assert (y.float() - ref).abs().max() <= 1e-2 * ref.abs().max()
+    xq, sx = quantize_rows(x.float())
+    wq, sw = quantize_rows(W1.float())
+    yq = gemm_fp8(xq, sx, wq, sw, None, False, krange=p1.fwd, krange256=p1.fwd256)
+    yd = gemm_fp8(xq, sx, wq, sw, None, False)
+    assert torch.equal(yq, yd)
+    W2 = (torch.randn(2 * D, H, device=dev) * 0.05 * m2).to(torch.bfloat16)
+    dy = torch.randn(B, 2 * D, device=dev).to(torch.bfloat16)
+    dx = torch.zeros(B, H, device=dev)
+    native().masked_gemm_nn(dy, W2, None, dx, p2.bwd, True, p2.bwd256)
+    ref = dy.float() @ W2.float()
+    assert (dx - ref).abs().max() <= 1e-4 * ref.abs().max()
+print("OK")
+''')

@@ -60,10 +60,21 @@ class DelayedScale:
     per-row absmax would couple every output to every input through the scale).
     """
 
-    def __init__(self, device):
-        self.amax = torch.zeros(2, device=device, dtype=torch.float32)
+    def __init__(self, device, amax: torch.Tensor | None = None):
+        # ``amax`` may be a [2] view into a pool shared by many states: an engine then rolls
+        # every state of a step in one launch (``external = True``) instead of two tiny
+        # kernels per quantised tensor
+        self.amax = amax if amax is not None else torch.zeros(2, device=device,
+                                                              dtype=torch.float32)
         self.scale = torch.ones(1, device=device, dtype=torch.float32)
         self.ready = False
+        self.external = False
+
+    def roll(self) -> None:
+        """amax_prev <- amax_cur, amax_cur <- 0 (skipped when the owner rolls the pool)."""
+        if not self.external:
+            self.amax[0].copy_(self.amax[1])
+            self.amax[1].zero_()
 
     def quantize(self, x: torch.Tensor, width: int | None = None, out: torch.Tensor | None = None):
         from ._ext import native
@@ -71,10 +82,12 @@ class DelayedScale:
         R, C = x.shape
         width = out.shape[1] if out is not None else (width or _pad128(C))
         if not self.ready:                       # bootstrap (device op, no host sync)
-            self.amax[1] = x.detach().abs().amax().float()
+            if self.external:
+                self.amax[0] = x.detach().abs().amax().float()
+            else:
+                self.amax[1] = x.detach().abs().amax().float()
             self.ready = True
-        self.amax[0].copy_(self.amax[1])
-        self.amax[1].zero_()
+        self.roll()
         q = out if out is not None else torch.empty(R, width, device=x.device,
                                                         dtype=torch.float8_e4m3fn)
         xc = x if x.stride(-1) == 1 else x.contiguous()
@@ -96,8 +109,7 @@ def gemm_fp8(xq, sx, wq, sw, bias=None, relu=False, krange=None, out=None, out_q
     b = bias.to(torch.bfloat16).contiguous() if bias is not None else None
     if out_q is not None:
         st = out_scale
-        st.amax[0].copy_(st.amax[1])
-        st.amax[1].zero_()
+        st.roll()
         native().gemm_fp8_nt(xq, sx, wq, sw, b, y, int(relu), krange, out_q, st.amax[0:1],
                              st.scale, st.amax[1:2], krange256)
         return y, st.scale

@@ -110,8 +110,7 @@ def maf_fwd(x, o, u, ldj, bound=5.0, ubf=None, uq=None, scale_state=None, ldj_in
     if _gpu(x):
         if uq is not None:
             st = scale_state
-            st.amax[0].copy_(st.amax[1])
-            st.amax[1].zero_()
+            st.roll()
             native().maf_fwd(x, o, float(bound), u, ubf, uq, st.amax[0:1], st.scale, st.amax[1:2],
                              ldj, bool(ldj_init))
         else:

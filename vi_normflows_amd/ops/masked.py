@@ -34,6 +34,35 @@ def tile_ranges(mask: torch.Tensor, tile_n: int = _TILE, align: int = 64):
     return torch.tensor(out, dtype=torch.int32)
 
 
+def tile_ranges2(mask: torch.Tensor, tile_n: int = 256, align: int = 64):
+    """Like :func:`tile_ranges` with up to TWO K ranges per output tile: the covering range
+    minus its largest interior run of all-zero ``align``-wide K blocks. Returns int32
+    (n_tiles, 4) [lo1, hi1, lo2, hi2] (an empty second range has lo2 == hi2)."""
+    nz = mask != 0
+    N, K = nz.shape
+    nb = (K + align - 1) // align
+    out = []
+    for t in range(0, N, tile_n):
+        colnz = nz[t:t + tile_n].any(0)
+        blk = [bool(colnz[b * align:(b + 1) * align].any()) for b in range(nb)]
+        idx = [b for b in range(nb) if blk[b]]
+        if not idx:
+            out.append((0, 0, 0, 0))
+            continue
+        first, last = idx[0], idx[-1]
+        best, gs, ge, run = 0, 0, 0, 0
+        for b in range(first, last + 1):
+            run = run + 1 if not blk[b] else 0
+            if run > best:
+                best, gs, ge = run, b - run + 1, b + 1
+        hi = min(K, (last + 1) * align)
+        if best == 0:
+            out.append((first * align, hi, 0, 0))
+        else:
+            out.append((first * align, gs * align, ge * align, hi))
+    return torch.tensor(out, dtype=torch.int32)
+
+
 def masked_fraction(mask: torch.Tensor, tile_n: int = _TILE, tile_k: int = 64) -> float:
     """Fraction of (tile_n x tile_k) tiles that are entirely zero (skippable work)."""
     N, K = mask.shape
@@ -72,7 +101,13 @@ class MaskPlan:
         # over 256x256 tiles; the first tile column is kept for the bias gradient), which the
         # multi-layer weight-gradient launch computes - the others are never launched
         self.fwd256 = tile_ranges(m, 256).to(dev).contiguous()
-        self.bwd256 = tile_ranges(m.t(), 256).to(dev).contiguous()
+        self.bwd256 = tile_ranges(m.t(), 256)
+        r2 = tile_ranges2(m.t(), 256)      # two ranges per tile pay off for [mu | s] outputs
+        cov1 = int((self.bwd256[:, 1] - self.bwd256[:, 0]).sum())
+        cov2 = int((r2[:, 1] - r2[:, 0] + r2[:, 3] - r2[:, 2]).sum())
+        if cov2 < 0.95 * cov1:
+            self.bwd256 = r2
+        self.bwd256 = self.bwd256.to(dev).contiguous()
         sk = skip_flags(m, 256)
         tn = (m.shape[1] + 255) // 256
         act = [t for t in range(sk.numel()) if not sk[t] or t % tn == 0]
