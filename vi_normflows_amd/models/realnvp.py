@@ -180,6 +180,11 @@ class RealNVPVI:
         # GEMM (gemm_tile.h EPI_CPL_BWD): dL/dh_{l+1} is finished there and consumed at once
         self.cpl_fuse = self.wgrad_defer and os.environ.get("VINF_CPL_FUSE", "1") != "0"
         self.dstL = self.dHL = None
+        # experiment (VINF_WGRAD_DEFER_STREAM=1): the deferred weight-gradient chunks on a side
+        # HIP stream, concurrent with the input-gradient chain
+        self.defer_stream = None
+        if self.wgrad_defer and os.environ.get("VINF_WGRAD_DEFER_STREAM", "0") == "1":
+            self.defer_stream = torch.cuda.Stream(device=dev)
         self._wplan = None
         if self.wgrad_defer:
             self.dstL = torch.empty(L, B, Np, dtype=self.cdt, device=dev)
@@ -356,6 +361,20 @@ class RealNVPVI:
         sched = gemm.WgradScheduler(plan, [(l + 1, plan.layer_end[l]) for l in range(L - 1, -1, -1)],
                                     self._wchunk, self.unit_ready_hook)
         fuse = self.cpl_fuse
+        side = self.defer_stream
+        main = torch.cuda.current_stream(self.device) if side is not None else None
+
+        def wgrad_ready(l):
+            if side is None:
+                sched.ready(plan.layer_end[l], final=(l == 0))
+                return
+            # the chunk runs beside the input-gradient chain: CUs in a GEMM's prologue /
+            # epilogue burst and CUs streaming a weight-gradient tile overlap
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                sched.ready(plan.layer_end[l], final=(l == 0))
 
         def cpl_bwd(l):
             fused.coupling_bwd(self.G[l + 2], self.ST[l][:, :cfg.half], self.h(l), self.dstL[l],
@@ -383,7 +402,9 @@ class RealNVPVI:
                                                gx=self.G[l - 1], scale=cfg.scale_bound, c=c)
                 else:
                     gemm.linear_dgrad(d, P.c(f"l{l}.W0"), self._G[l + 1], accumulate=True)
-            sched.ready(plan.layer_end[l], final=(l == 0))
+            wgrad_ready(l)
+        if side is not None:
+            main.wait_stream(side)
         self._base_backward()
         if self.unit_ready_hook is not None:
             self.unit_ready_hook(0)
