@@ -7,12 +7,20 @@
 #include <cstdlib>
 
 #include "launchers.h"
+#include "nf_common.h"
 
 namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 long ld2(const at::Tensor& t) { return t.size(0) <= 1 ? t.size(1) : t.stride(0); }
+
+// delayed-scale running amax: NF_AMAX_SLOTS contiguous fp32 partial maxima
+void chk_amax_slots(const at::Tensor& t) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() &&
+                  t.numel() >= NF_AMAX_SLOTS,
+              "amax_cur must hold ", NF_AMAX_SLOTS, " contiguous fp32 slots (ops.fp8.DelayedScale)");
+}
 
 void chk_mat(const at::Tensor& t, const char* n, at::ScalarType dt) {
   TORCH_CHECK(t.is_cuda(), n, " must be on the GPU");
@@ -309,6 +317,7 @@ void maf_fwd(const at::Tensor& x, const at::Tensor& o, double bound, const at::T
     ap = amax_prev->data_ptr<float>();
     sc = scale->data_ptr<float>();
     ac = amax_cur->data_ptr<float>();
+    chk_amax_slots(*amax_cur);
   }
   nf_launch_maf_fwd(x.data_ptr<float>(), ld2(x), o.data_ptr(), ld2(o), B, D, (float)bound,
                     u.data_ptr<float>(), ld2(u), ub, ldub, q, ldq, ap, sc, ac,
@@ -442,6 +451,7 @@ void fp8_quant_tensor(const at::Tensor& x, const at::Tensor& q, const at::Tensor
   TORCH_CHECK(q.size(0) == x.size(0) && q.size(1) >= x.size(1) && q.size(1) % 4 == 0, "q shape");
   for (const at::Tensor* t : {&amax_prev, &scale, &amax_cur})
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() >= 1, "scalars fp32");
+  chk_amax_slots(amax_cur);
   nf_launch_fp8_quant_tensor(x.data_ptr(), x.scalar_type() == at::kBFloat16, ld2(x), x.size(0),
                              x.size(1), q.data_ptr(), ld2(q), q.size(1), amax_prev.data_ptr<float>(),
                              scale.data_ptr<float>(), amax_cur.data_ptr<float>(), cur_stream());
@@ -488,6 +498,7 @@ void gemm_fp8_nt(const at::Tensor& xq, const at::Tensor& sx, const at::Tensor& w
     qap = q_amax_prev->data_ptr<float>();
     qs = q_scale->data_ptr<float>();
     qac = q_amax_cur->data_ptr<float>();
+    chk_amax_slots(*q_amax_cur);
   }
   // the 256x256 kernel when the caller supplies its K ranges (or the weight is dense) and the
   // product has a tile per CU (same rule as the bf16 products)

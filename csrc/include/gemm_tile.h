@@ -355,12 +355,10 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
         }
       }
     }
-    if (f8out) {  // one (mostly skipped) atomic per wave: amax >= 0, int order == float order
+    if (f8out) {  // one (mostly skipped) atomic per wave into the block's amax slot
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) qamax = fmaxf(qamax, __shfl_xor(qamax, off));
-      if (lane == 0 &&
-          qamax > __hip_atomic_load(a.f8_q_amax_cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMax(reinterpret_cast<int*>(a.f8_q_amax_cur), __float_as_int(qamax));
+      if (lane == 0) amax_slot_atomic(a.f8_q_amax_cur, qamax);
     }
   } else {
 #pragma unroll

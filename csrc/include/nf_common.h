@@ -123,3 +123,17 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& n0, fl
 }
 
 }  // namespace nf
+
+// Delayed fp8 scaling: the running amax of a tensor is folded into NF_AMAX_SLOTS partial maxima
+// (slot = blockIdx.x % NF_AMAX_SLOTS), so thousands of blocks do not serialise on one address;
+// the owner reduces the slots when it rolls the state (ops/fp8.py DelayedScale.roll).
+#define NF_AMAX_SLOTS 64
+namespace nf {
+// amax >= 0: integer max on the float bits orders like the floats; a plain read first skips
+// the atomic once the slot already holds a larger value
+__device__ __forceinline__ void amax_slot_atomic(float* slots, float v) {
+  float* dst = slots + (blockIdx.x % NF_AMAX_SLOTS);
+  if (v > __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMax(reinterpret_cast<int*>(dst), __float_as_int(v));
+}
+}  // namespace nf

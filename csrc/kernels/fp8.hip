@@ -71,8 +71,8 @@ __global__ void __launch_bounds__(256) quant_rows_kernel(const T* __restrict__ x
 // step's amax; 1 when none yet), q = e4m3(sat(x / scale)); the current amax is folded into
 // amax_cur with an integer atomicMax on the float bits (|x| >= 0 orders like its bits). A
 // constant scale keeps the map x -> q elementwise, so MADE's autoregressive structure is exact.
-// amax of a block's 4 waves -> one atomicMax per block (a per-wave atomic on one address
-// serialises: 8192 rows cost ~100 us; <= 256 blocks cost a few us)
+// amax of a block's 4 waves -> one atomicMax per block into one of NF_AMAX_SLOTS partial maxima
+// (a per-wave atomic on one address serialises: 8192 rows cost ~100 us)
 __device__ __forceinline__ void block_amax_atomic(float amax, float* dst) {
   __shared__ float red[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -80,10 +80,7 @@ __device__ __forceinline__ void block_amax_atomic(float amax, float* dst) {
   for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
   if (lane == 0) red[wave] = amax;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    atomicMax(reinterpret_cast<int*>(dst), __float_as_int(m));
-  }
+  if (threadIdx.x == 0) amax_slot_atomic(dst, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
 }
 
 template <typename T>

@@ -86,13 +86,8 @@ __global__ void __launch_bounds__(256) maf_fwd_kernel(const float* __restrict__ 
     for (int off = 32; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
     if (lane == 0) red[threadIdx.x >> 6] = amax;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      // amax >= 0, so int ordering == float ordering; a plain read first skips the atomic for
-      // most blocks once the running max has settled (the grid has up to 2048 blocks)
-      const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-      if (bm > __hip_atomic_load(amax_cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMax(reinterpret_cast<int*>(amax_cur), __float_as_int(bm));
-    }
+    if (threadIdx.x == 0)
+      amax_slot_atomic(amax_cur, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
   }
 }
 

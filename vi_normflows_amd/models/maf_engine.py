@@ -169,7 +169,9 @@ class MAFEngine:
             self.s1 = torch.empty(L * H, dtype=f32, device=dev)
             self.s2 = torch.empty(L * 2 * D, dtype=f32, device=dev)
             # every delayed-scale state of a step in one pool, rolled by one launch per step
-            self.amax_pool = torch.zeros(2 * L, 2, dtype=f32, device=dev)
+            from ..ops.fp8 import AMAX_SLOTS
+
+            self.amax_pool = torch.zeros(2 * L, 1 + AMAX_SLOTS, dtype=f32, device=dev)
             self.sx = [DelayedScale(dev, self.amax_pool[l]) for l in range(L)]      # input of l
             self.sh = [DelayedScale(dev, self.amax_pool[L + l]) for l in range(L)]  # hidden of l
             for st in self.sx + self.sh:
@@ -248,9 +250,9 @@ class MAFEngine:
 
             if not self._wq_fresh:
                 self.quantize_weights()
-            # amax_prev <- amax_cur, amax_cur <- 0 for every state at once
-            self.amax_pool[:, 0].copy_(self.amax_pool[:, 1])
-            self.amax_pool[:, 1].zero_()
+            # amax_prev <- max(amax_cur slots), slots <- 0 for every state at once
+            torch.amax(self.amax_pool[:, 1:], 1, out=self.amax_pool[:, 0])
+            self.amax_pool[:, 1:].zero_()
             _, sxs = self.sx[0].quantize(self.X[0], out=self.Xq)
         for l in range(L):
             mk = self._mask(l)

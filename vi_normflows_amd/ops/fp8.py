@@ -15,6 +15,7 @@ from __future__ import annotations
 import torch
 
 E4M3_MAX = 448.0
+AMAX_SLOTS = 64     # csrc/include/nf_common.h NF_AMAX_SLOTS
 
 
 def _pad128(n: int) -> int:
@@ -54,18 +55,21 @@ class DelayedScale:
     """Per-tensor activation scale from the previous call's amax (delayed scaling).
 
     Device state only (graph-capturable): ``amax[0]`` = amax of the previous input (the
-    scale basis), ``amax[1]`` = running amax of the current input (atomicMax in the quant
-    kernel). The first call bootstraps ``amax`` from the input itself. A constant scale within
+    scale basis), ``amax[1:]`` = running amax of the current input in AMAX_SLOTS partial
+    maxima (atomicMax in the producing kernel). The first call bootstraps ``amax`` from the input itself. A constant scale within
     a call keeps quantisation elementwise - MADE's autoregressive structure stays exact (a
     per-row absmax would couple every output to every input through the scale).
     """
 
     def __init__(self, device, amax: torch.Tensor | None = None):
-        # ``amax`` may be a [2] view into a pool shared by many states: an engine then rolls
-        # every state of a step in one launch (``external = True``) instead of two tiny
-        # kernels per quantised tensor
-        self.amax = amax if amax is not None else torch.zeros(2, device=device,
+        # amax[0] = the previous call's amax (scale basis); amax[1:] = AMAX_SLOTS partial maxima
+        # of the current call (producer blocks fold into slot blockIdx % AMAX_SLOTS, so they do
+        # not serialise on one address). ``amax`` may be a [1 + AMAX_SLOTS] row of a pool shared
+        # by many states: an engine then rolls every state of a step at once
+        # (``external = True``) instead of two tiny kernels per quantised tensor
+        self.amax = amax if amax is not None else torch.zeros(1 + AMAX_SLOTS, device=device,
                                                               dtype=torch.float32)
+        assert self.amax.numel() == 1 + AMAX_SLOTS
         self.scale = torch.ones(1, device=device, dtype=torch.float32)
         self.ready = False
         self.external = False
@@ -73,8 +77,13 @@ class DelayedScale:
     def roll(self) -> None:
         """amax_prev <- amax_cur, amax_cur <- 0 (skipped when the owner rolls the pool)."""
         if not self.external:
-            self.amax[0].copy_(self.amax[1])
-            self.amax[1].zero_()
+            torch.amax(self.amax[1:], 0, out=self.amax[0])
+            self.amax[1:].zero_()
+
+    @property
+    def cur(self) -> torch.Tensor:
+        """The running-amax slots of the current call."""
+        return self.amax[1:]
 
     def quantize(self, x: torch.Tensor, width: int | None = None, out: torch.Tensor | None = None):
         from ._ext import native
@@ -91,7 +100,7 @@ class DelayedScale:
         q = out if out is not None else torch.empty(R, width, device=x.device,
                                                         dtype=torch.float8_e4m3fn)
         xc = x if x.stride(-1) == 1 else x.contiguous()
-        native().fp8_quant_tensor(xc, q, self.amax[0:1], self.scale, self.amax[1:2])
+        native().fp8_quant_tensor(xc, q, self.amax[0:1], self.scale, self.cur)
         return q, self.scale
 
 
@@ -111,7 +120,7 @@ def gemm_fp8(xq, sx, wq, sw, bias=None, relu=False, krange=None, out=None, out_q
         st = out_scale
         st.roll()
         native().gemm_fp8_nt(xq, sx, wq, sw, b, y, int(relu), krange, out_q, st.amax[0:1],
-                             st.scale, st.amax[1:2], krange256)
+                             st.scale, st.cur, krange256)
         return y, st.scale
     native().gemm_fp8_nt(xq, sx, wq, sw, b, y, int(relu), krange, None, None, None, None,
                          krange256)

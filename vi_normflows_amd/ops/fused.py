@@ -111,7 +111,7 @@ def maf_fwd(x, o, u, ldj, bound=5.0, ubf=None, uq=None, scale_state=None, ldj_in
         if uq is not None:
             st = scale_state
             st.roll()
-            native().maf_fwd(x, o, float(bound), u, ubf, uq, st.amax[0:1], st.scale, st.amax[1:2],
+            native().maf_fwd(x, o, float(bound), u, ubf, uq, st.amax[0:1], st.scale, st.cur,
                              ldj, bool(ldj_init))
         else:
             native().maf_fwd(x, o, float(bound), u, ubf, None, None, None, None, ldj, bool(ldj_init))
