@@ -244,6 +244,50 @@ void gemm_tn_multi(at::TensorList dy, at::TensorList x, at::TensorList dW,
   nf_launch_gemm256_tn_multi((int)n, pr.data(), (int)tile0, (int)ntiles, cur_stream());
 }
 
+// Last conditioner product of coupling layer l with the layer's coupling forward in the epilogue:
+// st[:, :Dh] = s_hat (bf16), y = x e^s + t, yb = bf16(y) (0-padded), ldjp[tn] (+)= partial sum s.
+void gemm_nt_cpl(const at::Tensor& h, const at::Tensor& W, const c10::optional<at::Tensor>& b,
+                 const at::Tensor& st, const at::Tensor& x, const at::Tensor& y,
+                 const c10::optional<at::Tensor>& yb, const at::Tensor& ldjp, bool ldj_init,
+                 double scale) {
+  chk_mat(h, "h", at::kBFloat16);
+  chk_mat(W, "W", at::kBFloat16);
+  chk_mat(st, "st", at::kBFloat16);
+  const int M = h.size(0), K = h.size(1), Dh = x.size(1);
+  TORCH_CHECK(W.size(1) == K && W.size(0) >= 2 * Dh, "W: [>= 2 Dh, K]");
+  TORCH_CHECK(K % 32 == 0 && Dh % 8 == 0, "K % 32 and Dh % 8 required");
+  TORCH_CHECK(st.size(0) == M && st.size(1) >= Dh, "st shape");
+  for (const at::Tensor* t : {&x, &y})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->dim() == 2 &&
+                    t->stride(1) == 1 && t->size(0) == M && t->size(1) == Dh &&
+                    ld2(*t) % 4 == 0 && reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                "x, y: fp32 [M, Dh], 16-B aligned rows");
+  const int ntn = (Dh + 127) / 128;
+  TORCH_CHECK(ldjp.is_cuda() && ldjp.scalar_type() == at::kFloat && ldjp.dim() == 2 &&
+                  ldjp.size(0) >= ntn && ldjp.size(1) == M && ldjp.stride(1) == 1,
+              "ldjp: fp32 [ceil(Dh/128), M]");
+  const void* bp = nullptr;
+  if (b && b->defined()) {
+    TORCH_CHECK(b->scalar_type() == at::kBFloat16 && b->numel() == W.size(0) && b->is_contiguous(),
+                "bias");
+    bp = b->data_ptr();
+  }
+  void* ybp = nullptr;
+  long ldyb = 0;
+  int ybw = 0;
+  if (yb && yb->defined()) {
+    chk_mat(*yb, "yb", at::kBFloat16);
+    TORCH_CHECK(yb->size(0) == M && yb->size(1) >= Dh && yb->size(1) % 8 == 0, "yb shape");
+    ybp = yb->data_ptr();
+    ldyb = ld2(*yb);
+    ybw = (int)yb->size(1);
+  }
+  nf_launch_gemm256_nt_cpl(h.data_ptr(), ld2(h), W.data_ptr(), ld2(W), (int)W.size(0), bp,
+                           st.data_ptr(), ld2(st), M, K, Dh, x.data_ptr<float>(), ld2(x),
+                           y.data_ptr<float>(), ld2(y), ybp, ldyb, ybw, ldjp.data_ptr<float>(),
+                           ldjp.stride(0), ldj_init, (float)scale, cur_stream());
+}
+
 // Conditioner input gradient of coupling layer l (gy = G + dy W, fp32, not stored) fused with the
 // backward of coupling layer l-1: dst = [dS_hat | dT | 0] (bf16), gx = gy e^s (fp32).
 void gemm_nn_cpl(const at::Tensor& dy, const at::Tensor& W, const at::Tensor& G,
@@ -538,6 +582,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db) -> ()");
   m.def("gemm_tn_group(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, Tensor?[] skip, Tensor?[] cmask) -> ()");
   m.def("gemm_tn_multi(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles, Tensor?[] tiles, Tensor?[] cmask) -> ()");
+  m.def("gemm_nt_cpl(Tensor h, Tensor W, Tensor? b, Tensor(a!) st, Tensor x, Tensor(b!) y, Tensor(c!)? yb, Tensor(d!) ldjp, bool ldj_init, float scale) -> ()");
   m.def("gemm_nn_cpl(Tensor dy, Tensor W, Tensor G, Tensor s_hat, Tensor x, Tensor(a!) dst, Tensor(b!) gx, float scale, float c) -> ()");
   m.def("fp8_quant_rows_strided(Tensor x, int layer_stride, int rows_per, int layers, int C, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("maf_fwd(Tensor x, Tensor o, float bound, Tensor(a!) u, Tensor(b!)? ubf, Tensor(c!)? uq, Tensor? amax_prev, Tensor(d!)? scale, Tensor(e!)? amax_cur, Tensor(f!) ldj, bool ldj_init) -> ()");
@@ -554,6 +599,7 @@ TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
   m.impl("gemm_tn_group", &gemm_tn_group);
   m.impl("gemm_tn_multi", &gemm_tn_multi);
   m.impl("gemm_nn_cpl", &gemm_nn_cpl);
+  m.impl("gemm_nt_cpl", &gemm_nt_cpl);
   m.impl("fp8_quant_rows", &fp8_quant_rows);
   m.impl("fp8_quant_rows_strided", &fp8_quant_rows_strided);
   m.impl("maf_fwd", &maf_fwd);

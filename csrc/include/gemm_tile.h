@@ -28,6 +28,8 @@ enum Epi : int {
   EPI_F32_ACC = 3,       // C(fp32) += acc
   EPI_CPL_BWD = 4,       // gy = C(fp32) + acc, then the affine-coupling backward of the previous
                          // flow layer (staged path only; see GemmArgs::cpl_*)
+  EPI_CPL_FWD = 5,       // [s_hat | t] = acc + bias, then the affine-coupling forward of the same
+                         // layer (gemm256 only; see GemmArgs::cf_*)
 };
 
 struct GemmArgs {
@@ -78,6 +80,24 @@ struct GemmArgs {
   const float* f8_q_amax_prev;
   float* f8_q_scale_out;
   float* f8_q_amax_cur;
+  // EPI_CPL_FWD: the conditioner's last product with the coupling forward fused. Column tile tn
+  // holds features j in [128 tn, 128 tn + 128): tile columns 0..127 read weight rows j (s_hat),
+  // columns 128..255 rows cf_dh + j (t), so each block sees both halves of its features. The
+  // epilogue writes y = x e^s + t (fp32, cf_y), its bf16 copy (cf_yb, zero pad to cf_yb_width),
+  // s_hat (bf16, C at column j - what the backward recomputes s from) and this block's share of
+  // sum_j s into cf_ldj[tn][m] (one owner per entry: deterministic, no atomics).
+  const float* cf_x;
+  long ld_cf_x;
+  float* cf_y;
+  long ld_cf_y;
+  bf16_t* cf_yb;
+  long ld_cf_yb;
+  int cf_yb_width;
+  float* cf_ldj;
+  long ld_cf_ldj;
+  int cf_ldj_init;
+  int cf_dh, cf_b_rows;
+  float cf_scale;
 };
 
 // LDS-staged epilogue switch (VINF_GEMM_STAGED_EPI=0 restores the fragment-layout stores) and

@@ -89,6 +89,12 @@ void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, co
                           int N, int K, hipStream_t stream, int aux_is_bits = 0,
                           const int* krange = nullptr, int krange_segs = 1);
 void nf_gemm256_set_depth(int d);
+// last conditioner product of coupling layer l with its coupling forward fused (EPI_CPL_FWD)
+void nf_launch_gemm256_nt_cpl(const void* h, long ldh, const void* W, long ldw, int w_rows,
+                              const void* bias, void* st, long ld_st, int M, int K, int Dh,
+                              const float* x, long ld_x, float* y, long ld_y, void* yb, long ld_yb,
+                              int yb_width, float* ldjp, long ld_ldjp, int ldj_init, float scale,
+                              hipStream_t stream);
 // input gradient of coupling layer l's conditioner (fp32, + G) fused with coupling layer l-1's
 // backward: writes dst (bf16 [dS_hat | dT | 0]) and gx; G itself is not written
 void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw, const float* G,

@@ -75,10 +75,12 @@ __device__ __forceinline__ v8i cat16(v8s lo, v8s hi) {
 
 // EB: bytes per element (2 = bf16, 1 = e4m3); ld, k0, K in elements. A half-tile is 128 rows x
 // 128 bytes either way (64 bf16 or 128 e4m3 k-values per row).
+// pair_dh > 0 (EPI_CPL_FWD, B operand): tile row c < 128 -> weight row row0/2 + c, c >= 128 ->
+// pair_dh + row0/2 + c - 128 (the s_hat and t rows of the same 128 features)
 template <bool KMAJOR, int EB = 2>
 __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long ld, int row0,
                                            int rows_total, int k0, int K, bool is_a, bool hi,
-                                           char* dst, int wave, int lane) {
+                                           char* dst, int wave, int lane, int pair_dh = 0) {
   constexpr int CE = 16 / EB;  // elements per 16-B chunk
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -87,7 +89,9 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long
     if (KMAJOR) {
       const int r = piece * 8 + (lane >> 3);
       const int lc = (lane & 7) ^ (r & 7);
-      int gr = row0 + half_row(is_a, hi, r);
+      const int tc = half_row(is_a, hi, r);
+      int gr = pair_dh == 0 ? row0 + tc
+                            : (tc < 128 ? (row0 >> 1) + tc : pair_dh + (row0 >> 1) + tc - 128);
       gr = gr < rows_total ? gr : rows_total - 1;
       int gk = k0 + lc * CE;
       gk = gk < K ? gk : K - CE;
@@ -129,6 +133,117 @@ __device__ __forceinline__ void vmwait_count(int cnt) {
   else if (cnt == 2) vmwait<4>();
   else if (cnt == 1) vmwait<2>();
   else vmwait<0>();
+}
+
+// EPI_CPL_FWD epilogue (GemmArgs::cf_*). 1) every wave parks bf16(acc + bias) of its 128 x 64
+// sub-tile in its own 16 KiB LDS region (the staged-epilogue image); 2) after a block barrier
+// the 512 threads walk the 256 rows x 128 features, thread = (row of 32, 16-B chunk of 8
+// features), reading s_hat from the region of wave (wr, c/64) and t from wave (wr, 2 + c/64).
+__device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&acc)[4][8],
+                                                 int m0, int n0, int wr, int wc, char* smem,
+                                                 int lane) {
+  const int g = lane >> 4, c = lane & 15;
+  const int j0 = n0 >> 1, tn = n0 / BN;
+  char* region = smem + (wr * 4 + wc) * 16384;
+  // readback mapping, and its x rows / previous log-det partials fetched up front: the 8 rows'
+  // loads are all in flight while the accumulators are parked (the epilogue runs on every CU at
+  // once, so a load round trip per row pair would sit exposed after the main loop)
+  const int tid = threadIdx.x, f8 = tid & 15, rsub = tid >> 4;
+  const int ws = f8 >> 3, q = f8 & 7;
+  const int jf = j0 + f8 * 8;                                    // first of this thread's 8 features
+  const bool fok = jf < a.cf_dh;
+  float4 xv[8][2];
+  float lold[8];
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int m = m0 + it * 32 + rsub;
+    xv[it][0] = xv[it][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    lold[it] = 0.f;
+    if (m < a.M && fok) {
+      const float* xr = a.cf_x + (long)m * a.ld_cf_x + jf;
+      xv[it][0] = *reinterpret_cast<const float4*>(xr);
+      xv[it][1] = *reinterpret_cast<const float4*>(xr + 4);
+    }
+    if (!a.cf_ldj_init && f8 == 0 && m < a.M) lold[it] = a.cf_ldj[(long)tn * a.ld_cf_ldj + m];
+  }
+  float bv[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int tc = wc * 64 + i * 16 + g * 4;                     // tile column (4 consecutive)
+    const int f = j0 + (tc & 127);                               // feature
+    const int row = tc < 128 ? f : a.cf_dh + f;                  // weight / bias row
+    if (a.bias && f < a.cf_dh) {
+      const ushort4 bb = *reinterpret_cast<const ushort4*>(a.bias + row);
+      bv[i][0] = bf2f(bb.x); bv[i][1] = bf2f(bb.y); bv[i][2] = bf2f(bb.z); bv[i][3] = bf2f(bb.w);
+    } else {
+      bv[i][0] = bv[i][1] = bv[i][2] = bv[i][3] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int row = j * 16 + c;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const unsigned lo = (unsigned)f2bf(acc[i][j][0] + bv[i][0]) |
+                          ((unsigned)f2bf(acc[i][j][1] + bv[i][1]) << 16);
+      const unsigned hi = (unsigned)f2bf(acc[i][j][2] + bv[i][2]) |
+                          ((unsigned)f2bf(acc[i][j][3] + bv[i][3]) << 16);
+      const int slot = i * 4 + g;
+      *(LDS_AS v2u*)(region + row * 128 + (((slot >> 1) ^ (row & 7)) << 4) + (slot & 1) * 8) =
+          (v2u){lo, hi};
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  barrier();
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int lrow = it * 32 + rsub, m = m0 + lrow;
+    const int wrr = lrow >> 7, r = lrow & 127;
+    float part = 0.f;
+    if (m < a.M) {
+      if (fok) {
+        const int off = r * 128 + ((q ^ (r & 7)) << 4);
+        const v4u sh = *(const LDS_AS v4u*)(smem + (wrr * 4 + ws) * 16384 + off);
+        const v4u tt = *(const LDS_AS v4u*)(smem + (wrr * 4 + 2 + ws) * 16384 + off);
+        const float4 x0 = xv[it][0], x1 = xv[it][1];
+        const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        float y[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const unsigned us = sh[e >> 1], ut = tt[e >> 1];
+          const float shv = __uint_as_float((e & 1) ? (us & 0xffff0000u) : (us << 16));
+          const float tv = __uint_as_float((e & 1) ? (ut & 0xffff0000u) : (ut << 16));
+          const float sv = a.cf_scale * tanhf(shv);
+          y[e] = fmaf(xs[e], __expf(sv), tv);
+          part += sv;
+        }
+        float* yr = a.cf_y + (long)m * a.ld_cf_y + jf;
+        *reinterpret_cast<float4*>(yr) = make_float4(y[0], y[1], y[2], y[3]);
+        *reinterpret_cast<float4*>(yr + 4) = make_float4(y[4], y[5], y[6], y[7]);
+        if (a.cf_yb) {
+          uint4 o;
+          o.x = (unsigned)f2bf(y[0]) | ((unsigned)f2bf(y[1]) << 16);
+          o.y = (unsigned)f2bf(y[2]) | ((unsigned)f2bf(y[3]) << 16);
+          o.z = (unsigned)f2bf(y[4]) | ((unsigned)f2bf(y[5]) << 16);
+          o.w = (unsigned)f2bf(y[6]) | ((unsigned)f2bf(y[7]) << 16);
+          *reinterpret_cast<uint4*>(a.cf_yb + (long)m * a.ld_cf_yb + jf) = o;
+        }
+        *reinterpret_cast<uint4*>((bf16_t*)a.C + (long)m * a.ldc + jf) =
+            make_uint4(sh[0], sh[1], sh[2], sh[3]);
+      } else if (a.cf_yb && jf < a.cf_yb_width) {   // zero the next operand's pad columns
+        *reinterpret_cast<uint4*>(a.cf_yb + (long)m * a.ld_cf_yb + jf) = make_uint4(0, 0, 0, 0);
+      }
+    }
+    // sum of s over this block's 128 features: the 16 threads of a row are 16 adjacent lanes
+    part += __shfl_xor(part, 8);
+    part += __shfl_xor(part, 4);
+    part += __shfl_xor(part, 2);
+    part += __shfl_xor(part, 1);
+    if (f8 == 0 && m < a.M) {
+      float* lp = a.cf_ldj + (long)tn * a.ld_cf_ldj + m;
+      *lp = part + lold[it];
+    }
+  }
 }
 
 // F8: e4m3 operands (both k-major), one v_mfma_scale_f32_16x16x128_f8f6f4 per (i, j) and K-tile
@@ -210,6 +325,9 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
     const int ke = s2 ? kend2 : kend;
     if (j == H_ALO || j == H_AHI)
       stage_half<A_KMAJOR, EB>(a.A, a.lda, m0, a.M, k0, ke, true, j == H_AHI, dst, wave, lane);
+    else if constexpr (EPI == EPI_CPL_FWD)
+      stage_half<B_KMAJOR, EB>(a.B, a.ldb, n0, a.cf_b_rows, k0, ke, false, j == H_BHI, dst, wave,
+                               lane, a.cf_dh);
     else
       stage_half<B_KMAJOR, EB>(a.B, a.ldb, n0, a.N, k0, ke, false, j == H_BHI, dst, wave, lane);
   };
@@ -303,6 +421,11 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
       const int m = m0 + wr * 128 + h * 64 + wc * 16 + c;
       if (m < a.M) a.dbias[(long)split * a.M + m] = accb[h][0];
     }
+  }
+  if constexpr (EPI == EPI_CPL_FWD) {
+    barrier();  // every wave is past its last operand read
+    epi_coupling_fwd(a, acc, m0, n0, wr, wc, smem, lane);
+    return;
   }
   if (a.staged) {
     barrier();  // every wave is past its last operand read; each wave reuses 16 KiB of LDS
@@ -427,7 +550,7 @@ int device_cus_256() {
   static const int n = [] {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     return cus;
   }();
   return n;
@@ -504,6 +627,38 @@ void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, co
   } else {
     g256::launch<true, false, EPI_BF16>(a, 1, stream);
   }
+}
+
+// Last conditioner product of coupling layer l with its coupling forward fused (EPI_CPL_FWD):
+// W [2 Dh (+pad) rows][K], x/y fp32 [M][Dh], yb bf16 [M][>= yb_width] (or null), st bf16 [M][>= Dh]
+// (s_hat written), ldjp fp32 [ceil(Dh/128)][M] per-column-tile partial sums of s.
+void nf_launch_gemm256_nt_cpl(const void* h, long ldh, const void* W, long ldw, int w_rows,
+                              const void* bias, void* st, long ld_st, int M, int K, int Dh,
+                              const float* x, long ld_x, float* y, long ld_y, void* yb, long ld_yb,
+                              int yb_width, float* ldjp, long ld_ldjp, int ldj_init, float scale,
+                              hipStream_t stream) {
+  if (M <= 0) return;
+  GemmArgs a{};
+  a.A = (const nf::bf16_t*)h; a.lda = ldh;
+  a.B = (const nf::bf16_t*)W; a.ldb = ldw;
+  a.C = st; a.ldc = ld_st;
+  a.bias = (const nf::bf16_t*)bias;
+  const int ntn = (Dh + 127) / 128;
+  a.M = M; a.N = ntn * 256; a.K = K; a.k_per_split = ((K + 63) / 64) * 64;
+  a.cf_x = x; a.ld_cf_x = ld_x;
+  a.cf_y = y; a.ld_cf_y = ld_y;
+  a.cf_yb = (nf::bf16_t*)yb; a.ld_cf_yb = ld_yb; a.cf_yb_width = yb_width;
+  a.cf_ldj = ldjp; a.ld_cf_ldj = ld_ldjp; a.cf_ldj_init = ldj_init;
+  a.cf_dh = Dh; a.cf_b_rows = w_rows; a.cf_scale = scale;
+  auto al16 = [](const void* p) { return ((unsigned long)p & 15) == 0; };
+  if (Dh % 8 || w_rows < 2 * Dh || ld_x % 4 || ld_y % 4 || ld_st % 8 ||
+      (yb && (ld_yb % 8 || !al16(yb) || yb_width < Dh || yb_width % 8)) || !al16(x) || !al16(y) ||
+      !al16(st)) {
+    fprintf(stderr, "vinf: fused coupling-forward GEMM needs Dh %% 8 == 0, 16-B aligned rows and "
+                    "2 Dh weight rows\n");
+    abort();
+  }
+  g256::launch<true, true, EPI_CPL_FWD>(a, 1, stream);
 }
 
 // Conditioner input gradient of coupling layer l fused with the backward of coupling layer l-1

@@ -194,3 +194,63 @@ def test_gemm_nn_cpl_matches_torch(gpu):
     for o, r in zip(out, ref):
         err = (o.float() - r.float()).abs().max().item()
         assert err <= 2e-2 * r.float().abs().max().item(), err
+
+
+@pytest.mark.gpu
+def test_fused_coupling_forward_epilogue_matches_unfused(gpu, monkeypatch):
+    """The coupling forward inside the last conditioner GEMM's epilogue (EPI_CPL_FWD: each
+    column tile holds the s_hat and t columns of the same 128 features) gives bitwise the
+    states, bf16 operands and s_hat of the separate coupling kernel; the log-det only differs
+    in summation order (per-tile partials)."""
+    cfg = RealNVPConfig(dim=784, n_layers=4, hidden=512, anneal="none", init_out_std=0.1)
+    a = RealNVPVI(cfg, batch=768, device=gpu, seed=5)
+    monkeypatch.setenv("VINF_CPL_FWD_FUSE", "0")
+    b = RealNVPVI(cfg, batch=768, device=gpu, seed=5)
+    assert a.cf_fuse and not b.cf_fuse
+    for e in (a, b):
+        e._update_schedule()
+        e.forward()
+        e.backward()
+    torch.cuda.synchronize()
+    Dh = cfg.half
+    assert torch.equal(a.Hs, b.Hs)
+    assert torch.equal(a.Hbf, b.Hbf)
+    assert torch.equal(a.ST[:, :, :Dh], b.ST[:, :, :Dh])
+    assert torch.allclose(a.ldj, b.ldj, rtol=1e-5, atol=1e-3)
+    assert abs(a.loss.item() - b.loss.item()) <= 1e-5 * abs(b.loss.item()) + 1e-4
+    ga, gb = a.params.grad, b.params.grad
+    assert torch.isfinite(ga).all()
+    assert ((ga - gb).norm() / gb.norm()).item() < 1e-4
+
+
+@pytest.mark.gpu
+def test_gemm_nt_cpl_matches_torch(gpu):
+    """The fused GEMM + coupling-forward op vs its torch composite, with odd row counts."""
+    from vi_normflows_amd.ops import gemm
+
+    torch.manual_seed(7)
+    M, K, Dh = 700, 512, 392
+    h = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = torch.zeros(800, K, device=gpu)
+    W[:2 * Dh] = torch.randn(2 * Dh, K, device=gpu) * 0.03
+    W = W.to(torch.bfloat16)
+    b = (torch.randn(800, device=gpu) * 0.1).to(torch.bfloat16)
+    x = torch.randn(M, Dh, device=gpu)
+    outs = []
+    for backend in ("mfma", "blas"):
+        gemm.set_backend(backend)
+        try:
+            st = torch.zeros(M, 800, device=gpu, dtype=torch.bfloat16)
+            y = torch.empty(M, Dh, device=gpu)
+            yb = torch.full((M, 416), 3.0, device=gpu).to(torch.bfloat16)
+            ldjp = torch.full((4, M), 9.0, device=gpu)
+            gemm.linear_fwd_coupling(h, W, b, st, x, y, yb, ldjp, True, 1.0)
+            outs.append((st[:, :Dh].float(), y, yb.float(), ldjp.sum(0)))
+        finally:
+            gemm.set_backend("mfma")
+    torch.cuda.synchronize()
+    (s1, y1, b1, l1), (s2, y2, b2, l2) = outs
+    assert (b1[:, Dh:] == 0).all()
+    for u, v in ((s1, s2), (y1, y2), (b1, b2), (l1, l2)):
+        err = (u - v).abs().max().item()
+        assert err <= 2e-2 * v.abs().max().item() + 1e-3, err

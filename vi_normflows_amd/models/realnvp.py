@@ -180,6 +180,16 @@ class RealNVPVI:
         # GEMM (gemm_tile.h EPI_CPL_BWD): dL/dh_{l+1} is finished there and consumed at once
         self.cpl_fuse = self.wgrad_defer and os.environ.get("VINF_CPL_FUSE", "1") != "0"
         self.dstL = self.dHL = None
+        # fuse each layer's coupling forward into its last conditioner GEMM (gemm256
+        # EPI_CPL_FWD): s_hat / t never make an HBM round trip and t is never stored; the
+        # per-column-tile log-det partials land in ldjp and are summed once before the target
+        kc = H if cfg.n_hidden else Dp
+        self.cf_fuse = (dev.type == "cuda" and self.cdt == torch.bfloat16
+                        and Dh % 8 == 0 and kc % 32 == 0
+                        and os.environ.get("VINF_CPL_FWD_FUSE", "1") != "0")
+        self.ldjp = None
+        if self.cf_fuse:
+            self.ldjp = torch.empty((Dh + 127) // 128, B, dtype=f32, device=dev)
         # experiment (VINF_WGRAD_DEFER_STREAM=1): the deferred weight-gradient chunks on a side
         # HIP stream, concurrent with the input-gradient chain
         self.defer_stream = None
@@ -280,15 +290,21 @@ class RealNVPVI:
             self.beta.fill_(1.0)
 
     # ------------------------------------------------------------------ forward
-    def _conditioner_fwd(self, l: int, inp: torch.Tensor) -> torch.Tensor:
+    def _conditioner_hidden(self, l: int, inp: torch.Tensor) -> torch.Tensor:
+        """The ReLU hidden layers of layer l's conditioner; returns the last one's output."""
         P = self.params
         a = inp
-        nh = self.cfg.n_hidden
-        for i in range(nh):
+        for i in range(self.cfg.n_hidden):
             out = self.Act[l, i]
             gemm.linear_fwd(a, P.c(f"l{l}.W{i}"), P.c(f"l{l}.b{i}"), out, relu=True,
                             mask_out=None if self.Mk is None else self.Mk[l, i])
             a = out
+        return a
+
+    def _conditioner_fwd(self, l: int, inp: torch.Tensor) -> torch.Tensor:
+        P = self.params
+        nh = self.cfg.n_hidden
+        a = self._conditioner_hidden(l, inp)
         st = self.ST[l]
         gemm.linear_fwd(a, P.c(f"l{l}.W{nh}"), P.c(f"l{l}.b{nh}"), st, relu=False)
         return st
@@ -302,12 +318,22 @@ class RealNVPVI:
                                  eps=self.eps0, zbf=self.Hbf[0], nbf=Dh, logq0=self.logq0)
         else:
             self._base_from_eps(self.eps_override)
+        fuse = self.cf_fuse and gemm.backend() == "mfma"
+        nh = cfg.n_hidden
         for l in range(L):
-            st = self._conditioner_fwd(l, self.Hbf[l])
             ybf = self.Hbf[l + 1] if l + 1 < L else None
+            if fuse:
+                a = self._conditioner_hidden(l, self.Hbf[l])
+                gemm.linear_fwd_coupling(a, P.c(f"l{l}.W{nh}"), P.c(f"l{l}.b{nh}"), self.ST[l],
+                                         self.h(l), self.h(l + 2), ybf, self.ldjp,
+                                         ldj_init=(l == 0), scale=cfg.scale_bound)
+                continue
+            st = self._conditioner_fwd(l, self.Hbf[l])
             fused.coupling_fwd(st, self.h(l), self.h(l + 2), ybf=ybf, ssav=None,
                                ldj=self.ldj, scale=cfg.scale_bound, inverse=False,
                                ldj_init=(l == 0))
+        if fuse:
+            torch.sum(self.ldjp, 0, out=self.ldj)
         A, Bh, ia, ib = self.zK_halves()
         ta = self._target_args()
         fused.target_logp_grad(ta["kind"], A, Bh, gA=self.G[ia], gB=self.G[ib],

@@ -86,6 +86,45 @@ def linear_dgrad(dy: torch.Tensor, W: torch.Tensor, out: torch.Tensor,
     return out
 
 
+def linear_fwd_coupling(h: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None,
+                        st: torch.Tensor, x: torch.Tensor, y: torch.Tensor,
+                        ybf: torch.Tensor | None, ldjp: torch.Tensor, ldj_init: bool,
+                        scale: float) -> None:
+    """Last conditioner product of an affine coupling layer fused with the coupling forward
+    (MFMA path: one GEMM, ``EPI_CPL_FWD`` - each column tile computes the s_hat AND t columns of
+    the same 128 features, so the epilogue can apply the coupling):
+
+        [s_hat | t] = h W^T + b;   s = scale tanh(s_hat);   y = x e^s + t
+        st[:, :Dh] = s_hat (bf16),  ybf = bf16(y) (zero pad),  ldjp[tn] (+)= sum of s over tile tn
+
+    ``ldjp`` [ceil(Dh/128), B]: per-column-tile partial log-dets (the caller sums them; no
+    atomics, bitwise reproducible). Elsewhere: torch, with the whole sum in ``ldjp[0]``."""
+    Dh = x.shape[1]
+    if _mfma_ok(h) and h.is_cuda:
+        from ._ext import native
+
+        native().gemm_nt_cpl(h, W, b, st, x, y, ybf, ldjp, bool(ldj_init), float(scale))
+        return
+    o = h.float() @ W.float().t()
+    if b is not None:
+        o = o + b.float()
+    o = o.to(st.dtype).float()
+    sh, t = o[:, :Dh], o[:, Dh:2 * Dh]
+    s = scale * torch.tanh(sh)
+    yv = x * torch.exp(s) + t
+    st[:, :Dh].copy_(sh)
+    y.copy_(yv)
+    if ybf is not None:
+        ybf[:, :Dh].copy_(yv)
+        ybf[:, Dh:].zero_()
+    part = s.sum(1)
+    if ldj_init:
+        ldjp.zero_()
+        ldjp[0].copy_(part)
+    else:
+        ldjp[0].add_(part)
+
+
 def linear_dgrad_coupling(dy: torch.Tensor, W: torch.Tensor, G: torch.Tensor, s_hat: torch.Tensor,
                           x: torch.Tensor, dst: torch.Tensor, gx: torch.Tensor, scale: float,
                           c: float) -> None:
