@@ -35,8 +35,14 @@ namespace g256 {
 
 constexpr int BM = 256, BN = 256, BK = 64, NTHR = 512;
 constexpr int HALF_BYTES = 128 * 64 * 2;  // 16 KiB
-constexpr int BUF_BYTES = 4 * HALF_BYTES;  // A-lo, B-lo, B-hi, A-hi
-constexpr int SMEM_BYTES = 2 * BUF_BYTES;  // 128 KiB
+// LDS ring of half-tiles: half j of K-tile t (h = 4t + j, j = issue order A-lo, B-lo, B-hi,
+// A-hi) lives in slot h % NSLOT. Depth D = 4: NSLOT = 8 (two K-tile buffers, 128 KiB), half h
+// issued at phase h - 5. Depth D = 4 + X: NSLOT = 8 + X and half h issued X phases earlier
+// (h - 5 - X), every RAW / WAR distance unchanged; X = 2 fills the 160 KiB LDS and keeps 7-8
+// half-tiles (~120 KiB) in flight instead of 4-5, for the long-K products whose operands miss
+// L2 (a quarter of the weight-gradient fetches) and wait out HBM latency.
+constexpr int ring_extra(int D) { return D > 4 ? D - 4 : 0; }
+constexpr int smem_bytes(int D) { return (8 + ring_extra(D)) * HALF_BYTES; }
 // slot order inside a buffer == issue order j
 constexpr int H_ALO = 0, H_BLO = 1, H_BHI = 2, H_AHI = 3;
 
@@ -123,12 +129,17 @@ __device__ __forceinline__ void vmwait() {
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
 }
 
 // retire every half issued at phase <= P - D; `cnt` = valid halves issued in (P - D, P]
 template <int D>
 __device__ __forceinline__ void vmwait_count(int cnt) {
+  static_assert(D <= 6, "vmwait table");
   if (cnt >= D) vmwait<2 * D>();
+  else if (cnt == 5) vmwait<10>();
+  else if (cnt == 4) vmwait<8>();
   else if (cnt == 3) vmwait<6>();
   else if (cnt == 2) vmwait<4>();
   else if (cnt == 1) vmwait<2>();
@@ -254,6 +265,7 @@ template <bool A_KMAJOR, bool B_KMAJOR, int EPI, int D, bool DB, bool F8 = false
 __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int split, char* smem) {
   constexpr int BKE = F8 ? 2 * BK : BK;  // K-tile in elements
   constexpr int EB = F8 ? 1 : 2;
+  constexpr int X = ring_extra(D), NSLOT = 8 + X;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -316,10 +328,11 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
     }
   };
 
+  auto slot = [&](int t, int j) { return smem + ((4 * t + j) % NSLOT) * HALF_BYTES; };
   // issue half j of K-tile t (no-op past the end)
   auto issue = [&](int t, int j) {
     if (t >= nkt) return;
-    char* dst = smem + (t & 1) * BUF_BYTES + j * HALF_BYTES;
+    char* dst = slot(t, j);
     const bool s2 = t >= n1;
     const int k0 = s2 ? kbeg2 + (t - n1) * BKE : kbeg + t * BKE;
     const int ke = s2 ? kend2 : kend;
@@ -331,23 +344,24 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
     else
       stage_half<B_KMAJOR, EB>(a.B, a.ldb, n0, a.N, k0, ke, false, j == H_BHI, dst, wave, lane);
   };
-  // valid halves issued at global phases (P - D, P]; half (t, j) is issued at 4t - 5 + j
+  auto issue_h = [&](int h) { issue(h >> 2, h & 3); };
+  // valid halves issued at global phases (P - D, P]; half (t, j) is issued at 4t - 5 - X + j
   auto outstanding = [&](int P) {
-    int hi = P < 4 * nkt - 6 ? P : 4 * nkt - 6;
+    const int last = 4 * nkt - 6 - X;
+    int hi = P < last ? P : last;
     int c = hi - (P - D);
     return c < 0 ? 0 : (c > D ? D : c);
   };
 
   if (nkt > 0) {
-    issue(0, H_ALO); issue(0, H_BLO); issue(0, H_BHI); issue(0, H_AHI);
-    issue(1, H_ALO); issue(1, H_BLO);
+#pragma unroll
+    for (int h = 0; h < 6 + X; ++h) issue_h(h);   // every half issued at phase <= 0
     vmwait_count<D>(outstanding(0));
     barrier();
     if (wr == 1) barrier();
 
     v8s fa[4][2], fbl[2][2], fbh[2][2];
     for (int t = 0; t < nkt; ++t) {
-      const char* buf = smem + (t & 1) * BUF_BYTES;
       const bool two = F8 || (t >= n1 ? (kend2 - (kbeg2 + (t - n1) * BK)) > 32
                                        : (kend - (kbeg + t * BK)) > 32);
       const int P = 4 * t;
@@ -356,13 +370,13 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          fbl[i][ks] = read_frag<B_KMAJOR>(buf + H_BLO * HALF_BYTES, wc * 32 + i * 16, ks, lane);
+          fbl[i][ks] = read_frag<B_KMAJOR>(slot(t, H_BLO), wc * 32 + i * 16, ks, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          fa[j][ks] = read_frag<A_KMAJOR>(buf + H_ALO * HALF_BYTES, wr * 64 + j * 16, ks, lane);
-      issue(t + 1, H_BHI);
+          fa[j][ks] = read_frag<A_KMAJOR>(slot(t, H_ALO), wr * 64 + j * 16, ks, lane);
+      issue_h(4 * t + 6 + X);
       vmwait_count<D>(outstanding(P + 1));
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -376,8 +390,8 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          fbh[i][ks] = read_frag<B_KMAJOR>(buf + H_BHI * HALF_BYTES, wc * 32 + i * 16, ks, lane);
-      issue(t + 1, H_AHI);
+          fbh[i][ks] = read_frag<B_KMAJOR>(slot(t, H_BHI), wc * 32 + i * 16, ks, lane);
+      issue_h(4 * t + 7 + X);
       vmwait_count<D>(outstanding(P + 2));
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -390,8 +404,8 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          fa[j][ks] = read_frag<A_KMAJOR>(buf + H_AHI * HALF_BYTES, wr * 64 + j * 16, ks, lane);
-      issue(t + 2, H_ALO);
+          fa[j][ks] = read_frag<A_KMAJOR>(slot(t, H_AHI), wr * 64 + j * 16, ks, lane);
+      issue_h(4 * t + 8 + X);
       vmwait_count<D>(outstanding(P + 3));
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -401,7 +415,7 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
       __builtin_amdgcn_s_setprio(0);
       barrier();
       // ---- r4: M4-7 x N0-1 (no LDS reads)
-      issue(t + 2, H_BLO);
+      issue_h(4 * t + 9 + X);
       vmwait_count<D>(outstanding(P + 4));
       barrier();
       __builtin_amdgcn_s_setprio(1);
@@ -457,7 +471,7 @@ __device__ __forceinline__ int krange_len(const GemmArgs& a, int tn) {
 
 template <bool A_KMAJOR, bool B_KMAJOR, int EPI, int D, bool DB, bool F8 = false>
 __global__ void __launch_bounds__(NTHR, 1) gemm256_kernel(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[smem_bytes(D)];
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   if (!a.pair_tiles) {
     gemm256_body<A_KMAJOR, B_KMAJOR, EPI, D, DB, F8>(a, xcd_remap(blockIdx.x, ntm * ntn),
@@ -491,7 +505,7 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_kernel(GemmArgs a) {
 // grouped weight gradients (same block layout as gemm.hip's gemm_group_kernel)
 template <int D>
 __global__ void __launch_bounds__(NTHR, 1) gemm256_group_kernel(GroupArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[smem_bytes(D)];
   const int id = xcd_remap(blockIdx.x, g.start[g.nprob]);
   int p = 0;
 #pragma unroll
@@ -525,7 +539,7 @@ struct TnMulti {
 
 template <int D>
 __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[smem_bytes(D)];
   const int id = t.tile0 + xcd_remap(blockIdx.x, t.ntiles);
   int p = 0;
   for (int q = 1; q < t.n; ++q)
@@ -544,7 +558,10 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
   gemm256_body<false, false, EPI_F32, D, true>(a, local, 0, smem);
 }
 
-static int g_depth = 4;
+static int g_depth = [] {
+  const char* e = getenv("VINF_G256_DEPTH");
+  return e && atoi(e) == 6 ? 6 : 4;
+}();
 
 int device_cus_256() {
   static const int n = [] {
@@ -573,10 +590,10 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
   a.pair_tiles = pair_env && a.krange && splits == 1 && ntn % 2 == 0 &&
                  (pair_env == 2 || (long)ntm * (ntn / 2) >= device_cus_256());
   dim3 grid(a.pair_tiles ? ntm * (ntn / 2) : ntm * ntn, splits), block(NTHR);
-  if (g_depth == 4)
+  if (g_depth != 6)
     hipLaunchKernelGGL((gemm256_kernel<AK, BK_, EPI, 4, DB>), grid, block, 0, stream, a);
   else
-    hipLaunchKernelGGL((gemm256_kernel<AK, BK_, EPI, 3, DB>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((gemm256_kernel<AK, BK_, EPI, 6, DB>), grid, block, 0, stream, a);
   NF_HIP_CHECK(hipGetLastError());
 }
 
@@ -586,7 +603,9 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
 
 using namespace nf::gemm;
 
-void nf_gemm256_set_depth(int d) { g256::g_depth = d == 3 ? 3 : 4; }
+// 4 (default): 8-slot LDS ring, 128 KiB; 6: 10-slot ring, 160 KiB, half-tiles issued 2 phases
+// earlier (VINF_G256_DEPTH at load, or set_mode's depth argument)
+void nf_gemm256_set_depth(int d) { g256::g_depth = d == 6 ? 6 : 4; }
 
 // y[M][N] = act(x[M][K] W[N][K]^T + bias) -> bf16
 void nf_launch_gemm256_nt(const void* x, long ldx, const void* W, long ldw, const void* bias,
@@ -740,8 +759,8 @@ void nf_launch_gemm256_fp8_nt(const void* xq, long ldx, const float* sx, int sx_
   a.pair_tiles = pv && krange && ntn % 2 == 0 &&
                  (pv == 2 || (long)ntm * (ntn / 2) >= g256::device_cus_256());
   const int nblk = a.pair_tiles ? ntm * (ntn / 2) : ntm * ntn;
-  if (g256::g_depth == 3)
-    hipLaunchKernelGGL((g256::gemm256_kernel<true, true, EPI_BF16, 3, false, true>),
+  if (g256::g_depth == 6)
+    hipLaunchKernelGGL((g256::gemm256_kernel<true, true, EPI_BF16, 6, false, true>),
                        dim3(nblk), dim3(g256::NTHR), 0, stream, a);
   else
     hipLaunchKernelGGL((g256::gemm256_kernel<true, true, EPI_BF16, 4, false, true>),
@@ -796,16 +815,16 @@ void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int
   }
   t.tile0 = tile0;
   t.ntiles = ntiles;
-  if (g256::g_depth == 3)
-    hipLaunchKernelGGL(g256::gemm256_multi_kernel<3>, dim3(ntiles), dim3(g256::NTHR), 0, stream, t);
+  if (g256::g_depth == 6)
+    hipLaunchKernelGGL(g256::gemm256_multi_kernel<6>, dim3(ntiles), dim3(g256::NTHR), 0, stream, t);
   else
     hipLaunchKernelGGL(g256::gemm256_multi_kernel<4>, dim3(ntiles), dim3(g256::NTHR), 0, stream, t);
   NF_HIP_CHECK(hipGetLastError());
 }
 
 void nf_launch_gemm256_tn_group(const GroupArgs& g, hipStream_t stream) {
-  if (g256::g_depth == 3)
-    hipLaunchKernelGGL(g256::gemm256_group_kernel<3>, dim3(g.start[g.nprob]), dim3(g256::NTHR), 0,
+  if (g256::g_depth == 6)
+    hipLaunchKernelGGL(g256::gemm256_group_kernel<6>, dim3(g.start[g.nprob]), dim3(g256::NTHR), 0,
                        stream, g);
   else
     hipLaunchKernelGGL(g256::gemm256_group_kernel<4>, dim3(g.start[g.nprob]), dim3(g256::NTHR), 0,

@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--only", default=None, help="comma-separated shape names")
     ap.add_argument("--mine-only", action="store_true", help="skip the hipBLASLt reference")
     ap.add_argument("--modes", default=None,
-                    help="compare kernel choices, e.g. 128,256d3,256d4 (M = batch products)")
+                    help="compare kernel choices, e.g. 128,256d4,256d6 (M = batch products)")
     ap.add_argument("--custom", default=None,
                     help="extra shapes 'kind:M:N:K,...' (kind nt | ntplain | nn_mask | tn)")
     a = ap.parse_args()
@@ -132,7 +132,7 @@ def main():
                 for m in res:
                     mode = 1 if m == "128" else (3 if m.startswith("256t") else
                                                  (2 if m.startswith("256") else 0))
-                    ops.gemm_set_mode(mode, 3 if m.endswith("d3") else 4)
+                    ops.gemm_set_mode(mode, 6 if m.endswith("d6") else 4)
                     res[m].append(_time(mine, a.iters))
             ops.gemm_set_mode(0, 4)
             rec = {"shape": name, "M": M, "N": N, "K": K}
