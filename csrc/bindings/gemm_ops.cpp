@@ -383,6 +383,44 @@ void maf_bwd(const at::Tensor& gu, const at::Tensor& u, const at::Tensor& o, dou
                     gx.data_ptr<float>(), ld2(gx), cur_stream());
 }
 
+// gated IAF update: y = m + sigmoid(s + gb) (z - m), ldj = sum log sigmoid(s + gb)
+void iaf_gate_fwd(const at::Tensor& o, const at::Tensor& z, double gate_bias, const at::Tensor& y,
+                  const at::Tensor& ldj) {
+  chk_mat(o, "o", at::kBFloat16);
+  chk_mat(z, "z", at::kFloat);
+  chk_mat(y, "y", at::kFloat);
+  const int B = z.size(0), D = z.size(1);
+  TORCH_CHECK(D % 4 == 0 && o.size(0) == B && o.size(1) == 2 * D && y.size(0) == B &&
+                  y.size(1) == D, "iaf_gate_fwd shapes");
+  TORCH_CHECK(ldj.is_cuda() && ldj.scalar_type() == at::kFloat && ldj.is_contiguous() &&
+                  ldj.numel() == B, "ldj: fp32 [B]");
+  nf_launch_iaf_gate_fwd(o.data_ptr(), ld2(o), z.data_ptr<float>(), ld2(z), B, D, (float)gate_bias,
+                         y.data_ptr<float>(), ld2(y), ldj.data_ptr<float>(), cur_stream());
+}
+
+void iaf_gate_bwd(const at::Tensor& gy, const c10::optional<at::Tensor>& gl, const at::Tensor& z,
+                  const at::Tensor& o, double gate_bias, const at::Tensor& dout,
+                  const at::Tensor& gz) {
+  chk_mat(gy, "gy", at::kFloat);
+  chk_mat(z, "z", at::kFloat);
+  chk_mat(o, "o", at::kBFloat16);
+  chk_mat(dout, "dout", at::kBFloat16);
+  chk_mat(gz, "gz", at::kFloat);
+  const int B = z.size(0), D = z.size(1);
+  TORCH_CHECK(D % 4 == 0 && gy.size(0) == B && gy.size(1) == D && o.size(0) == B &&
+                  o.size(1) == 2 * D && dout.size(0) == B && dout.size(1) == 2 * D &&
+                  gz.size(0) == B && gz.size(1) == D, "iaf_gate_bwd shapes");
+  const float* glp = nullptr;
+  if (gl && gl->defined()) {
+    TORCH_CHECK(gl->is_cuda() && gl->scalar_type() == at::kFloat && gl->is_contiguous() &&
+                    gl->numel() == B, "gl: fp32 [B]");
+    glp = gl->data_ptr<float>();
+  }
+  nf_launch_iaf_gate_bwd(gy.data_ptr<float>(), ld2(gy), glp, z.data_ptr<float>(), ld2(z),
+                         o.data_ptr(), ld2(o), B, D, (float)gate_bias, dout.data_ptr(), ld2(dout),
+                         gz.data_ptr<float>(), ld2(gz), cur_stream());
+}
+
 // ----------------------------------------------------------------- masked (MADE) variants
 void chk_ranges(const at::Tensor& r, long ntiles, const char* n) {
   TORCH_CHECK(r.is_cuda() && r.scalar_type() == at::kInt && r.is_contiguous() && r.numel() == 2 * ntiles,
@@ -586,6 +624,8 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("gemm_nn_cpl(Tensor dy, Tensor W, Tensor G, Tensor s_hat, Tensor x, Tensor(a!) dst, Tensor(b!) gx, float scale, float c) -> ()");
   m.def("fp8_quant_rows_strided(Tensor x, int layer_stride, int rows_per, int layers, int C, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("maf_fwd(Tensor x, Tensor o, float bound, Tensor(a!) u, Tensor(b!)? ubf, Tensor(c!)? uq, Tensor? amax_prev, Tensor(d!)? scale, Tensor(e!)? amax_cur, Tensor(f!) ldj, bool ldj_init) -> ()");
+  m.def("iaf_gate_fwd(Tensor o, Tensor z, float gate_bias, Tensor(a!) y, Tensor(b!) ldj) -> ()");
+  m.def("iaf_gate_bwd(Tensor gy, Tensor? gl, Tensor z, Tensor o, float gate_bias, Tensor(a!) dout, Tensor(b!) gz) -> ()");
   m.def("maf_bwd(Tensor gu, Tensor u, Tensor o, float bound, float c_ldj, Tensor(a!) dout, Tensor(b!) gx) -> ()");
 }
 
@@ -604,6 +644,8 @@ TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
   m.impl("fp8_quant_rows_strided", &fp8_quant_rows_strided);
   m.impl("maf_fwd", &maf_fwd);
   m.impl("maf_bwd", &maf_bwd);
+  m.impl("iaf_gate_fwd", &iaf_gate_fwd);
+  m.impl("iaf_gate_bwd", &iaf_gate_bwd);
   m.impl("fp8_quant_tensor", &fp8_quant_tensor);
   m.impl("gemm_fp8_nt", &gemm_fp8_nt);
 }

@@ -169,6 +169,12 @@ void nf_launch_maf_fwd(const float* x, long ldx, const void* o, long ldo, int B,
 void nf_launch_maf_bwd(const float* gu, long ldg, const float* u, long ldu, const void* o, long ldo,
                        int B, int D, float bound, float c_ldj, void* dout, long lddo, float* gx,
                        long ldgx, hipStream_t stream);
+// maf.hip: gated IAF update (o = [m | s] bf16 from the MADE GEMM)
+void nf_launch_iaf_gate_fwd(const void* o, long ldo, const float* z, long ldz, int B, int D,
+                            float gate_bias, float* y, long ldy, float* ldj, hipStream_t stream);
+void nf_launch_iaf_gate_bwd(const float* gy, long ldg, const float* gl, const float* z, long ldz,
+                            const void* o, long ldo, int B, int D, float gate_bias, void* dout,
+                            long lddo, float* gz, long ldgz, hipStream_t stream);
 // fp8.hip: layer-strided per-row weight quantisation (rows r -> layer r / rows_per)
 void nf_launch_fp8_quant_rows_strided(const void* x, int x_is_bf16, long ldx, long layer_stride,
                                       int rows_per, int R, int C, void* q, long ldq, int Cq,

@@ -132,9 +132,116 @@ __global__ void __launch_bounds__(256) maf_bwd_kernel(const float* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------- gated IAF update
+// Kingma et al. 2016 (eq. 11-12), the VI direction of an IAF layer, o = MADE(z, h) = [m | s]:
+//   sig = sigmoid(s + gate_bias),  y = sig * z + (1 - sig) * m = m + sig * (z - m),
+//   ldj = sum_d log sig
+// iaf_gate_bwd, given gy = dL/dy and gl = dL/dldj (per row, optional):
+//   gz = gy sig,  dm = gy (1 - sig),  ds = gy sig (1 - sig)(z - m) + gl (1 - sig)
+// (d log sig / ds = 1 - sig). d_o = [dm | ds] is written in bf16 (the masked GEMMs' operand).
+// One wave per row, 4 columns per lane-step.
+__device__ __forceinline__ float sigmoidf_(float t) { return 1.f / (1.f + __expf(-t)); }
+__device__ __forceinline__ float log_sigmoidf_(float t) {   // min(t, 0) - log1p(exp(-|t|))
+  return fminf(t, 0.f) - log1pf(__expf(-fabsf(t)));
+}
+
+__global__ void __launch_bounds__(256) iaf_gate_fwd_kernel(const bf16_t* __restrict__ o, long ldo,
+                                                           const float* __restrict__ z, long ldz,
+                                                           int B, int D, float gb,
+                                                           float* __restrict__ y, long ldy,
+                                                           float* __restrict__ ldj) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const bf16_t* mr = o + (long)row * ldo;
+  const bf16_t* sr = mr + D;
+  const float* zr = z + (long)row * ldz;
+  float* yr = y + (long)row * ldy;
+  float acc = 0.f;
+  for (int c = lane * 4; c < D; c += 256) {
+    const ushort4 mv = *reinterpret_cast<const ushort4*>(mr + c);
+    const ushort4 sv = *reinterpret_cast<const ushort4*>(sr + c);
+    const float4 zv = *reinterpret_cast<const float4*>(zr + c);
+    const float ms[4] = {bf2f(mv.x), bf2f(mv.y), bf2f(mv.z), bf2f(mv.w)};
+    const float ss[4] = {bf2f(sv.x), bf2f(sv.y), bf2f(sv.z), bf2f(sv.w)};
+    const float zs[4] = {zv.x, zv.y, zv.z, zv.w};
+    float ys[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float t = ss[e] + gb;
+      ys[e] = fmaf(sigmoidf_(t), zs[e] - ms[e], ms[e]);
+      acc += log_sigmoidf_(t);
+    }
+    *reinterpret_cast<float4*>(yr + c) = make_float4(ys[0], ys[1], ys[2], ys[3]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if (lane == 0) ldj[row] = acc;
+}
+
+__global__ void __launch_bounds__(256) iaf_gate_bwd_kernel(const float* __restrict__ gy, long ldg,
+                                                           const float* __restrict__ gl,
+                                                           const float* __restrict__ z, long ldz,
+                                                           const bf16_t* __restrict__ o, long ldo,
+                                                           int B, int D, float gb,
+                                                           bf16_t* __restrict__ dout, long lddo,
+                                                           float* __restrict__ gz, long ldgz) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const float g_l = gl ? gl[row] : 0.f;
+  const bf16_t* mr = o + (long)row * ldo;
+  const bf16_t* sr = mr + D;
+  const float* gr = gy + (long)row * ldg;
+  const float* zr = z + (long)row * ldz;
+  bf16_t* dm = dout + (long)row * lddo;
+  bf16_t* ds = dm + D;
+  for (int c = lane * 4; c < D; c += 256) {
+    const ushort4 mv = *reinterpret_cast<const ushort4*>(mr + c);
+    const ushort4 sv = *reinterpret_cast<const ushort4*>(sr + c);
+    const float4 zv = *reinterpret_cast<const float4*>(zr + c);
+    const float4 gv = *reinterpret_cast<const float4*>(gr + c);
+    const float ms[4] = {bf2f(mv.x), bf2f(mv.y), bf2f(mv.z), bf2f(mv.w)};
+    const float ss[4] = {bf2f(sv.x), bf2f(sv.y), bf2f(sv.z), bf2f(sv.w)};
+    const float zs[4] = {zv.x, zv.y, zv.z, zv.w};
+    const float gs[4] = {gv.x, gv.y, gv.z, gv.w};
+    float gzs[4], dms[4], dss[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float sg = sigmoidf_(ss[e] + gb), om = 1.f - sg;
+      gzs[e] = gs[e] * sg;
+      dms[e] = gs[e] * om;
+      dss[e] = om * fmaf(gs[e] * sg, zs[e] - ms[e], g_l);
+    }
+    *reinterpret_cast<float4*>(gz + (long)row * ldgz + c) = make_float4(gzs[0], gzs[1], gzs[2], gzs[3]);
+    ushort4 a, b;
+    a.x = f2bf(dms[0]); a.y = f2bf(dms[1]); a.z = f2bf(dms[2]); a.w = f2bf(dms[3]);
+    b.x = f2bf(dss[0]); b.y = f2bf(dss[1]); b.z = f2bf(dss[2]); b.w = f2bf(dss[3]);
+    *reinterpret_cast<ushort4*>(dm + c) = a;
+    *reinterpret_cast<ushort4*>(ds + c) = b;
+  }
+}
+
 }  // namespace nf
 
 using namespace nf;
+
+void nf_launch_iaf_gate_fwd(const void* o, long ldo, const float* z, long ldz, int B, int D,
+                            float gate_bias, float* y, long ldy, float* ldj, hipStream_t stream) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(iaf_gate_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream,
+                     (const bf16_t*)o, ldo, z, ldz, B, D, gate_bias, y, ldy, ldj);
+  NF_HIP_CHECK(hipGetLastError());
+}
+
+void nf_launch_iaf_gate_bwd(const float* gy, long ldg, const float* gl, const float* z, long ldz,
+                            const void* o, long ldo, int B, int D, float gate_bias, void* dout,
+                            long lddo, float* gz, long ldgz, hipStream_t stream) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(iaf_gate_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, gy, ldg, gl, z,
+                     ldz, (const bf16_t*)o, ldo, B, D, gate_bias, (bf16_t*)dout, lddo, gz, ldgz);
+  NF_HIP_CHECK(hipGetLastError());
+}
 
 void nf_launch_maf_fwd(const float* x, long ldx, const void* o, long ldo, int B, int D, float bound,
                        float* u, long ldu, void* ubf, long ldub, void* uq, long lduq,

@@ -101,6 +101,11 @@ class MADE(nn.Module):
             last.weight.mul_(1e-2)
 
     def forward(self, x, context=None):
+        from ..ops import made_fused
+
+        if made_fused.supported(self, x, context):   # GPU: one fused node (ops/made_fused.py)
+            return made_fused.made_forward(self, x, context).view(x.shape[0], self.out_mult,
+                                                                  self.dim)
         h = x
         for i, layer in enumerate(self.layers):
             h = layer(h)
@@ -124,6 +129,11 @@ class IAF(Flow):
         self.uses_context = context_dim > 0
 
     def forward(self, z, context=None):
+        if self.mode == "gated":
+            from ..ops import made_fused
+
+            if made_fused.supported(self.made, z, context):
+                return made_fused.iaf_gated(self, z, context)
         out = self.made(z, context)
         m, s = out[:, 0], out[:, 1]
         if self.mode == "gated":
