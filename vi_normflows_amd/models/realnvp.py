@@ -311,15 +311,28 @@ class RealNVPVI:
 
     def forward(self):
         cfg, P = self.cfg, self.params
-        L, Dh = cfg.n_layers, cfg.half
+        Dh = cfg.half
         if self.eps_override is None:
             fused.reparam_sample(self.z0, mu=P.p("base.mu"), logvar=P.p("base.logvar"),
                                  seed=self.seed, offset=self.rng_offset, stream_id=self.rank,
                                  eps=self.eps0, zbf=self.Hbf[0], nbf=Dh, logq0=self.logq0)
         else:
             self._base_from_eps(self.eps_override)
+        self._flow_layers()
+        A, Bh, ia, ib = self.zK_halves()
+        ta = self._target_args()
+        fused.target_logp_grad(ta["kind"], A, Bh, gA=self.G[ia], gB=self.G[ib],
+                               grad_accumulate=False, params=ta.get("params"), p0=ta.get("p0", 1.0),
+                               p1=ta.get("p1", 1.0), p2=ta.get("p2", 0.0), cst=ta["cst"],
+                               beta=self.beta, row_weight=1.0 / self.B, logq0=self.logq0,
+                               ldj=self.ldj, logp_out=self.logp, frow_out=self.frow)
+        torch.mean(self.frow, 0, out=self.loss)
+
+    def _flow_layers(self):
+        """h_0, h_1 -> h_{L+1} through the L coupling layers; ldj = sum of the log-dets."""
+        cfg, P = self.cfg, self.params
+        L, nh = cfg.n_layers, cfg.n_hidden
         fuse = self.cf_fuse and gemm.backend() == "mfma"
-        nh = cfg.n_hidden
         for l in range(L):
             ybf = self.Hbf[l + 1] if l + 1 < L else None
             if fuse:
@@ -334,14 +347,6 @@ class RealNVPVI:
                                ldj_init=(l == 0))
         if fuse:
             torch.sum(self.ldjp, 0, out=self.ldj)
-        A, Bh, ia, ib = self.zK_halves()
-        ta = self._target_args()
-        fused.target_logp_grad(ta["kind"], A, Bh, gA=self.G[ia], gB=self.G[ib],
-                               grad_accumulate=False, params=ta.get("params"), p0=ta.get("p0", 1.0),
-                               p1=ta.get("p1", 1.0), p2=ta.get("p2", 0.0), cst=ta["cst"],
-                               beta=self.beta, row_weight=1.0 / self.B, logq0=self.logq0,
-                               ldj=self.ldj, logp_out=self.logp, frow_out=self.frow)
-        torch.mean(self.frow, 0, out=self.loss)
 
     def _base_from_eps(self, eps: torch.Tensor):
         """Deterministic base sample from given noise (tests / replaying a noise stream)."""
@@ -536,15 +541,11 @@ class RealNVPVI:
         n = n or self.B
         assert n <= self.B
         cfg, P = self.cfg, self.params
-        Dh, L = cfg.half, cfg.n_layers
+        Dh = cfg.half
         fused.reparam_sample(self.z0, mu=P.p("base.mu"), logvar=P.p("base.logvar"),
                              seed=self.seed + 1, offset_host=offset, stream_id=self.rank,
                              eps=self.eps0, zbf=self.Hbf[0], nbf=Dh, logq0=self.logq0)
-        for l in range(L):
-            st = self._conditioner_fwd(l, self.Hbf[l])
-            ybf = self.Hbf[l + 1] if l + 1 < L else None
-            fused.coupling_fwd(st, self.h(l), self.h(l + 2), ybf=ybf, ssav=None, ldj=self.ldj,
-                               scale=cfg.scale_bound, ldj_init=(l == 0))
+        self._flow_layers()
         A, Bh, _, _ = self.zK_halves()
         z = torch.cat([A, Bh], 1)[:n].clone()
         logq = (self.logq0 - self.ldj)[:n].clone()
