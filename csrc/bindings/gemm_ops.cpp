@@ -369,7 +369,8 @@ void maf_fwd(const at::Tensor& x, const at::Tensor& o, double bound, const at::T
 }
 
 void maf_bwd(const at::Tensor& gu, const at::Tensor& u, const at::Tensor& o, double bound,
-             double c_ldj, const at::Tensor& dout, const at::Tensor& gx) {
+             double c_ldj, const at::Tensor& dout, const at::Tensor& gx,
+             const c10::optional<at::Tensor>& c_row) {
   chk_mat(gu, "gu", at::kFloat);
   chk_mat(u, "u", at::kFloat);
   chk_mat(o, "o", at::kBFloat16);
@@ -378,9 +379,15 @@ void maf_bwd(const at::Tensor& gu, const at::Tensor& u, const at::Tensor& o, dou
   const int B = gu.size(0), D = gu.size(1);
   TORCH_CHECK(D % 4 == 0 && u.size(0) == B && u.size(1) == D && o.size(1) == 2 * D &&
                   dout.size(1) == 2 * D && gx.size(1) == D, "maf_bwd shapes");
+  const float* cr = nullptr;
+  if (c_row && c_row->defined()) {
+    TORCH_CHECK(c_row->is_cuda() && c_row->scalar_type() == at::kFloat &&
+                    c_row->is_contiguous() && c_row->numel() == B, "c_row: fp32 [B]");
+    cr = c_row->data_ptr<float>();
+  }
   nf_launch_maf_bwd(gu.data_ptr<float>(), ld2(gu), u.data_ptr<float>(), ld2(u), o.data_ptr(),
                     ld2(o), B, D, (float)bound, (float)c_ldj, dout.data_ptr(), ld2(dout),
-                    gx.data_ptr<float>(), ld2(gx), cur_stream());
+                    gx.data_ptr<float>(), ld2(gx), cur_stream(), cr);
 }
 
 // gated IAF update: y = m + sigmoid(s + gb) (z - m), ldj = sum log sigmoid(s + gb)
@@ -626,7 +633,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("maf_fwd(Tensor x, Tensor o, float bound, Tensor(a!) u, Tensor(b!)? ubf, Tensor(c!)? uq, Tensor? amax_prev, Tensor(d!)? scale, Tensor(e!)? amax_cur, Tensor(f!) ldj, bool ldj_init) -> ()");
   m.def("iaf_gate_fwd(Tensor o, Tensor z, float gate_bias, Tensor(a!) y, Tensor(b!) ldj) -> ()");
   m.def("iaf_gate_bwd(Tensor gy, Tensor? gl, Tensor z, Tensor o, float gate_bias, Tensor(a!) dout, Tensor(b!) gz) -> ()");
-  m.def("maf_bwd(Tensor gu, Tensor u, Tensor o, float bound, float c_ldj, Tensor(a!) dout, Tensor(b!) gx) -> ()");
+  m.def("maf_bwd(Tensor gu, Tensor u, Tensor o, float bound, float c_ldj, Tensor(a!) dout, Tensor(b!) gx, Tensor? c_row=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(vinf, CUDA, m) {

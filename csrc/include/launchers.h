@@ -168,7 +168,7 @@ void nf_launch_maf_fwd(const float* x, long ldx, const void* o, long ldo, int B,
                        int ldj_init, hipStream_t stream);
 void nf_launch_maf_bwd(const float* gu, long ldg, const float* u, long ldu, const void* o, long ldo,
                        int B, int D, float bound, float c_ldj, void* dout, long lddo, float* gx,
-                       long ldgx, hipStream_t stream);
+                       long ldgx, hipStream_t stream, const float* c_row = nullptr);
 // maf.hip: gated IAF update (o = [m | s] bf16 from the MADE GEMM)
 void nf_launch_iaf_gate_fwd(const void* o, long ldo, const float* z, long ldz, int B, int D,
                             float gate_bias, float* y, long ldy, float* ldj, hipStream_t stream);

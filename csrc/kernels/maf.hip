@@ -95,11 +95,13 @@ __global__ void __launch_bounds__(256) maf_bwd_kernel(const float* __restrict__ 
                                                       const float* __restrict__ u, long ldu,
                                                       const bf16_t* __restrict__ o, long ldo,
                                                       int B, int D, float bound, float c_ldj,
+                                                      const float* __restrict__ c_row,
                                                       bf16_t* __restrict__ dout, long lddo,
                                                       float* __restrict__ gx, long ldgx) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
+  if (c_row) c_ldj = c_row[row];   // per-row dL/d(sum alpha) (autograd callers)
   const float* gr = gu + (long)row * ldg;
   const float* ur = u + (long)row * ldu;
   const bf16_t* sr = o + (long)row * ldo + D;
@@ -260,9 +262,10 @@ void nf_launch_maf_fwd(const float* x, long ldx, const void* o, long ldo, int B,
 
 void nf_launch_maf_bwd(const float* gu, long ldg, const float* u, long ldu, const void* o, long ldo,
                        int B, int D, float bound, float c_ldj, void* dout, long lddo, float* gx,
-                       long ldgx, hipStream_t stream) {
+                       long ldgx, hipStream_t stream, const float* c_row) {
   if (B <= 0) return;
   hipLaunchKernelGGL(maf_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, gu, ldg, u, ldu,
-                     (const bf16_t*)o, ldo, B, D, bound, c_ldj, (bf16_t*)dout, lddo, gx, ldgx);
+                     (const bf16_t*)o, ldo, B, D, bound, c_ldj, c_row, (bf16_t*)dout, lddo, gx,
+                     ldgx);
   NF_HIP_CHECK(hipGetLastError());
 }

@@ -182,6 +182,10 @@ class MAF(Flow):
         return out[:, 0], self.bound * torch.tanh(out[:, 1] / self.bound)
 
     def inverse(self, x, context=None):
+        from ..ops import made_fused
+
+        if made_fused.supported(self.made, x, context) and x.shape[1] % 4 == 0:
+            return made_fused.maf_inverse(self, x, context)
         mu, alpha = self._mu_alpha(x, context)
         return (x - mu) * torch.exp(-alpha), -alpha.sum(1)
 

@@ -56,7 +56,7 @@ def supported(made, x: torch.Tensor, context) -> bool:
     """Shapes the fused path handles (else the per-layer path runs)."""
     if not (enabled() and x.is_cuda and x.dim() == 2 and x.dtype == torch.float32):
         return False
-    if any(getattr(l, "precision", "bf16") != "bf16" for l in made.layers):
+    if any(getattr(l, "precision", "bf16") not in ("bf16", "fp8") for l in made.layers):
         return False
     if not isinstance(made.act, torch.nn.ReLU) or len(made.layers) < 2:
         return False
@@ -105,11 +105,32 @@ def _made_fwd(made, x, context):
             Ws.append(W)
             masks.append(m)
         out = torch.empty(N, W.shape[0], device=x.device, dtype=_BF)
-        native().masked_gemm_nt(h, W, b, out, 1 if i < L - 1 else 0, plan_for(m).fwd)
-        if i < L - 1:
+        relu = i < L - 1
+        if getattr(layer, "precision", "bf16") == "fp8" and h.shape[1] % 128 == 0:
+            Wf = layer.weight * layer.mask       # quantised from fp32, as ops.masked does
+            if i == 0 and has_ctx:
+                Wf = torch.cat([Wf, made.ctx.weight], 1)
+            _fp8_product(layer, h, Wf, b, m, relu, out)
+        else:
+            native().masked_gemm_nt(h, W, b, out, 1 if relu else 0, plan_for(m).fwd)
+        if relu:
             acts.append(out)
         h = out
     return h, (Ws, masks, acts, has_ctx, D)
+
+
+def _fp8_product(layer, h, Wf, b, m, relu, out):
+    """The forward product of an fp8 MaskedLinear (same scaling as ``ops.masked``): e4m3
+    activations under the layer's delayed per-tensor scale, e4m3 masked weights with per-row
+    scales, the K=128 MX MFMA kernel (256x256 instantiation with the plan's K ranges)."""
+    from .fp8 import DelayedScale, gemm_fp8, quantize_rows
+
+    st = layer.__dict__.get("_fp8_scale")
+    if st is None or st.amax.device != h.device:
+        st = layer.__dict__["_fp8_scale"] = DelayedScale(h.device)
+    xq, sx = st.quantize(h)
+    wq, sw = quantize_rows(Wf.contiguous(), xq.shape[1])
+    gemm_fp8(xq, sx, wq, sw, b, relu, plan_for(m).fwd, out=out)
 
 
 def _made_bwd(made, saved, g: torch.Tensor, dx0: torch.Tensor | None, need_dx: bool):
@@ -219,5 +240,49 @@ def iaf_gated(iaf, z, context=None):
     """(y, ldj) of a gated IAF layer through the fused path."""
     made = iaf.made
     has_ctx = made.ctx is not None and context is not None
-    return _IAFGatedFn.apply(made, iaf.gate_bias, z, context if has_ctx else None,
+    return _IAFGatedFn.apply(made, iaf.gate_bias, z.contiguous(), context if has_ctx else None,
                              *_params(made, has_ctx))
+
+
+class _MAFInverseFn(torch.autograd.Function):
+    """MAF density direction x -> u (``flows.made.MAF.inverse``): the fused MADE, then
+    ``maf_fwd`` (u = (x - mu) e^-alpha, ldj = -sum alpha, alpha = bound tanh(s / bound)) and,
+    backward, ``maf_bwd`` with the per-row log-det gradient (csrc/kernels/maf.hip)."""
+
+    @staticmethod
+    def forward(ctx, made, bound, x, context, *params):
+        o, saved = _made_fwd(made, x, context)
+        N, D = x.shape
+        u = torch.empty(N, D, device=x.device, dtype=torch.float32)
+        ldj = torch.empty(N, device=x.device, dtype=torch.float32)
+        native().maf_fwd(x, o, float(bound), u, None, None, None, None, None, ldj, True)
+        ctx.made, ctx.saved, ctx.bound = made, saved, float(bound)
+        ctx.save_for_backward(u, o)
+        return u, ldj
+
+    @staticmethod
+    def backward(ctx, gu, gldj):
+        u, o = ctx.saved_tensors
+        N, D = u.shape
+        if gu is None:
+            gu = torch.zeros(N, D, device=u.device, dtype=torch.float32)
+        gu = gu.float().contiguous()
+        # L += gldj * ldj = -gldj * sum(alpha): dL/d(sum alpha) = -gldj per row
+        c_row = (-gldj.float()).contiguous() if gldj is not None else None
+        dout = torch.empty(N, 2 * D, device=u.device, dtype=_BF)
+        gx = torch.empty(N, D, device=u.device, dtype=torch.float32)
+        native().maf_bwd(gu, u, o, ctx.bound, 0.0, dout, gx, c_row)
+        need = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        dx, dctx, grads = _made_bwd(ctx.made, ctx.saved, dout, gx, need)
+        if not need:
+            dx = None
+        ctx.saved = None
+        return (None, None, dx, dctx, *grads)
+
+
+def maf_inverse(maf, x, context=None):
+    """(u, ldj) of a MAF layer's density direction through the fused path."""
+    made = maf.made
+    has_ctx = made.ctx is not None and context is not None
+    return _MAFInverseFn.apply(made, maf.bound, x.contiguous(), context if has_ctx else None,
+                               *_params(made, has_ctx))
