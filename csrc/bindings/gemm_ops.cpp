@@ -73,13 +73,21 @@ void gemm_nt(const at::Tensor& x, const at::Tensor& W, const c10::optional<at::T
 
 // dx = dy W  [* 1(h > 0)]: dy [M,K], W [K,N] bf16; dx bf16 (mask) or fp32 (+= when accumulate)
 void gemm_nn(const at::Tensor& dy, const at::Tensor& W, const c10::optional<at::Tensor>& h,
-             const at::Tensor& dx, bool accumulate, const c10::optional<at::Tensor>& hbits) {
+             const at::Tensor& dx, bool accumulate, const c10::optional<at::Tensor>& hbits,
+             const c10::optional<at::Tensor>& Wt) {
   chk_mat(dy, "dy", at::kBFloat16);
   chk_mat(W, "W", at::kBFloat16);
   const bool f32 = dx.scalar_type() == at::kFloat;
   chk_mat(dx, "dx", f32 ? at::kFloat : at::kBFloat16);
   const int M = dy.size(0), K = dy.size(1), N = W.size(1);
   TORCH_CHECK(W.size(0) == K, "W rows must equal dy cols");
+  const bool use_wt = Wt && Wt->defined();
+  if (use_wt) {   // the transposed copy replaces W as the B operand (NT instantiation)
+    chk_mat(*Wt, "Wt", at::kBFloat16);
+    TORCH_CHECK(Wt->size(0) == N && Wt->size(1) == K, "Wt must be W^T [N, K]");
+    TORCH_CHECK(!f32 && !accumulate, "the transposed-weight path writes bf16");
+    TORCH_CHECK(ld2(*Wt) % 8 == 0 && ((uintptr_t)Wt->data_ptr() & 15) == 0, "Wt rows 16-B");
+  }
   TORCH_CHECK(dx.size(0) == M && dx.size(1) == N, "dx shape");
   TORCH_CHECK(K % 32 == 0 && N % 8 == 0, "K % 32 and N % 8 required");
   const void* hp = nullptr;
@@ -103,8 +111,21 @@ void gemm_nn(const at::Tensor& dy, const at::Tensor& W, const c10::optional<at::
     bits = 1;
   }
   TORCH_CHECK(!accumulate || f32, "accumulate needs an fp32 output");
+  if (use_wt) {
+    nf_launch_gemm256_nt_dgrad(dy.data_ptr(), ld2(dy), Wt->data_ptr(), ld2(*Wt), hp, ldh, bits,
+                               dx.data_ptr(), ld2(dx), M, N, K, cur_stream());
+    return;
+  }
   nf_launch_gemm_nn(dy.data_ptr(), ld2(dy), W.data_ptr(), ld2(W), hp, ldh, dx.data_ptr(), ld2(dx),
                     f32, accumulate, M, N, K, cur_stream(), bits);
+}
+
+// batched bf16 transposes: desc = int64 [n, 5] device table of (src, dst, rows | cols << 32,
+// lds | ldd << 32, tile0) as written by ops.layout.TransposePlan
+void transpose_bf16_batched(const at::Tensor& desc, int64_t n, int64_t tiles) {
+  TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == at::kLong && desc.is_contiguous() &&
+                  desc.numel() >= 5 * n, "desc: int64 GPU [n, 5]");
+  nf_launch_transpose_bf16_batched(desc.data_ptr(), (int)n, (int)tiles, cur_stream());
 }
 
 // dW = dy^T x (fp32), db = colsum(dy) (fp32): dy [K,M], x [K,N] bf16
@@ -292,11 +313,17 @@ void gemm_nt_cpl(const at::Tensor& h, const at::Tensor& W, const c10::optional<a
 // backward of coupling layer l-1: dst = [dS_hat | dT | 0] (bf16), gx = gy e^s (fp32).
 void gemm_nn_cpl(const at::Tensor& dy, const at::Tensor& W, const at::Tensor& G,
                  const at::Tensor& s_hat, const at::Tensor& x, const at::Tensor& dst,
-                 const at::Tensor& gx, double scale, double c) {
+                 const at::Tensor& gx, double scale, double c, const c10::optional<at::Tensor>& Wt) {
   chk_mat(dy, "dy", at::kBFloat16);
   chk_mat(W, "W", at::kBFloat16);
   const int M = dy.size(0), K = dy.size(1), N = W.size(1);
   TORCH_CHECK(W.size(0) == K, "W rows must equal dy cols");
+  const bool use_wt = Wt && Wt->defined();
+  if (use_wt) {
+    chk_mat(*Wt, "Wt", at::kBFloat16);
+    TORCH_CHECK(Wt->size(0) == N && Wt->size(1) == K, "Wt must be W^T [N, K]");
+    TORCH_CHECK(ld2(*Wt) % 8 == 0 && ((uintptr_t)Wt->data_ptr() & 15) == 0, "Wt rows 16-B");
+  }
   TORCH_CHECK(K % 32 == 0 && N % 8 == 0, "K % 32 and N % 8 required");
   for (const at::Tensor* t : {&G, &s_hat, &x, &dst, &gx})
     TORCH_CHECK(t->is_cuda() && t->dim() == 2 && t->stride(1) == 1 && t->size(0) == M,
@@ -308,10 +335,12 @@ void gemm_nn_cpl(const at::Tensor& dy, const at::Tensor& W, const at::Tensor& G,
   TORCH_CHECK(s_hat.scalar_type() == at::kBFloat16 && s_hat.size(1) >= Dh, "s_hat: bf16 [M, >= Dh]");
   TORCH_CHECK(dst.scalar_type() == at::kBFloat16 && dst.size(1) >= 2 * Dh && dst.size(1) <= Dh + N,
               "dst: bf16 [M, 2 Dh .. Dh + N]");
-  nf_launch_gemm256_nn_cpl(dy.data_ptr(), ld2(dy), W.data_ptr(), ld2(W), G.data_ptr<float>(),
+  nf_launch_gemm256_nn_cpl(dy.data_ptr(), ld2(dy), use_wt ? Wt->data_ptr() : W.data_ptr(),
+                           use_wt ? ld2(*Wt) : ld2(W), G.data_ptr<float>(),
                            ld2(G), M, N, K, s_hat.data_ptr(), ld2(s_hat), x.data_ptr<float>(),
                            ld2(x), dst.data_ptr(), ld2(dst), (int)dst.size(1),
-                           gx.data_ptr<float>(), ld2(gx), Dh, (float)scale, (float)c, cur_stream());
+                           gx.data_ptr<float>(), ld2(gx), Dh, (float)scale, (float)c, cur_stream(),
+                           use_wt ? 1 : 0);
 }
 
 // all `layers` weights of one kind (rows_per x C each, layer_stride elements apart in the flat
@@ -623,12 +652,13 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("masked_gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, Tensor krange, bool accumulate=False, Tensor? krange256=None) -> ()");
   m.def("masked_gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db, Tensor skip) -> ()");
   m.def("gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu, Tensor(b!)? mask=None) -> ()");
-  m.def("gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, bool accumulate, Tensor? hbits=None) -> ()");
+  m.def("gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, bool accumulate, Tensor? hbits=None, Tensor? Wt=None) -> ()");
+  m.def("transpose_bf16_batched(Tensor desc, int n, int tiles) -> ()");
   m.def("gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db) -> ()");
   m.def("gemm_tn_group(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, Tensor?[] skip, Tensor?[] cmask) -> ()");
   m.def("gemm_tn_multi(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles, Tensor?[] tiles, Tensor?[] cmask) -> ()");
   m.def("gemm_nt_cpl(Tensor h, Tensor W, Tensor? b, Tensor(a!) st, Tensor x, Tensor(b!) y, Tensor(c!)? yb, Tensor(d!) ldjp, bool ldj_init, float scale) -> ()");
-  m.def("gemm_nn_cpl(Tensor dy, Tensor W, Tensor G, Tensor s_hat, Tensor x, Tensor(a!) dst, Tensor(b!) gx, float scale, float c) -> ()");
+  m.def("gemm_nn_cpl(Tensor dy, Tensor W, Tensor G, Tensor s_hat, Tensor x, Tensor(a!) dst, Tensor(b!) gx, float scale, float c, Tensor? Wt=None) -> ()");
   m.def("fp8_quant_rows_strided(Tensor x, int layer_stride, int rows_per, int layers, int C, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("maf_fwd(Tensor x, Tensor o, float bound, Tensor(a!) u, Tensor(b!)? ubf, Tensor(c!)? uq, Tensor? amax_prev, Tensor(d!)? scale, Tensor(e!)? amax_cur, Tensor(f!) ldj, bool ldj_init) -> ()");
   m.def("iaf_gate_fwd(Tensor o, Tensor z, float gate_bias, Tensor(a!) y, Tensor(b!) ldj) -> ()");
@@ -642,6 +672,7 @@ TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
   m.impl("masked_gemm_tn", &masked_gemm_tn);
   m.impl("gemm_nt", &gemm_nt);
   m.impl("gemm_nn", &gemm_nn);
+  m.impl("transpose_bf16_batched", &transpose_bf16_batched);
   m.impl("gemm_tn", &gemm_tn);
   m.impl("gemm_tn_group", &gemm_tn_group);
   m.impl("gemm_tn_multi", &gemm_tn_multi);

@@ -89,6 +89,13 @@ void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, co
                           int N, int K, hipStream_t stream, int aux_is_bits = 0,
                           const int* krange = nullptr, int krange_segs = 1);
 void nf_gemm256_set_depth(int d);
+// input gradient with W given transposed (Wt [N][K]): NT instantiation, bf16 (ReLU-mask) epilogue
+void nf_launch_gemm256_nt_dgrad(const void* dy, long lddy, const void* Wt, long ldwt,
+                                const void* aux, long ld_aux, int aux_is_bits, void* dx,
+                                long lddx, int M, int N, int K, hipStream_t stream);
+// layout.hip: batched bf16 transposes (TrDesc table on the device)
+void nf_launch_transpose_bf16_batched(const void* desc, int n, int total_tiles,
+                                      hipStream_t stream);
 // last conditioner product of coupling layer l with its coupling forward fused (EPI_CPL_FWD)
 void nf_launch_gemm256_nt_cpl(const void* h, long ldh, const void* W, long ldw, int w_rows,
                               const void* bias, void* st, long ld_st, int M, int K, int Dh,
@@ -101,7 +108,7 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
                               long ldg, int M, int N, int K, const void* s_hat, long ld_s,
                               const float* x, long ld_x, void* dst, long ld_dst, int dst_pad,
                               float* gx, long ld_gx, int Dh, float scale, float c,
-                              hipStream_t stream);
+                              hipStream_t stream, int w_kmajor = 0);
 int nf_launch_gemm256_tn_partials(const void* dy, long lddy, const void* x, long ldx, float* C,
                                   long ldc, long slab_stride, float* dbias, int M, int N, int K,
                                   int splits, hipStream_t stream);

@@ -648,6 +648,24 @@ void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, co
   }
 }
 
+// Input gradient dx[M][N] = dy[M][K] W[K][N] with W given transposed (Wt [N][K], k-major):
+// the NT instantiation (b128 fragment reads of both operands) with the bf16 ReLU-mask (aux =
+// activation or bitmask) or plain bf16 epilogue.
+void nf_launch_gemm256_nt_dgrad(const void* dy, long lddy, const void* Wt, long ldwt,
+                                const void* aux, long ld_aux, int aux_is_bits, void* dx,
+                                long lddx, int M, int N, int K, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  GemmArgs a{};
+  a.A = (const nf::bf16_t*)dy; a.lda = lddy;
+  a.B = (const nf::bf16_t*)Wt; a.ldb = ldwt;
+  a.C = dx; a.ldc = lddx;
+  a.aux = (const nf::bf16_t*)aux; a.ld_aux = ld_aux;
+  a.aux_bits = aux_is_bits;
+  a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + 63) / 64) * 64;
+  if (aux) g256::launch<true, true, EPI_BF16_RELUMASK>(a, 1, stream);
+  else g256::launch<true, true, EPI_BF16>(a, 1, stream);
+}
+
 // Last conditioner product of coupling layer l with its coupling forward fused (EPI_CPL_FWD):
 // W [2 Dh (+pad) rows][K], x/y fp32 [M][Dh], yb bf16 [M][>= yb_width] (or null), st bf16 [M][>= Dh]
 // (s_hat written), ldjp fp32 [ceil(Dh/128)][M] per-column-tile partial sums of s.
@@ -687,7 +705,7 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
                               long ldg, int M, int N, int K, const void* s_hat, long ld_s,
                               const float* x, long ld_x, void* dst, long ld_dst, int dst_pad,
                               float* gx, long ld_gx, int Dh, float scale, float c,
-                              hipStream_t stream) {
+                              hipStream_t stream, int w_kmajor) {
   if (M <= 0 || N <= 0) return;
   GemmArgs a{};
   a.A = (const nf::bf16_t*)dy; a.lda = lddy;
@@ -706,7 +724,8 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
                     "4-element aligned rows and the staged epilogue\n");
     abort();
   }
-  g256::launch<true, false, EPI_CPL_BWD>(a, 1, stream);
+  if (w_kmajor) g256::launch<true, true, EPI_CPL_BWD>(a, 1, stream);   // W given as Wt [N][K]
+  else g256::launch<true, false, EPI_CPL_BWD>(a, 1, stream);
 }
 
 // dW[M][N] (+ db[M]) = split-K partials of dy[K][M]^T x[K][N] written to `work` slabs (or

@@ -10,7 +10,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "vi_normflows_amd", "_native", "libvinf_hip.so")
 
-OPS = ["gemm_nt", "gemm_nn", "gemm_tn", "gemm_tn_group", "gemm_tn_multi", "gemm_nn_cpl", "gemm_nt_cpl", "iaf_gate_fwd", "iaf_gate_bwd",
+OPS = ["gemm_nt", "gemm_nn", "gemm_tn", "gemm_tn_group", "gemm_tn_multi", "gemm_nn_cpl", "gemm_nt_cpl", "iaf_gate_fwd", "iaf_gate_bwd", "transpose_bf16_batched",
        "masked_gemm_nt", "masked_gemm_nn", "masked_gemm_tn", "gemm_fp8_nt", "coupling_fwd",
        "coupling_bwd", "flat_optimizer", "sumsq_guard", "cu_hold", "maf_fwd", "maf_bwd"]
 

@@ -81,6 +81,10 @@ def main():
                 y = torch.empty(M, N, device=dev, dtype=bf)
                 mine = lambda: ops.gemm_nn(dy, W, h, y, False)
                 ref = lambda: y.copy_(torch.mm(dy, W) * (h > 0))
+            elif kind == "nnbf":      # plain bf16 output (layout A/B against "ntplain")
+                y = torch.empty(M, N, device=dev, dtype=bf)
+                mine = lambda: ops.gemm_nn(dy, W, None, y, False)
+                ref = lambda: torch.mm(dy, W, out=y)
             else:
                 y = torch.zeros(M, N, device=dev)
                 mine = lambda: ops.gemm_nn(dy, W, None, y, True)

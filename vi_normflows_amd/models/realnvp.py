@@ -195,6 +195,11 @@ class RealNVPVI:
         self.defer_stream = None
         if self.wgrad_defer and os.environ.get("VINF_WGRAD_DEFER_STREAM", "0") == "1":
             self.defer_stream = torch.cuda.Stream(device=dev)
+        # input gradients dx = dy W as NT products against a per-step copy of W^T (one batched
+        # transpose launch, ops.layout): both operands k-major, 5-7 % faster than the NN form
+        self.wt_dgrad = self.wgrad_defer and os.environ.get("VINF_DGRAD_NT", "1") != "0"
+        self.WT = None
+        self._wt_plan = None
         self._wplan = None
         if self.wgrad_defer:
             self.dstL = torch.empty(L, B, Np, dtype=self.cdt, device=dev)
@@ -380,6 +385,30 @@ class RealNVPVI:
             self._wplan = plan
         return self._wplan
 
+    def _weights_t(self):
+        """Refresh W^T of every conditioner weight (bf16) and return them as WT[l][i]."""
+        if self._wt_plan is None:
+            from ..ops.layout import TransposePlan
+
+            cfg, P = self.cfg, self.params
+            Ws = [[P.c(f"l{l}.W{i}") for i in range(cfg.n_hidden + 1)]
+                  for l in range(cfg.n_layers)]
+            buf = torch.empty(sum(W.numel() for row in Ws for W in row), dtype=self.cdt,
+                              device=self.device)
+            self.WT, pairs, off = [], [], 0
+            for row in Ws:
+                out = []
+                for W in row:
+                    o, i = W.shape
+                    Wt = buf[off:off + o * i].view(i, o)
+                    off += o * i
+                    out.append(Wt)
+                    pairs.append((W, Wt))
+                self.WT.append(out)
+            self._wt_plan = TransposePlan(pairs)
+        self._wt_plan.run()
+        return self.WT
+
     def _backward_deferred(self):
         """Backward with the weight gradients batched across layers (see ``wgrad_defer``):
         the input-gradient chain runs layer by layer; whenever a CU-count worth of weight-
@@ -412,6 +441,7 @@ class RealNVPVI:
                                self.G[l], c=c, scale=cfg.scale_bound, gx_accumulate=False,
                                s_is_hat=True)
 
+        WT = self._weights_t() if self.wt_dgrad else None
         if fuse:
             cpl_bwd(L - 1)
         for l in range(L - 1, -1, -1):
@@ -422,7 +452,8 @@ class RealNVPVI:
                 if i > 0:
                     nd = self.dHL[l, i - 1]
                     gemm.linear_dgrad(d, P.c(f"l{l}.W{i}"), nd, relu_of=self.Act[l, i - 1],
-                                      relu_bits=None if self.Mk is None else self.Mk[l, i - 1])
+                                      relu_bits=None if self.Mk is None else self.Mk[l, i - 1],
+                                      Wt=None if WT is None else WT[l][i])
                     d = nd
                 elif fuse and l > 0:
                     # dL/dh_{l+1} = G[l+1] + d W0 is finished and consumed by layer l-1's
@@ -430,7 +461,8 @@ class RealNVPVI:
                     gemm.linear_dgrad_coupling(d, P.c(f"l{l}.W0"), self._G[l + 1],
                                                s_hat=self.ST[l - 1][:, :cfg.half],
                                                x=self.h(l - 1), dst=self.dstL[l - 1],
-                                               gx=self.G[l - 1], scale=cfg.scale_bound, c=c)
+                                               gx=self.G[l - 1], scale=cfg.scale_bound, c=c,
+                                               Wt=None if WT is None else WT[l][0])
                 else:
                     gemm.linear_dgrad(d, P.c(f"l{l}.W0"), self._G[l + 1], accumulate=True)
             wgrad_ready(l)

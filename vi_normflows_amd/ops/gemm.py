@@ -61,17 +61,19 @@ def linear_fwd(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, out: to
 
 def linear_dgrad(dy: torch.Tensor, W: torch.Tensor, out: torch.Tensor,
                  relu_of: torch.Tensor | None = None, accumulate: bool = False,
-                 relu_bits: torch.Tensor | None = None) -> torch.Tensor:
+                 relu_bits: torch.Tensor | None = None,
+                 Wt: torch.Tensor | None = None) -> torch.Tensor:
     """out (+)= (dy @ W) * 1(relu_of > 0). ``out`` may be fp32 while dy/W are bf16.
     ``relu_bits`` (MFMA path): the bitmask :func:`linear_fwd` wrote for ``relu_of``, read
-    instead of the bf16 activation; the other paths use ``relu_of``."""
+    instead of the bf16 activation; the other paths use ``relu_of``. ``Wt`` (MFMA path, bf16
+    output): a current copy of W^T, which runs the product as NT (both operands k-major)."""
     if _mfma_ok(dy) and dy.is_cuda:
         from ._ext import native
 
         if relu_bits is not None:
-            native().gemm_nn(dy, W, None, out, bool(accumulate), relu_bits)
+            native().gemm_nn(dy, W, None, out, bool(accumulate), relu_bits, Wt)
         else:
-            native().gemm_nn(dy, W, relu_of, out, bool(accumulate))
+            native().gemm_nn(dy, W, relu_of, out, bool(accumulate), None, Wt)
         return out
     if dy.is_cuda and out.dtype != dy.dtype:
         r = torch.mm(dy, W, out_dtype=out.dtype)
@@ -127,7 +129,7 @@ def linear_fwd_coupling(h: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None
 
 def linear_dgrad_coupling(dy: torch.Tensor, W: torch.Tensor, G: torch.Tensor, s_hat: torch.Tensor,
                           x: torch.Tensor, dst: torch.Tensor, gx: torch.Tensor, scale: float,
-                          c: float) -> None:
+                          c: float, Wt: torch.Tensor | None = None) -> None:
     """Input gradient of a coupling conditioner fused with the PREVIOUS coupling layer's
     backward (MFMA path: one GEMM whose epilogue does both, ``EPI_CPL_BWD``):
 
@@ -139,7 +141,7 @@ def linear_dgrad_coupling(dy: torch.Tensor, W: torch.Tensor, G: torch.Tensor, s_
     if _mfma_ok(dy) and dy.is_cuda:
         from ._ext import native
 
-        native().gemm_nn_cpl(dy, W, G, s_hat, x, dst, gx, float(scale), float(c))
+        native().gemm_nn_cpl(dy, W, G, s_hat, x, dst, gx, float(scale), float(c), Wt)
         return
     Dh = x.shape[1]
     gy = (G.float() + (dy.float() @ W.float()))[:, :Dh]
