@@ -485,7 +485,7 @@ void masked_gemm_nt(const at::Tensor& x, const at::Tensor& W, const c10::optiona
 
 void masked_gemm_nn(const at::Tensor& dy, const at::Tensor& W, const c10::optional<at::Tensor>& h,
                     const at::Tensor& dx, const at::Tensor& krange, bool accumulate,
-                    const c10::optional<at::Tensor>& krange256) {
+                    const c10::optional<at::Tensor>& krange256, const c10::optional<at::Tensor>& Wt) {
   chk_mat(dy, "dy", at::kBFloat16);
   chk_mat(W, "W", at::kBFloat16);
   const bool f32 = dx.scalar_type() == at::kFloat;
@@ -513,9 +513,18 @@ void masked_gemm_nn(const at::Tensor& dy, const at::Tensor& W, const c10::option
                 "ReLU-mask operand rows must be 16-B aligned for the 256x256 kernel");
     k256 = krange256->data_ptr<int>();
   }
+  const void* wtp = nullptr;
+  long ldwt = 0;
+  if (Wt && Wt->defined()) {   // (W*M)^T [N, K], used by the 256x256 path
+    chk_mat(*Wt, "Wt", at::kBFloat16);
+    TORCH_CHECK(Wt->size(0) == N && Wt->size(1) == K, "Wt must be W^T [N, K]");
+    TORCH_CHECK(ld2(*Wt) % 8 == 0 && ((uintptr_t)Wt->data_ptr() & 15) == 0, "Wt rows 16-B");
+    wtp = Wt->data_ptr();
+    ldwt = ld2(*Wt);
+  }
   nf_launch_gemm_nn_masked(dy.data_ptr(), ld2(dy), W.data_ptr(), ld2(W), hp, ldh, dx.data_ptr(),
                            ld2(dx), f32, accumulate, M, N, K, krange.data_ptr<int>(), cur_stream(),
-                           k256, segs);
+                           k256, segs, wtp, ldwt);
 }
 
 void masked_gemm_tn(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dW,
@@ -649,7 +658,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("fp8_quant_tensor(Tensor x, Tensor(a!) q, Tensor amax_prev, Tensor(b!) scale, Tensor(c!) amax_cur) -> ()");
   m.def("gemm_fp8_nt(Tensor xq, Tensor sx, Tensor wq, Tensor sw, Tensor? b, Tensor(a!) y, int relu, Tensor? krange, Tensor(b!)? yq=None, Tensor? q_amax_prev=None, Tensor(c!)? q_scale=None, Tensor(d!)? q_amax_cur=None, Tensor? krange256=None) -> ()");
   m.def("masked_gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu, Tensor krange, Tensor? krange256=None) -> ()");
-  m.def("masked_gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, Tensor krange, bool accumulate=False, Tensor? krange256=None) -> ()");
+  m.def("masked_gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, Tensor krange, bool accumulate=False, Tensor? krange256=None, Tensor? Wt=None) -> ()");
   m.def("masked_gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db, Tensor skip) -> ()");
   m.def("gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu, Tensor(b!)? mask=None) -> ()");
   m.def("gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, bool accumulate, Tensor? hbits=None, Tensor? Wt=None) -> ()");

@@ -87,7 +87,7 @@ void nf_launch_gemm256_nt(const void* x, long ldx, const void* W, long ldw, cons
 void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                           long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
                           int N, int K, hipStream_t stream, int aux_is_bits = 0,
-                          const int* krange = nullptr, int krange_segs = 1);
+                          const int* krange = nullptr, int krange_segs = 1, int w_kmajor = 0);
 void nf_gemm256_set_depth(int d);
 // input gradient with W given transposed (Wt [N][K]): NT instantiation, bf16 (ReLU-mask) epilogue
 void nf_launch_gemm256_nt_dgrad(const void* dy, long lddy, const void* Wt, long ldwt,
@@ -163,7 +163,8 @@ void nf_launch_gemm_nt_masked(const void* x, long ldx, const void* W, long ldw, 
 void nf_launch_gemm_nn_masked(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                               long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
                               int N, int K, const int* krange, hipStream_t stream,
-                              const int* krange256 = nullptr, int krange256_segs = 1);
+                              const int* krange256 = nullptr, int krange256_segs = 1,
+                              const void* Wt = nullptr, long ldwt = 0);
 void nf_launch_gemm_tn_masked(const void* dy, long lddy, const void* x, long ldx, float* dW,
                               long lddw, float* db, int M, int N, int K, int splits, float* work,
                               const unsigned char* skip, hipStream_t stream);

@@ -546,11 +546,12 @@ void nf_launch_gemm_nt_masked(const void* x, long ldx, const void* W, long ldw, 
 void nf_launch_gemm_nn_masked(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                               long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
                               int N, int K, const int* krange, hipStream_t stream,
-                              const int* krange256, int krange256_segs) {
+                              const int* krange256, int krange256_segs, const void* Wt,
+                              long ldwt) {
   if (M <= 0 || N <= 0) return;
-  if (krange256 && use_256(M, N, K)) {
-    nf_launch_gemm256_nn(dy, lddy, W, ldw, aux, ld_aux, dx, lddx, dx_is_f32, accumulate, M, N, K,
-                         stream, 0, krange256, krange256_segs);
+  if (krange256 && use_256(M, N, K)) {   // with Wt = (W*M)^T [N][K]: the NT instantiation
+    nf_launch_gemm256_nn(dy, lddy, Wt ? Wt : W, Wt ? ldwt : ldw, aux, ld_aux, dx, lddx, dx_is_f32,
+                         accumulate, M, N, K, stream, 0, krange256, krange256_segs, Wt ? 1 : 0);
     return;
   }
   GemmArgs a{};

@@ -627,7 +627,7 @@ void nf_launch_gemm256_nt(const void* x, long ldx, const void* W, long ldw, cons
 void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                           long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
                           int N, int K, hipStream_t stream, int aux_is_bits, const int* krange,
-                          int krange_segs) {
+                          int krange_segs, int w_kmajor) {
   if (M <= 0 || N <= 0) return;
   GemmArgs a{};
   a.krange = krange;
@@ -638,6 +638,17 @@ void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, co
   a.aux = (const nf::bf16_t*)aux; a.ld_aux = ld_aux;
   a.aux_bits = aux_is_bits;
   a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + 63) / 64) * 64;
+  if (w_kmajor) {   // W given as Wt [N][K]: the NT instantiation (k-major fragment reads)
+    if (dx_is_f32) {
+      if (accumulate) g256::launch<true, true, EPI_F32_ACC>(a, 1, stream);
+      else g256::launch<true, true, EPI_F32>(a, 1, stream);
+    } else if (aux) {
+      g256::launch<true, true, EPI_BF16_RELUMASK>(a, 1, stream);
+    } else {
+      g256::launch<true, true, EPI_BF16>(a, 1, stream);
+    }
+    return;
+  }
   if (dx_is_f32) {
     if (accumulate) g256::launch<true, false, EPI_F32_ACC>(a, 1, stream);
     else g256::launch<true, false, EPI_F32>(a, 1, stream);

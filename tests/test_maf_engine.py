@@ -130,3 +130,22 @@ def test_engine_deferred_masked_wgrad_and_256_kernels(gpu, tile, monkeypatch):
         mk = a._mask(l)
         assert (a.params.g(f"l{l}.W1")[mk["M1"] == 0] == 0).all()
         assert (a.params.g(f"l{l}.W2")[mk["M2"] == 0] == 0).all()
+
+
+@pytest.mark.gpu
+def test_engine_masked_dgrad_nt_matches_nn(gpu, monkeypatch):
+    """Masked input gradients against (W*M)^T (NT, VINF_DGRAD_NT=1) == the NN path."""
+    from vi_normflows_amd.models.maf_engine import MAFEngine, MAFEngineConfig
+
+    cfg = MAFEngineConfig(dim=256, hidden=512, n_layers=3, precision="bf16")
+    a = MAFEngine(cfg, batch=512, device=gpu, seed=4)
+    monkeypatch.setenv("VINF_DGRAD_NT", "0")
+    b = MAFEngine(cfg, batch=512, device=gpu, seed=4)
+    assert a.wt_dgrad and not b.wt_dgrad
+    for e in (a, b):
+        e.train_step()
+        e.train_step()
+    torch.cuda.synchronize()
+    ga, gb = a.params.grad, b.params.grad
+    assert torch.isfinite(ga).all()
+    assert ((ga - gb).norm() / gb.norm()).item() < 1e-5

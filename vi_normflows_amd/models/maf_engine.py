@@ -154,6 +154,10 @@ class MAFEngine:
 
         self.wgrad_defer = dev.type == "cuda" and os.environ.get("VINF_WGRAD_DEFER", "1") != "0"
         self._wplan = None
+        # masked input gradients as NT products against a per-step (W*M)^T copy (ops.layout)
+        self.wt_dgrad = self.wgrad_defer and os.environ.get("VINF_DGRAD_NT", "1") != "0"
+        self.WT = None
+        self._wt_plan = None
         if self.wgrad_defer:
             self.dOL = torch.empty(L, B, 2 * D, dtype=self.cdt, device=dev)
             self.dHL = torch.empty(L, B, H, dtype=self.cdt, device=dev)
@@ -309,6 +313,30 @@ class MAFEngine:
             self._wplan = plan
         return self._wplan
 
+    def _weights_t(self):
+        """Refresh (W*M)^T of both masked weights of every layer (bf16, one launch): the
+        masked input-gradient GEMMs then run NT (see models/realnvp.py ``wt_dgrad``)."""
+        if self._wt_plan is None:
+            from ..ops.layout import TransposePlan
+
+            P = self.params
+            Ws = [[P.c(f"l{l}.W1"), P.c(f"l{l}.W2")] for l in range(self.cfg.n_layers)]
+            buf = torch.empty(sum(W.numel() for row in Ws for W in row), dtype=torch.bfloat16,
+                              device=self.device)
+            self.WT, pairs, off = [], [], 0
+            for row in Ws:
+                out = []
+                for W in row:
+                    o, i = W.shape
+                    Wt = buf[off:off + o * i].view(i, o)
+                    off += o * i
+                    out.append(Wt)
+                    pairs.append((W, Wt))
+                self.WT.append(out)
+            self._wt_plan = TransposePlan(pairs)
+        self._wt_plan.run()
+        return self.WT
+
     def _backward_deferred(self):
         """Input-gradient chain layer by layer; the masked weight gradients of all layers
         in CU-count chunks of whole tiles (ops.gemm.WgradScheduler), the DP hook firing per
@@ -320,15 +348,16 @@ class MAFEngine:
         plan = self._wgrad_plan()
         sched = gemm.WgradScheduler(plan, plan.unit_ends, self._wchunk, self.unit_ready_hook)
         gu, gx = self.gU, self.gX
+        WT = self._weights_t() if self.wt_dgrad else None
         for k, l in enumerate(range(L - 1, -1, -1)):
             mk = self._mask(l)
             dO, dH = self.dOL[l], self.dHL[l]
             fused.maf_bwd(gu, self.X[l + 1], self.O[l], dO, gx, bound=cfg.alpha_bound,
                           c_ldj=1.0 / self.B)
             native().masked_gemm_nn(dO, P.c(f"l{l}.W2"), self.Hbf[l], dH, mk["P2"].bwd, False,
-                                    mk["P2"].bwd256)
+                                    mk["P2"].bwd256, None if WT is None else WT[l][1])
             native().masked_gemm_nn(dH, P.c(f"l{l}.W1"), None, gx, mk["P1"].bwd, True,
-                                    mk["P1"].bwd256)
+                                    mk["P1"].bwd256, None if WT is None else WT[l][0])
             sched.ready(plan.unit_ends[k][1], final=(l == 0))
             gu, gx = gx, gu
 
