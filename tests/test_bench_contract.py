@@ -1,0 +1,64 @@
+"""bench.py driver contract on the CPU (gloo): one JSON line from rank 0 with the whole-job
+aggregate, the max step time over ranks, weak-scaling metadata; also under
+``torch.distributed.run`` with 2 ranks (the launcher the driver uses for N > 1)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--cpu", "--steps", "2", "--warmup", "1", "--batch", "64", "--layers", "2",
+         "--dim", "64", "--hidden", "64"]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _json_lines(out: str):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def _check(rec, n):
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in rec, k
+    assert rec["n_gpus"] == n and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["higher_is_better"] is True and rec["scaling"] == "weak"
+    assert rec["config"]["global_batch"] == 64 * n
+    assert rec["config"]["parallelism"] == f"dp{n}"
+    assert rec["value"] > 0 and rec["ms_per_step"] > 0
+    # value = global batch * steps / max-over-ranks time
+    assert abs(rec["value"] * rec["ms_per_step"] / 1000.0 - 64 * n) / (64 * n) < 1e-3
+
+
+def _env():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    return env
+
+
+def test_bench_single_process_cpu():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *SMALL], cwd=ROOT,
+                       env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1
+    _check(recs[0], 1)
+
+
+def test_bench_torchrun_two_ranks_cpu():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", *SMALL]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout      # rank 0 only
+    _check(recs[0], 2)
