@@ -15,6 +15,8 @@ from pathlib import Path
 import torch
 
 _LIB_PATH = Path(__file__).resolve().parent.parent / "_native" / "libvinf_hip.so"
+if os.environ.get("VINF_NATIVE_LIB"):   # a variant build (kernel A/B experiments)
+    _LIB_PATH = Path(os.environ["VINF_NATIVE_LIB"]).resolve()
 _lock = threading.Lock()
 _loaded = False
 _load_error: Exception | None = None
