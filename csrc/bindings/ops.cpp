@@ -209,6 +209,34 @@ void reparam_sample(const c10::optional<at::Tensor>& mu, const c10::optional<at:
                            cur_stream());
 }
 
+// Diagonal-base reparameterisation backward; dL/dz0 = [g_lo | g_hi] (two strided views).
+void reparam_grad(const at::Tensor& g_lo, const at::Tensor& g_hi, const at::Tensor& eps,
+                  const at::Tensor& logvar, const at::Tensor& partial, const at::Tensor& gmu,
+                  const at::Tensor& glv) {
+  check_2d(g_lo, "g_lo");
+  check_2d(g_hi, "g_hi");
+  check_2d(eps, "eps");
+  for (const at::Tensor* t : {&g_lo, &g_hi, &eps, &logvar, &partial, &gmu, &glv})
+    check_dtype(*t, at::kFloat, "reparam_grad operand");
+  const int B = eps.size(0), D = eps.size(1), Dl = g_lo.size(1);
+  TORCH_CHECK(g_lo.size(0) == B && g_hi.size(0) == B && Dl + g_hi.size(1) == D, "reparam_grad shapes");
+  TORCH_CHECK(g_lo.stride(1) == 1 && g_hi.stride(1) == 1 && eps.stride(1) == 1, "reparam_grad: unit column stride");
+  // one float4 column group per thread of a 256-thread block
+  TORCH_CHECK(D % 4 == 0 && Dl % 4 == 0 && D <= 1024, "reparam_grad: D, Dl multiples of 4, D <= 1024");
+  const long ldlo = ld_of(g_lo), ldhi = ld_of(g_hi), lde = ld_of(eps);
+  TORCH_CHECK(ldlo % 4 == 0 && ldhi % 4 == 0 && lde % 4 == 0, "reparam_grad: 16-B aligned rows");
+  for (const at::Tensor* t : {&g_lo, &g_hi, &eps, &partial})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "reparam_grad: 16-B aligned base");
+  TORCH_CHECK(logvar.numel() == D && gmu.numel() == D && glv.numel() == D && logvar.is_contiguous() &&
+              gmu.is_contiguous() && glv.is_contiguous(), "reparam_grad: (D,) vectors");
+  TORCH_CHECK(partial.is_contiguous() && partial.numel() >= 2L * D, "reparam_grad: partial");
+  const int npartial = (int)std::min<long>(partial.numel() / (2L * D), (long)B);
+  nf_launch_reparam_grad(g_lo.data_ptr<float>(), ldlo, g_hi.data_ptr<float>(), ldhi,
+                         eps.data_ptr<float>(), lde, logvar.data_ptr<float>(),
+                         partial.data_ptr<float>(), std::max(npartial, 1), gmu.data_ptr<float>(),
+                         glv.data_ptr<float>(), B, D, Dl, cur_stream());
+}
+
 void normal_fill(const at::Tensor& out, int64_t seed, const c10::optional<at::Tensor>& offset,
                  int64_t offset_host, int64_t stream_id) {
   check_cuda(out, "out");
@@ -276,6 +304,8 @@ TORCH_LIBRARY(vinf, m) {
         "int stream_id, Tensor(a!) z, Tensor(b!)? eps, Tensor(c!)? zbf, int nbf, "
         "Tensor(d!)? logq0) -> ()");
   m.def("normal_fill(Tensor(a!) out, int seed, Tensor? offset, int offset_host, int stream_id) -> ()");
+  m.def("reparam_grad(Tensor g_lo, Tensor g_hi, Tensor eps, Tensor logvar, Tensor(a!) partial, "
+        "Tensor(b!) gmu, Tensor(c!) glv) -> ()");
   m.def("flat_optimizer(int kind, Tensor(a!) p, Tensor g, Tensor(b!)? m, Tensor(c!)? v, "
         "Tensor(d!)? pbf, float lr, float b1, float b2, float eps, float wd, Tensor? step, "
         "float step_host, Tensor? gscale, float gscale_host, Tensor? skip) -> ()");
@@ -291,6 +321,7 @@ TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
   m.impl("bernoulli_logits", &bernoulli_logits);
   m.impl("reparam_sample", &reparam_sample);
   m.impl("normal_fill", &normal_fill);
+  m.impl("reparam_grad", &reparam_grad);
   m.impl("flat_optimizer", &flat_optimizer);
   m.impl("sumsq_guard", &sumsq_guard);
 }

@@ -36,6 +36,10 @@ void nf_launch_reparam_sample(const float* mu, const float* logvar, uint64_t see
                               long ldzb, int nbf, float* logq0, int B, int D, hipStream_t stream);
 void nf_launch_normal_fill(float* out, long n, uint64_t seed, const int64_t* offset_ptr,
                            int64_t offset_host, uint32_t stream_id, hipStream_t stream);
+void nf_launch_reparam_grad(const float* g_lo, long ldlo, const float* g_hi, long ldhi,
+                            const float* eps, long lde, const float* logvar, float* partial,
+                            int npartial, float* gmu, float* glv, int B, int D, int Dl,
+                            hipStream_t stream);
 
 // optim.hip
 void nf_launch_flat_optimizer(int kind, float* p, const float* g, float* m, float* v, void* pbf,

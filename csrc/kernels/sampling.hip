@@ -52,6 +52,65 @@ __global__ void __launch_bounds__(256) reparam_sample_kernel(
   if (lane == 0 && logq0) logq0[row] = -0.5f * (float)D * 1.8378770664093453f - 0.5f * slv - 0.5f * sq;
 }
 
+// Backward of z0 = mu + exp(logvar/2) * eps for the learnable diagonal base:
+//   gmu[c] = sum_b g[b,c],  glv[c] = 0.5 exp(lv[c]/2) sum_b g[b,c] eps[b,c] - 0.5
+// where dL/dz0 arrives as two strided column blocks (g_lo = columns [0, Dl), g_hi = [Dl, D)),
+// so no concatenated copy is materialised. Pass 1: each block owns a row slab and every
+// column (one float4 column group per thread) and writes its two column sums to its own
+// partial row; pass 2 sums the partial rows in a fixed order (bitwise deterministic).
+__global__ void __launch_bounds__(256) reparam_grad_partial_kernel(
+    const float* __restrict__ g_lo, long ldlo, const float* __restrict__ g_hi, long ldhi,
+    const float* __restrict__ eps, long lde, float* __restrict__ partial, int B, int D, int Dl,
+    int rows_per) {
+  const int q = threadIdx.x;  // float4 column group
+  if (4 * q >= D) return;
+  const int c = 4 * q;
+  const float* gp = c < Dl ? g_lo + c : g_hi + (c - Dl);
+  const long ldg = c < Dl ? ldlo : ldhi;
+  const long r0 = (long)blockIdx.x * rows_per;
+  const long r1 = min((long)B, r0 + rows_per);
+  float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
+  long r = r0;
+  for (; r + 4 <= r1; r += 4) {
+    float4 g[4], e[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      g[u] = *reinterpret_cast<const float4*>(gp + (r + u) * ldg);
+      e[u] = *reinterpret_cast<const float4*>(eps + (r + u) * lde + c);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s1.x += g[u].x; s1.y += g[u].y; s1.z += g[u].z; s1.w += g[u].w;
+      s2.x = fmaf(g[u].x, e[u].x, s2.x); s2.y = fmaf(g[u].y, e[u].y, s2.y);
+      s2.z = fmaf(g[u].z, e[u].z, s2.z); s2.w = fmaf(g[u].w, e[u].w, s2.w);
+    }
+  }
+  for (; r < r1; ++r) {
+    const float4 g = *reinterpret_cast<const float4*>(gp + r * ldg);
+    const float4 e = *reinterpret_cast<const float4*>(eps + r * lde + c);
+    s1.x += g.x; s1.y += g.y; s1.z += g.z; s1.w += g.w;
+    s2.x = fmaf(g.x, e.x, s2.x); s2.y = fmaf(g.y, e.y, s2.y);
+    s2.z = fmaf(g.z, e.z, s2.z); s2.w = fmaf(g.w, e.w, s2.w);
+  }
+  float* out = partial + (long)blockIdx.x * 2 * D;
+  *reinterpret_cast<float4*>(out + c) = s1;
+  *reinterpret_cast<float4*>(out + D + c) = s2;
+}
+
+__global__ void __launch_bounds__(256) reparam_grad_finalize_kernel(
+    const float* __restrict__ partial, int np, const float* __restrict__ logvar,
+    float* __restrict__ gmu, float* __restrict__ glv, int D) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= D) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int p = 0; p < np; ++p) {
+    s1 += partial[(long)p * 2 * D + c];
+    s2 += partial[(long)p * 2 * D + D + c];
+  }
+  gmu[c] = s1;
+  glv[c] = 0.5f * __expf(0.5f * logvar[c]) * s2 - 0.5f;
+}
+
 // Plain N(0,1) fill with the same counter scheme (used by MC estimators and tests).
 __global__ void __launch_bounds__(256) normal_fill_kernel(float* __restrict__ out, long n,
                                                            uint32_t seed_lo, uint32_t seed_hi,
@@ -108,5 +167,19 @@ void nf_launch_normal_fill(float* out, long n, uint64_t seed, const int64_t* off
   hipLaunchKernelGGL(normal_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, out, n,
                      (uint32_t)(seed & 0xffffffffu), (uint32_t)(seed >> 32), offset_ptr,
                      offset_host, stream_id);
+  NF_HIP_CHECK(hipGetLastError());
+}
+
+void nf_launch_reparam_grad(const float* g_lo, long ldlo, const float* g_hi, long ldhi,
+                            const float* eps, long lde, const float* logvar, float* partial,
+                            int npartial, float* gmu, float* glv, int B, int D, int Dl,
+                            hipStream_t stream) {
+  if (B <= 0 || D <= 0) return;
+  const int rows_per = (B + npartial - 1) / npartial;
+  const int np = (B + rows_per - 1) / rows_per;
+  hipLaunchKernelGGL(reparam_grad_partial_kernel, dim3(np), dim3(256), 0, stream, g_lo, ldlo,
+                     g_hi, ldhi, eps, lde, partial, B, D, Dl, rows_per);
+  hipLaunchKernelGGL(reparam_grad_finalize_kernel, dim3((D + 255) / 256), dim3(256), 0, stream,
+                     partial, np, logvar, gmu, glv, D);
   NF_HIP_CHECK(hipGetLastError());
 }

@@ -142,6 +142,31 @@ def test_reparam_sample_statistics_and_logq0(gpu):
     assert not torch.allclose(z, z2)
 
 
+@pytest.mark.parametrize("B,D,npart", [(65536, 784, 512), (1000, 64, 512), (37, 16, 8)])
+def test_reparam_grad_matches_fp32_reference(gpu, B, D, npart):
+    """Fused base backward vs plain fp32 torch on [G1 | G0] held as strided views of a padded
+    buffer (the engine's layout); bitwise repeatable."""
+    Dl = D // 2
+    pad = Dl + 8
+    torch.manual_seed(0)
+    Gbuf = torch.randn(2, B, pad, device=gpu)
+    g_lo, g_hi = Gbuf[1, :, :Dl], Gbuf[0, :, :D - Dl]
+    eps = torch.randn(B, D, device=gpu)
+    lv = torch.linspace(-1, 0.5, D, device=gpu)
+    part = torch.empty(npart * 2 * D, device=gpu)
+    gmu, glv = torch.empty(D, device=gpu), torch.empty(D, device=gpu)
+    torch.ops.vinf.reparam_grad(g_lo, g_hi, eps, lv, part, gmu, glv)
+    g = torch.cat([g_lo, g_hi], 1).double()
+    ref_mu = g.sum(0)
+    ref_lv = 0.5 * torch.exp(0.5 * lv.double()) * (g * eps.double()).sum(0) - 0.5
+    tol = 1e-5 * math.sqrt(B) + 1e-4
+    assert torch.allclose(gmu.double(), ref_mu, rtol=1e-5, atol=tol)
+    assert torch.allclose(glv.double(), ref_lv, rtol=1e-5, atol=tol)
+    gmu2, glv2 = torch.empty_like(gmu), torch.empty_like(glv)
+    torch.ops.vinf.reparam_grad(g_lo, g_hi, eps, lv, part, gmu2, glv2)
+    assert torch.equal(gmu, gmu2) and torch.equal(glv, glv2)
+
+
 def test_normal_fill(gpu):
     out = torch.empty(1_000_003, device=gpu)
     torch.ops.vinf.normal_fill(out, 7, None, 3, 0)

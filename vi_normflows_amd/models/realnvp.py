@@ -212,6 +212,11 @@ class RealNVPVI:
             self.wgrad_stream = torch.cuda.Stream(device=dev)
         self._G = torch.zeros(L + 2, B, Dp, dtype=f32, device=dev)   # dL/dh_i, 0-padded rows
         self.G = self._G[:, :, :Dh]
+        # per-slab column sums of the base backward (HIP path: float4 columns, <= 1024 wide)
+        self._rg_partial = None
+        if (dev.type == "cuda" and D % 4 == 0 and Dh % 4 == 0 and Dp % 4 == 0 and D <= 1024
+                and os.environ.get("VINF_REPARAM_GRAD", "1") == "1"):
+            self._rg_partial = torch.empty(512 * 2 * D, dtype=f32, device=dev)
         self.logq0 = torch.empty(B, dtype=f32, device=dev)
         self.ldj = torch.empty(B, dtype=f32, device=dev)
         self.logp = torch.empty(B, dtype=f32, device=dev)
@@ -532,6 +537,11 @@ class RealNVPVI:
             glv.zero_()
             return
         # z0 = [h_1 | h_0]: dL/dz0 = [G1 | G0]
+        if self._rg_partial is not None:
+            # one HIP pass over G1, G0, eps0 + a deterministic column finalize
+            fused.reparam_grad(self.G[1], self.G[0], self.eps0, P.p("base.logvar"),
+                               self._rg_partial, gmu, glv)
+            return
         g0 = torch.cat([self.G[1], self.G[0]], 1)
         torch.sum(g0, 0, out=gmu)
         sig = torch.exp(0.5 * P.p("base.logvar"))

@@ -77,6 +77,16 @@ def reparam_sample(z, mu=None, logvar=None, seed=0, offset=None, offset_host=0, 
                            eps, zbf, int(nbf), logq0)
 
 
+def reparam_grad(g_lo, g_hi, eps, logvar, partial, gmu, glv):
+    """Backward of z0 = mu + exp(logvar/2) * eps with dL/dz0 = [g_lo | g_hi]:
+    gmu = sum_b g, glv = 0.5 exp(logvar/2) sum_b g * eps - 0.5 (HIP: two deterministic passes,
+    no concatenated copy; `partial` holds per-slab column sums, >= 2 * D floats)."""
+    if _gpu(eps):
+        native().reparam_grad(g_lo, g_hi, eps, logvar, partial, gmu, glv)
+    else:
+        ref.reparam_grad(g_lo, g_hi, eps, logvar, partial, gmu, glv)
+
+
 def normal_fill(out, seed=0, offset=None, offset_host=0, stream_id=0):
     if _gpu(out):
         native().normal_fill(out, int(seed), offset, int(offset_host), int(stream_id))

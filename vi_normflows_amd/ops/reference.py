@@ -127,6 +127,12 @@ def reparam_sample(mu, logvar, seed, offset, offset_host, stream_id, z, eps, zbf
         logq0.copy_(-0.5 * D * LOG2PI - 0.5 * lv.sum() - 0.5 * (e * e).sum(1))
 
 
+def reparam_grad(g_lo, g_hi, eps, logvar, partial, gmu, glv):
+    g = torch.cat([g_lo, g_hi], 1)
+    gmu.copy_(g.sum(0))
+    glv.copy_(0.5 * torch.exp(0.5 * logvar) * (g * eps).sum(0) - 0.5)
+
+
 # ----------------------------------------------------------------- optimizer
 def flat_optimizer(kind, p, g, m, v, pbf, lr, b1, b2, eps, wd, step, step_host, gscale,
                    gscale_host, skip):
