@@ -105,10 +105,24 @@ __global__ void __launch_bounds__(256) sumsq_partial_kernel(const float* __restr
   float acc = 0.f;
   const long n4 = n >> 2;
   const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  // four independent float4 loads in flight per thread (512 blocks = 8 waves per CU)
+  float acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    const float4 v0 = reinterpret_cast<const float4*>(x)[i];
+    const float4 v1 = reinterpret_cast<const float4*>(x)[i + stride];
+    const float4 v2 = reinterpret_cast<const float4*>(x)[i + 2 * stride];
+    const float4 v3 = reinterpret_cast<const float4*>(x)[i + 3 * stride];
+    acc += v0.x * v0.x + v0.y * v0.y + v0.z * v0.z + v0.w * v0.w;
+    acc1 += v1.x * v1.x + v1.y * v1.y + v1.z * v1.z + v1.w * v1.w;
+    acc2 += v2.x * v2.x + v2.y * v2.y + v2.z * v2.z + v2.w * v2.w;
+    acc3 += v3.x * v3.x + v3.y * v3.y + v3.z * v3.z + v3.w * v3.w;
+  }
+  for (; i < n4; i += stride) {
     const float4 v = reinterpret_cast<const float4*>(x)[i];
     acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
   }
+  acc += (acc1 + acc2) + acc3;
   for (long i = 4 * n4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
     acc += x[i] * x[i];
   acc = block_sum(acc, scratch);

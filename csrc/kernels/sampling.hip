@@ -97,18 +97,44 @@ __global__ void __launch_bounds__(256) reparam_grad_partial_kernel(
   *reinterpret_cast<float4*>(out + D + c) = s2;
 }
 
+// One block per 64 columns: wave w sums partial rows w, w+4, ... for its lane's column (8 rows
+// per batch of independent loads), then the 4 wave sums combine in a fixed order via LDS.
 __global__ void __launch_bounds__(256) reparam_grad_finalize_kernel(
     const float* __restrict__ partial, int np, const float* __restrict__ logvar,
     float* __restrict__ gmu, float* __restrict__ glv, int D) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= D) return;
+  __shared__ float red[2][4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float s1 = 0.f, s2 = 0.f;
-  for (int p = 0; p < np; ++p) {
-    s1 += partial[(long)p * 2 * D + c];
-    s2 += partial[(long)p * 2 * D + D + c];
+  if (c < D) {
+    int p = w;
+    for (; p + 28 < np; p += 32) {
+      float a[8], b[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a[u] = partial[(long)(p + 4 * u) * 2 * D + c];
+        b[u] = partial[(long)(p + 4 * u) * 2 * D + D + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s1 += a[u];
+        s2 += b[u];
+      }
+    }
+    for (; p < np; p += 4) {
+      s1 += partial[(long)p * 2 * D + c];
+      s2 += partial[(long)p * 2 * D + D + c];
+    }
   }
-  gmu[c] = s1;
-  glv[c] = 0.5f * __expf(0.5f * logvar[c]) * s2 - 0.5f;
+  red[0][w][lane] = s1;
+  red[1][w][lane] = s2;
+  __syncthreads();
+  if (w == 0 && c < D) {
+    const float t1 = (red[0][0][lane] + red[0][1][lane]) + (red[0][2][lane] + red[0][3][lane]);
+    const float t2 = (red[1][0][lane] + red[1][1][lane]) + (red[1][2][lane] + red[1][3][lane]);
+    gmu[c] = t1;
+    glv[c] = 0.5f * __expf(0.5f * logvar[c]) * t2 - 0.5f;
+  }
 }
 
 // Plain N(0,1) fill with the same counter scheme (used by MC estimators and tests).
@@ -179,7 +205,7 @@ void nf_launch_reparam_grad(const float* g_lo, long ldlo, const float* g_hi, lon
   const int np = (B + rows_per - 1) / rows_per;
   hipLaunchKernelGGL(reparam_grad_partial_kernel, dim3(np), dim3(256), 0, stream, g_lo, ldlo,
                      g_hi, ldhi, eps, lde, partial, B, D, Dl, rows_per);
-  hipLaunchKernelGGL(reparam_grad_finalize_kernel, dim3((D + 255) / 256), dim3(256), 0, stream,
+  hipLaunchKernelGGL(reparam_grad_finalize_kernel, dim3((D + 63) / 64), dim3(256), 0, stream,
                      partial, np, logvar, gmu, glv, D);
   NF_HIP_CHECK(hipGetLastError());
 }

@@ -174,7 +174,8 @@ def test_normal_fill(gpu):
 
 
 @pytest.mark.parametrize("kind", [0, 1, 2, 3])
-@pytest.mark.parametrize("n", [1, 4099, 100_000])
+# 4_500_001: > 2 grid strides of float4 groups (the paired loop, the odd group and the scalar tail)
+@pytest.mark.parametrize("n", [1, 4099, 100_000, 4_500_001])
 def test_flat_optimizer(gpu, kind, n):
     torch.manual_seed(4)
     p0 = torch.randn(n, device=gpu)
@@ -193,8 +194,9 @@ def test_flat_optimizer(gpu, kind, n):
         _close(a, b, 1e-5 if a.dtype == torch.float32 else 1e-2)
 
 
-def test_sumsq_guard(gpu):
-    x = torch.randn(1_000_000, device=gpu)
+@pytest.mark.parametrize("n", [1_000_000, 5_000_003])
+def test_sumsq_guard(gpu, n):
+    x = torch.randn(n, device=gpu)
     part = torch.empty(512, device=gpu)
     s, sk, sc = (torch.empty((), device=gpu) for _ in range(3))
     torch.ops.vinf.sumsq_guard(x, part, s, sk, sc, 10.0, 0.5)
