@@ -15,7 +15,7 @@ __global__ void __launch_bounds__(256) reparam_sample_kernel(
     const float* __restrict__ mu, const float* __restrict__ logvar, uint32_t seed_lo,
     uint32_t seed_hi, const int64_t* __restrict__ offset_ptr, int64_t offset_host, uint32_t stream,
     float* __restrict__ z, long ldz, float* __restrict__ eps_out, long lde, TZ* __restrict__ zbf,
-    long ldzb, int nbf, float* __restrict__ logq0, int B, int D) {
+    long ldzb, int nbf, float* __restrict__ logq0, int B, int D, int vec) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
@@ -28,6 +28,32 @@ __global__ void __launch_bounds__(256) reparam_sample_kernel(
     float n[4];
     box_muller(r.x, r.y, n[0], n[1]);
     box_muller(r.z, r.w, n[2], n[3]);
+    if (vec && 4 * g + 3 < D) {
+      // whole float4 group: 16-B stores of z / eps, 8-B store of the bf16 copy
+      const int j = 4 * g;
+      const float4 lv4 = logvar ? *reinterpret_cast<const float4*>(logvar + j) : make_float4(0, 0, 0, 0);
+      const float4 m4 = mu ? *reinterpret_cast<const float4*>(mu + j) : make_float4(0, 0, 0, 0);
+      float4 z4;
+      z4.x = fmaf(__expf(0.5f * lv4.x), n[0], m4.x);
+      z4.y = fmaf(__expf(0.5f * lv4.y), n[1], m4.y);
+      z4.z = fmaf(__expf(0.5f * lv4.z), n[2], m4.z);
+      z4.w = fmaf(__expf(0.5f * lv4.w), n[3], m4.w);
+      *reinterpret_cast<float4*>(z + row * ldz + j) = z4;
+      if (eps_out) *reinterpret_cast<float4*>(eps_out + row * lde + j) = make_float4(n[0], n[1], n[2], n[3]);
+      if (zbf && j + 3 < nbf) {
+        st_cv<TZ>(zbf + row * ldzb + j, z4.x);
+        st_cv<TZ>(zbf + row * ldzb + j + 1, z4.y);
+        st_cv<TZ>(zbf + row * ldzb + j + 2, z4.z);
+        st_cv<TZ>(zbf + row * ldzb + j + 3, z4.w);
+      } else if (zbf) {
+        const float zz[4] = {z4.x, z4.y, z4.z, z4.w};
+        for (int q = 0; q < 4; ++q)
+          if (j + q < nbf) st_cv<TZ>(zbf + row * ldzb + j + q, zz[q]);
+      }
+      sq += (n[0] * n[0] + n[1] * n[1]) + (n[2] * n[2] + n[3] * n[3]);
+      slv += (lv4.x + lv4.y) + (lv4.z + lv4.w);
+      continue;
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int j = 4 * g + q;
@@ -171,16 +197,20 @@ void nf_launch_reparam_sample(const float* mu, const float* logvar, uint64_t see
                               long ldzb, int nbf, float* logq0, int B, int D, hipStream_t stream) {
   if (B <= 0) return;
   dim3 grid((B + 3) / 4), block(256);
+  // float4 groups need 16-B aligned rows of z / eps / mu / logvar
+  const auto al16 = [](const void* p) { return p == nullptr || ((uintptr_t)p & 15) == 0; };
+  const int vec = (D % 4 == 0) && (ldz % 4 == 0) && (eps == nullptr || lde % 4 == 0) && al16(z) &&
+                  al16(eps) && al16(mu) && al16(logvar);
   if (zbf_is_bf16 || zbf == nullptr)
     hipLaunchKernelGGL(reparam_sample_kernel<bf16_t>, grid, block, 0, stream, mu, logvar,
                        (uint32_t)(seed & 0xffffffffu), (uint32_t)(seed >> 32), offset_ptr,
                        offset_host, stream_id, z, ldz, eps, lde, (bf16_t*)zbf, ldzb, nbf, logq0, B,
-                       D);
+                       D, vec);
   else
     hipLaunchKernelGGL(reparam_sample_kernel<float>, grid, block, 0, stream, mu, logvar,
                        (uint32_t)(seed & 0xffffffffu), (uint32_t)(seed >> 32), offset_ptr,
                        offset_host, stream_id, z, ldz, eps, lde, (float*)zbf, ldzb, nbf, logq0, B,
-                       D);
+                       D, vec);
   NF_HIP_CHECK(hipGetLastError());
 }
 
