@@ -61,6 +61,32 @@ __device__ __forceinline__ void opt_update(const OptArgs& a, float& p, float g, 
   }
 }
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// NT = true: the read-once streams (g, m, v, p) are loaded and the master / moment streams are
+// stored with nontemporal hints so they do not evict the bf16 copy (read by the transpose and
+// the next step's GEMMs) from L2 / MALL.
+template <bool NT>
+__device__ __forceinline__ float4 ld4(const float* p, long i) {
+  if constexpr (NT) {
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p) + i);
+    return make_float4(v.x, v.y, v.z, v.w);
+  } else {
+    return reinterpret_cast<const float4*>(p)[i];
+  }
+}
+
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, long i, const float4& x) {
+  if constexpr (NT) {
+    f4v v = {x.x, x.y, x.z, x.w};
+    __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p) + i);
+  } else {
+    reinterpret_cast<float4*>(p)[i] = x;
+  }
+}
+
+template <bool NT>
 __global__ void __launch_bounds__(256) flat_optimizer_kernel(OptArgs a) {
   if (a.skip_ptr && *a.skip_ptr != 0.f) return;
   const float step = a.step_ptr ? *a.step_ptr : a.step_host;
@@ -70,17 +96,17 @@ __global__ void __launch_bounds__(256) flat_optimizer_kernel(OptArgs a) {
   const long n4 = a.n >> 2;
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 p = reinterpret_cast<float4*>(a.p)[i];
-    const float4 g = reinterpret_cast<const float4*>(a.g)[i];
-    float4 m = a.m ? reinterpret_cast<float4*>(a.m)[i] : make_float4(0, 0, 0, 0);
-    float4 v = a.v ? reinterpret_cast<float4*>(a.v)[i] : make_float4(0, 0, 0, 0);
+    float4 p = ld4<NT>(a.p, i);
+    const float4 g = ld4<NT>(a.g, i);
+    float4 m = a.m ? ld4<NT>(a.m, i) : make_float4(0, 0, 0, 0);
+    float4 v = a.v ? ld4<NT>(a.v, i) : make_float4(0, 0, 0, 0);
     opt_update(a, p.x, g.x * gs, m.x, v.x, bc1, bc2);
     opt_update(a, p.y, g.y * gs, m.y, v.y, bc1, bc2);
     opt_update(a, p.z, g.z * gs, m.z, v.z, bc1, bc2);
     opt_update(a, p.w, g.w * gs, m.w, v.w, bc1, bc2);
-    reinterpret_cast<float4*>(a.p)[i] = p;
-    if (a.m) reinterpret_cast<float4*>(a.m)[i] = m;
-    if (a.v) reinterpret_cast<float4*>(a.v)[i] = v;
+    st4<NT>(a.p, i, p);
+    if (a.m) st4<NT>(a.m, i, m);
+    if (a.v) st4<NT>(a.v, i, v);
     if (a.pbf) {
       ushort4 o;
       o.x = f2bf(p.x); o.y = f2bf(p.y); o.z = f2bf(p.z); o.w = f2bf(p.w);
@@ -171,10 +197,17 @@ void nf_launch_flat_optimizer(int kind, float* p, const float* g, float* m, floa
   a.step_ptr = step_ptr; a.step_host = step_host;
   a.gscale_ptr = gscale_ptr; a.gscale_host = gscale_host;
   a.skip_ptr = skip_ptr; a.kind = kind;
+  // knobs: VINF_OPT_NT=0 plain loads/stores (nontemporal is the default: 446 -> 397 us for the
+  // headline's 72.2M parameters, tools/opt_probe.py), VINF_OPT_BLOCKS grid cap
+  static const int nt = [] { const char* e = getenv("VINF_OPT_NT"); return !(e && e[0] == '0'); }();
+  static const long cap = [] { const char* e = getenv("VINF_OPT_BLOCKS"); return e ? atol(e) : 2048L; }();
   long blocks = ((n >> 2) + 255) / 256;
   if (blocks < 1) blocks = 1;
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(flat_optimizer_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+  if (blocks > cap) blocks = cap;
+  if (nt)
+    hipLaunchKernelGGL(flat_optimizer_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(flat_optimizer_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   NF_HIP_CHECK(hipGetLastError());
 }
 
