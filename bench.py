@@ -104,7 +104,7 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": {torch.bfloat16: "bf16", torch.float16: "fp16"}.get(eng.cdt, "fp32"),
             "data": "synthetic (MC samples of the learnable diagonal-Gaussian base; "
                     "normalised 784-d twisted-Gaussian target; random-init weights)",
             "config": {
