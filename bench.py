@@ -10,84 +10,135 @@ skipped inside the timed region. Data are synthetic (Monte-Carlo samples of the
 base distribution; the target is a normalised 784-d twisted Gaussian) and the
 weights are random-init.
 
+The benchmarked run TRAINS: beta = 1 (the free energy F = KL(q || p) - log Z
+with log Z = 0, so F >= 0 and decreases towards 0), Adam lr 1e-4 with a linear
+warm-up over the first 100 steps (the first bias-corrected Adam step is a sign
+step on all 72 M parameters; without the ramp the flow's log-det collapses to
+-1500 in one step). ``final_free_energy`` in the record is the F of the last
+timed step; ``profiles/r2_headline_convergence.jsonl`` holds a long trajectory
+of this exact configuration.
+
     python bench.py --gpus N --steps K --warmup W
-(N>1 under torchrun: one rank per GPU; value = whole-job samples/s; the max
-step time over ranks is used.)
+N > 1: run under torch.distributed.run (one rank per GPU), or directly - then
+bench.py launches the N ranks itself (fresh worker processes, started before
+this process touches the GPU). value = whole-job samples/s from the max step
+time over ranks.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI  # noqa: E402
-from vi_normflows_amd.ops import gemm  # noqa: E402
-from vi_normflows_amd.parallel import dist as vdist  # noqa: E402
-from vi_normflows_amd.parallel.runner import DataParallelRunner  # noqa: E402
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
 
 METRIC = "ELBO samples/sec (whole node), 32-layer RealNVP on 784-dim synthetic"
 CPU_ANCHOR = 17.8e3  # BASELINE.md "measured here" reference CPU forward-only samples/s (planar VAE)
 
 
-def main() -> None:
+def _args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     # 65536 MC samples per GPU per step: ~30 GB of the 288 GB HBM; the weight-gradient tiles get
-    # K = 65536 and the 289 MB gradient all-reduce is ~1 % of a 41 ms step
+    # K = 65536 and the 289 MB gradient all-reduce is ~1 % of a 40 ms step
     ap.add_argument("--batch", type=int, default=int(os.environ.get("VINF_BENCH_BATCH", 65536)),
                     help="per-GPU ELBO samples per step")
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--dim", type=int, default=784)
     ap.add_argument("--hidden", type=int, default=1024)
+    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--lr-warmup", type=float, default=100.0,
+                    help="linear learning-rate ramp (steps) applied by the device optimizer")
+    ap.add_argument("--max-grad-norm", type=float, default=0.0)
+    ap.add_argument("--anneal", choices=["none", "reference"], default="none",
+                    help="beta_t schedule: none (beta = 1) or the reference's min(1, 0.001 + t/T)")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--gemm", choices=["mfma", "blas"], default=os.environ.get("VINF_GEMM", "mfma"))
     ap.add_argument("--bucket-mb", type=float, default=32.0)
-    ap.add_argument("--cpu", action="store_true", help="plumbing run on CPU (tiny sizes)")
+    ap.add_argument("--force-reduce", action="store_true",
+                    help="run the bucketed all-reduce path even at world size 1 (RCCL check)")
+    ap.add_argument("--cpu", action="store_true", help="plumbing run on CPU (gloo; use tiny sizes)")
     ap.add_argument("--verbose", action="store_true")
-    a = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _self_launch(a) -> int:
+    """Start N ranks of this script under torch.distributed.run as a CHILD process (this
+    process has not initialised HIP: nothing above imports torch.cuda state) and return its
+    exit code. The JSON line of rank 0 passes straight through on stdout."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(a.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def main() -> int:
+    a = _args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        return _self_launch(a)
+    if env_world is not None and int(env_world) != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={env_world}; launch one rank "
+                         f"per GPU (torch.distributed.run --nproc-per-node {a.gpus}) or drop --gpus")
+
+    import torch
+
+    from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI
+    from vi_normflows_amd.ops import gemm
+    from vi_normflows_amd.parallel import dist as vdist
+    from vi_normflows_amd.parallel.runner import DataParallelRunner
 
     gemm.set_backend(a.gemm)
     info = vdist.init(device_type="cpu" if a.cpu else None)
     world = info.world
-    if world != a.gpus and info.is_main:
-        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    cfg = RealNVPConfig(dim=a.dim, n_layers=a.layers, hidden=a.hidden, anneal="reference",
+    cfg = RealNVPConfig(dim=a.dim, n_layers=a.layers, hidden=a.hidden, anneal=a.anneal,
                         anneal_iters=10000)
-    eng = RealNVPVI(cfg, batch=a.batch, device=info.device, seed=1234, rank=info.rank, lr=1e-4)
-    runner = DataParallelRunner(eng, info, bucket_cap_mb=a.bucket_mb)
+    eng = RealNVPVI(cfg, batch=a.batch, device=info.device, seed=1234, rank=info.rank, lr=a.lr,
+                    lr_warmup=a.lr_warmup, max_grad_norm=a.max_grad_norm)
+    runner = DataParallelRunner(eng, info, bucket_cap_mb=a.bucket_mb, force_reduce=a.force_reduce)
+    cuda = info.device.type == "cuda"
 
     captured = False
-    if a.graph != "off" and info.device.type == "cuda":
+    if a.graph != "off" and cuda:
         captured = runner.capture(warmup=max(1, min(a.warmup, 3)))
         if a.graph == "on" and not captured:
             raise RuntimeError("hipGraph capture failed")
     for _ in range(a.warmup):
         runner.step()
-    if info.device.type == "cuda":
+    if cuda:
         torch.cuda.synchronize()
     vdist.barrier()
-    if info.device.type == "cuda":
+    if cuda:
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         runner.step()
-    if info.device.type == "cuda":
+    if cuda:
         torch.cuda.synchronize()
     vdist.barrier()
-    if info.device.type == "cuda":
+    if cuda:
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     dt = vdist.all_reduce_max(dt)
     loss = float(eng.loss.item())
+    steps_done = int(eng.step_t.item())
     ms = 1000.0 * dt / a.steps
     global_batch = a.batch * world
     value = global_batch * a.steps / dt
@@ -120,16 +171,21 @@ def main() -> None:
                 "hipgraph": captured,
                 "gemm_backend": a.gemm,
                 "model_tflops": round(tflops, 1),
+                "optimizer": f"adam lr {a.lr:g}, linear warm-up {a.lr_warmup:g} steps, "
+                             f"clip {a.max_grad_norm:g}, anneal {a.anneal}",
                 "final_free_energy": loss,
+                "final_free_energy_step": steps_done,
+                "free_energy_floor": "-log Z = 0 at beta = 1",
                 "vs_reference_cpu_anchor": round(value / CPU_ANCHOR, 1),
                 "cpu_anchor_note": "BASELINE.md measured-here reference NumPy planar VAE "
                                    "forward-only 17.8k samples/s (different workload; "
                                    "no published number for this metric)",
             },
         }
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     vdist.shutdown()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -131,7 +131,7 @@ void target_logp_grad(int64_t kind, const at::Tensor& A, const at::Tensor& Bh,
   check_dtype(Bh, at::kFloat, "B");
   const int B = A.size(0), Dh = A.size(1);
   TORCH_CHECK(Bh.size(0) == B && Bh.size(1) == Dh, "halves must match");
-  TORCH_CHECK(kind == 0 || kind == 1, "unknown target kind");
+  TORCH_CHECK(kind >= 0 && kind <= 2, "unknown target kind");
   if (kind == 0) {
     TORCH_CHECK(params && params->defined() && params->numel() == 4 * Dh, "gaussian params [2D]");
   }
@@ -252,7 +252,7 @@ void flat_optimizer(int64_t kind, const at::Tensor& p, const at::Tensor& g,
                     const c10::optional<at::Tensor>& pbf, double lr, double b1, double b2,
                     double eps, double wd, const c10::optional<at::Tensor>& step, double step_host,
                     const c10::optional<at::Tensor>& gscale, double gscale_host,
-                    const c10::optional<at::Tensor>& skip) {
+                    const c10::optional<at::Tensor>& skip, double warmup) {
   check_cuda(p, "p");
   check_dtype(p, at::kFloat, "p");
   check_dtype(g, at::kFloat, "g");
@@ -265,12 +265,18 @@ void flat_optimizer(int64_t kind, const at::Tensor& p, const at::Tensor& g,
   chk(v, "v");
   chk(pbf, "pbf");
   if (pbf && pbf->defined()) check_dtype(*pbf, at::kBFloat16, "pbf");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(p.data_ptr()) % 16 == 0, "p must be 16-B aligned");
+  // the kernel moves 16 B per lane on p, g, m, v and 8 B on the bf16 copy
+  auto aligned = [](const void* q, uintptr_t a) { return reinterpret_cast<uintptr_t>(q) % a == 0; };
+  TORCH_CHECK(aligned(p.data_ptr(), 16), "p must be 16-B aligned");
+  TORCH_CHECK(aligned(g.data_ptr(), 16), "g must be 16-B aligned");
+  if (m && m->defined()) TORCH_CHECK(aligned(m->data_ptr(), 16), "m must be 16-B aligned");
+  if (v && v->defined()) TORCH_CHECK(aligned(v->data_ptr(), 16), "v must be 16-B aligned");
+  if (pbf && pbf->defined()) TORCH_CHECK(aligned(pbf->data_ptr(), 8), "pbf must be 8-B aligned");
   nf_launch_flat_optimizer((int)kind, p.data_ptr<float>(), g.data_ptr<float>(), opt_ptr<float>(m),
                            opt_ptr<float>(v), opt_ptr<void>(pbf), n, (float)lr, (float)b1,
                            (float)b2, (float)eps, (float)wd, opt_ptr<float>(step), (float)step_host,
                            opt_ptr<float>(gscale), (float)gscale_host, opt_ptr<float>(skip),
-                           cur_stream());
+                           (float)warmup, cur_stream());
 }
 
 void sumsq_guard(const at::Tensor& x, const at::Tensor& partial,
@@ -280,6 +286,8 @@ void sumsq_guard(const at::Tensor& x, const at::Tensor& partial,
   check_dtype(x, at::kFloat, "x");
   check_dtype(partial, at::kFloat, "partial");
   TORCH_CHECK(x.is_contiguous() && partial.is_contiguous(), "contiguous");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "x must be 16-B aligned");
+  TORCH_CHECK(partial.numel() >= 1, "partial needs at least one slot (one block per slot)");
   nf_launch_sumsq_guard(x.data_ptr<float>(), x.numel(), partial.data_ptr<float>(),
                         (int)partial.numel(), opt_ptr<float>(out_sumsq), opt_ptr<float>(skip),
                         opt_ptr<float>(scale), (float)max_norm, (float)base_scale, cur_stream());
@@ -308,7 +316,7 @@ TORCH_LIBRARY(vinf, m) {
         "Tensor(b!) gmu, Tensor(c!) glv) -> ()");
   m.def("flat_optimizer(int kind, Tensor(a!) p, Tensor g, Tensor(b!)? m, Tensor(c!)? v, "
         "Tensor(d!)? pbf, float lr, float b1, float b2, float eps, float wd, Tensor? step, "
-        "float step_host, Tensor? gscale, float gscale_host, Tensor? skip) -> ()");
+        "float step_host, Tensor? gscale, float gscale_host, Tensor? skip, float warmup=0.0) -> ()");
   m.def("cu_hold(int blocks, float usec) -> ()", &cu_hold);
   m.def("sumsq_guard(Tensor x, Tensor(a!) partial, Tensor(b!)? out_sumsq, Tensor(c!)? skip, "
         "Tensor(d!)? scale, float max_norm, float base_scale) -> ()");

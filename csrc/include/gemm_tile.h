@@ -211,6 +211,19 @@ __device__ __forceinline__ void epi_store(const GemmArgs& a, v4f v, int m, int n
 }
 
 // ---------------------------------------------------------------------------------------------
+// bf16 staging image of one wave's sub-tile: [rows][64 n] in 128-B rows, 16-B chunk q of row r
+// at q ^ (r & 7), and the two 8-B halves of a chunk swapped on rows with bit 3 set. The swap makes
+// the fragment writes conflict-free: a ds_write_b64 lane group (16 lanes = 16 rows r0..r0+15,
+// one 8-B slot each) covers 32 distinct dwords of the 32-bank write space, where rows r and r+8
+// used to land on the same two banks (2-way; SQ_LDS_BANK_CONFLICT 0.23-0.30 per LDS cycle on
+// the bf16 epilogues). The 16-B readback reads the same chunk and swaps the halves back.
+__device__ __forceinline__ int bf_stage_off(int row, int slot) {
+  return row * 128 + (((slot >> 1) ^ (row & 7)) << 4) + (((slot & 1) ^ ((row >> 3) & 1)) << 3);
+}
+__device__ __forceinline__ v4u bf_stage_fix(v4u v, bool swapped) {
+  return swapped ? (v4u){v[2], v[3], v[0], v[1]} : v;
+}
+
 // LDS-staged epilogue. In the fragment layout one store instruction covers 16 rows x 32 B
 // (bf16) or 16 rows x 64 B (fp32): 16 partial cache lines per instruction, which made the
 // output write, not the MFMAs, the per-tile fixed cost at K <= 1024 (~15 us per 256^2 tile).
@@ -282,8 +295,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
         const unsigned lo = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
         const unsigned hi = (unsigned)f2bf(v2) | ((unsigned)f2bf(v3) << 16);
         const int slot = i * 4 + g;  // 8-B slot of the 128-B row
-        *(LDS_AS v2u*)(region + row * 128 + (((slot >> 1) ^ (row & 7)) << 4) + (slot & 1) * 8) =
-            (v2u){lo, hi};
+        *(LDS_AS v2u*)(region + bf_stage_off(row, slot)) = (v2u){lo, hi};
       }
     }
     // aux rows (ReLU mask) for every readback row, in flight while the LDS writes drain
@@ -321,7 +333,9 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
 #pragma unroll
     for (int it = 0; it < NJ * 2; ++it) {
       const int row = it * 8 + (lane >> 3);
-      const v4u v = *(const LDS_AS v4u*)(region + row * 128 + ((q ^ (row & 7)) << 4));
+      // (row >> 3) & 1 == it & 1: the half swap of bf_stage_off is a compile-time register swap
+      const v4u v = bf_stage_fix(*(const LDS_AS v4u*)(region + row * 128 + ((q ^ (row & 7)) << 4)),
+                                 (it & 1) != 0);
       const int m = m0 + row, n = n0 + q * 8;
       if (m < a.M && n < a.N) {
         uint4 o = make_uint4(v[0], v[1], v[2], v[3]);

@@ -45,7 +45,8 @@ void nf_launch_reparam_grad(const float* g_lo, long ldlo, const float* g_hi, lon
 void nf_launch_flat_optimizer(int kind, float* p, const float* g, float* m, float* v, void* pbf,
                               long n, float lr, float b1, float b2, float eps, float wd,
                               const float* step_ptr, float step_host, const float* gscale_ptr,
-                              float gscale_host, const float* skip_ptr, hipStream_t stream);
+                              float gscale_host, const float* skip_ptr, float warmup,
+                              hipStream_t stream);
 // diagnostics: hold `blocks` CU slots for `usec` us (collective-occupancy emulation)
 void nf_launch_cu_hold(int blocks, float usec, hipStream_t stream);
 void nf_launch_sumsq_guard(const float* x, long n, float* partial, int npartial, float* out_sumsq,

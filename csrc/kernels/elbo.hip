@@ -11,6 +11,8 @@
 //   kind 0 (diag Gaussian): log N(z; m, diag(v)), params = [m(D), 1/v(D)], cst = -D/2 log 2pi - 1/2 sum log v
 //   kind 1 (banana / twisted Gaussian, Haario et al.): pairs (x=z_2i, y=z_2i+1),
 //           log N(x; 0, s1^2) + log N(y - b (x^2 - s1^2); 0, s2^2); exactly normalised (log Z = 0).
+//   kind 2 (banana, split pairing): the same density with pairs (x=z_i, y=z_{D/2+i}), i.e. each
+//           pair straddles the RealNVP coupling split.
 //
 // bernoulli_logits: per-row sum_j x_j l_j - softplus(l_j) and dL/dl = coef (x - sigmoid(l)).
 #include "nf_common.h"
@@ -53,18 +55,21 @@ __global__ void __launch_bounds__(256) target_logp_grad_kernel(
   } else {
     const float s1 = p0, s2 = p1, bend = p2;
     const float is1 = 1.f / (s1 * s1), is2 = 1.f / (s2 * s2);
+    const bool split = kind == 2;
     for (int i = lane; i < Dh; i += 64) {
-      // pair (2i, 2i+1); straddles the two halves only when Dh is odd
-      const int j = 2 * i;
+      // kind 1: pair (2i, 2i+1) - both in one coupling half (straddles only when Dh is odd);
+      // kind 2: pair (i, Dh + i) - x in the first half, y in the second
+      const int j = split ? i : 2 * i;
+      const int j1 = split ? Dh + i : 2 * i + 1;
       const float x = zval(A, lda, Bh, ldb, row, j, Dh);
-      const float y = zval(A, lda, Bh, ldb, row, j + 1, Dh);
+      const float y = zval(A, lda, Bh, ldb, row, j1, Dh);
       const float r = y - bend * (x * x - s1 * s1);
       acc += x * x * is1 + r * r * is2;
       if (gA) {
         const float dy = -r * is2;
         const float dx = -x * is1 + r * is2 * 2.f * bend * x;
         float* gp0 = j < Dh ? (gA + row * ldga + j) : (gB + row * ldgb + (j - Dh));
-        float* gp1 = (j + 1) < Dh ? (gA + row * ldga + j + 1) : (gB + row * ldgb + (j + 1 - Dh));
+        float* gp1 = j1 < Dh ? (gA + row * ldga + j1) : (gB + row * ldgb + (j1 - Dh));
         const float g0 = coef * dx, g1 = coef * dy;
         if (grad_accumulate) {
           *gp0 += g0;

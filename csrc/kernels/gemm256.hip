@@ -200,8 +200,7 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
       const unsigned hi = (unsigned)f2bf(acc[i][j][2] + bv[i][2]) |
                           ((unsigned)f2bf(acc[i][j][3] + bv[i][3]) << 16);
       const int slot = i * 4 + g;
-      *(LDS_AS v2u*)(region + row * 128 + (((slot >> 1) ^ (row & 7)) << 4) + (slot & 1) * 8) =
-          (v2u){lo, hi};
+      *(LDS_AS v2u*)(region + bf_stage_off(row, slot)) = (v2u){lo, hi};
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -214,8 +213,9 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
     if (m < a.M) {
       if (fok) {
         const int off = r * 128 + ((q ^ (r & 7)) << 4);
-        const v4u sh = *(const LDS_AS v4u*)(smem + (wrr * 4 + ws) * 16384 + off);
-        const v4u tt = *(const LDS_AS v4u*)(smem + (wrr * 4 + 2 + ws) * 16384 + off);
+        const bool swp = (r >> 3) & 1;   // bf_stage_off's half swap
+        const v4u sh = bf_stage_fix(*(const LDS_AS v4u*)(smem + (wrr * 4 + ws) * 16384 + off), swp);
+        const v4u tt = bf_stage_fix(*(const LDS_AS v4u*)(smem + (wrr * 4 + 2 + ws) * 16384 + off), swp);
         const float4 x0 = xv[it][0], x1 = xv[it][1];
         const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
         float y[8];

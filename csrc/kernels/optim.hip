@@ -29,6 +29,7 @@ struct OptArgs {
   const float* gscale_ptr; // device gradient multiplier, may be null
   float gscale_host;
   const float* skip_ptr;   // device flag; != 0 -> no update
+  float warmup;            // > 0: lr ramps linearly over the first `warmup` steps (lr * min(1, t / warmup))
   int kind;
 };
 
@@ -87,12 +88,17 @@ __device__ __forceinline__ void st4(float* p, long i, const float4& x) {
 }
 
 template <bool NT>
-__global__ void __launch_bounds__(256) flat_optimizer_kernel(OptArgs a) {
+__global__ void __launch_bounds__(256) flat_optimizer_kernel(OptArgs a_) {
+  OptArgs a = a_;
   if (a.skip_ptr && *a.skip_ptr != 0.f) return;
   const float step = a.step_ptr ? *a.step_ptr : a.step_host;
   const float gs = a.gscale_ptr ? *a.gscale_ptr : a.gscale_host;
   const float bc1 = 1.f - powf(a.b1, step);
   const float bc2 = 1.f - powf(a.b2, step);
+  // linear learning-rate warm-up, read from the device step so a captured graph replays it: the
+  // first bias-corrected Adam step is a sign step of size lr on EVERY parameter, which at 72 M
+  // parameters and 32 coupling layers throws the flow far off (ldj -1 -> -1500 in one step)
+  if (a.warmup > 0.f && step < a.warmup) a.lr *= fmaxf(step, 1.f) / a.warmup;
   const long n4 = a.n >> 2;
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -189,14 +195,15 @@ using namespace nf;
 void nf_launch_flat_optimizer(int kind, float* p, const float* g, float* m, float* v, void* pbf,
                               long n, float lr, float b1, float b2, float eps, float wd,
                               const float* step_ptr, float step_host, const float* gscale_ptr,
-                              float gscale_host, const float* skip_ptr, hipStream_t stream) {
+                              float gscale_host, const float* skip_ptr, float warmup,
+                              hipStream_t stream) {
   if (n <= 0) return;
   OptArgs a;
   a.p = p; a.g = g; a.m = m; a.v = v; a.pbf = (bf16_t*)pbf; a.n = n;
   a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd;
   a.step_ptr = step_ptr; a.step_host = step_host;
   a.gscale_ptr = gscale_ptr; a.gscale_host = gscale_host;
-  a.skip_ptr = skip_ptr; a.kind = kind;
+  a.skip_ptr = skip_ptr; a.kind = kind; a.warmup = warmup;
   // knobs: VINF_OPT_NT=0 plain loads/stores (nontemporal is the default: 446 -> 397 us for the
   // headline's 72.2M parameters, tools/opt_probe.py), VINF_OPT_BLOCKS grid cap
   static const int nt = [] { const char* e = getenv("VINF_OPT_NT"); return !(e && e[0] == '0'); }();

@@ -3,8 +3,10 @@ encoder 784 -> 64 x 3 (ReLU) -> (mu, logvar, W, U, b), K planar flows, Bernoulli
 decoder, beta-annealed free energy, Adam lr 1e-3, batch 128, N = 2000.
 
 MNIST is not shipped with the reference (``data/`` only holds HW0_data.csv) and there is no
-network: pass ``--data digits.npy`` (N x 784 binary, e.g. digits {0,1,4,7} binarised at 0.5
-as in learning_mnist.py:44-54) or it trains on synthetic binary prototypes. Writes the
+network: pass ``--data DIR`` holding ``train-images-idx3-ubyte`` / ``train-labels-idx1-ubyte``
+(optionally .gz; read by ``utils.mnist_idx``, digits {0,1,4,7} kept and binarised at 0.5 as in
+learning_mnist.py:44-54), or ``--data digits.npy`` (N x 784 binary), or it trains on synthetic
+binary prototypes. Writes the
 reference-format ``weights_{phi,theta}_{K}.npy`` and appends ``"{K} flows: F"`` (per batch of
 128, the reference's units) to ``free_energy.txt``.
 

@@ -62,3 +62,29 @@ def test_bench_torchrun_two_ranks_cpu():
     recs = _json_lines(r.stdout)
     assert len(recs) == 1, r.stdout      # rank 0 only
     _check(recs[0], 2)
+
+
+def test_bench_self_launch_two_ranks_cpu():
+    """``python bench.py --gpus 2`` without torchrun starts its own 2 ranks (child launcher)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *SMALL],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    _check(recs[0], 2)
+
+
+def test_bench_gpus_world_mismatch_is_an_error():
+    env = dict(_env(), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *SMALL],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "WORLD_SIZE" in r.stderr
+
+
+def test_bench_force_reduce_cpu():
+    """The world-size-1 forced all-reduce path (gloo on the CPU, RCCL on a GPU)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--force-reduce", *SMALL],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    _check(_json_lines(r.stdout)[0], 1)

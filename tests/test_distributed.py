@@ -125,3 +125,69 @@ def test_injected_nan_on_one_rank_skips_step_on_all(tmp_path):
     assert torch.equal(f0["snaps"][2], f0["snaps"][1])        # step 2 skipped
     assert not torch.equal(f0["snaps"][3], f0["snaps"][2])    # training continued
     assert torch.isfinite(f0["snaps"]).all()
+
+
+# ------------------------------------------------------------------------------------------
+# Module-path data parallelism (inference.trainer.Trainer): broadcast init, hook-driven
+# bucketed all-reduce over flat gradient views, device-side guard with one shared decision.
+def _mlp(seed):
+    g = torch.Generator().manual_seed(seed)
+    m = torch.nn.Sequential(torch.nn.Linear(5, 16), torch.nn.Tanh(), torch.nn.Linear(16, 16),
+                            torch.nn.Tanh(), torch.nn.Linear(16, 3))
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * 0.5)
+    return m
+
+
+def _trainer_worker(rank, world, port, X, Y, out_dir, nan_rank):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from vi_normflows_amd.inference.elbo import FreeEnergy
+    from vi_normflows_amd.inference.trainer import TrainConfig, Trainer
+
+    model = _mlp(1000 + rank)            # deliberately different init per rank
+    n = X.shape[0] // world
+    xs, ys = X[rank * n:(rank + 1) * n], Y[rank * n:(rank + 1) * n]
+
+    def loss_fn(t, beta):
+        F = ((model(xs) - ys) ** 2).mean()
+        if nan_rank == rank and t == 1:
+            F = F * float("nan")         # only THIS rank's loss is non-finite at t = 1
+        return FreeEnergy(F, {})
+
+    tr = Trainer(model.parameters(), loss_fn,
+                 TrainConfig(iters=3, lr=0.05, optimizer="sgd", log_every=1), bucket_mb=0.0005)
+    assert tr.reducer is not None and len(tr.reducer.buckets) > 2
+    tr.fit(3)
+    torch.save({"params": [p.detach().clone() for p in model.parameters()],
+                "skipped": tr.n_skipped}, os.path.join(out_dir, f"t{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nan_rank", [-1, 1])
+def test_trainer_dp_broadcast_hooks_equal_single_process(tmp_path, nan_rank):
+    from vi_normflows_amd.inference.elbo import FreeEnergy
+    from vi_normflows_amd.inference.trainer import TrainConfig, Trainer
+
+    world = 2
+    torch.manual_seed(3)
+    X, Y = torch.randn(8, 5), torch.randn(8, 3)
+    mp.spawn(_trainer_worker, args=(world, _free_port(), X, Y, str(tmp_path), nan_rank),
+             nprocs=world, join=True)
+    r = [torch.load(tmp_path / f"t{k}.pt", weights_only=True) for k in range(world)]
+    for a, b in zip(r[0]["params"], r[1]["params"]):
+        assert torch.equal(a, b)          # replicas identical after broadcast + reduced steps
+    assert r[0]["skipped"] == r[1]["skipped"] == (1 if nan_rank >= 0 else 0)
+    # single process on the concatenated batch from rank 0's init (the broadcast source)
+    model = _mlp(1000)
+    skip = {1} if nan_rank >= 0 else set()
+
+    def loss_fn(t, beta):
+        F = ((model(X) - Y) ** 2).mean()
+        return FreeEnergy(F * float("nan") if t in skip else F, {})
+
+    tr = Trainer(model.parameters(), loss_fn, TrainConfig(iters=3, lr=0.05, optimizer="sgd"))
+    tr.fit(3)
+    for a, b in zip(r[0]["params"], model.parameters()):
+        assert torch.allclose(a, b.detach(), atol=1e-6, rtol=1e-5)

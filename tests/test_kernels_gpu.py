@@ -75,7 +75,7 @@ def test_coupling_bwd_from_s_hat(gpu, B, Dh):
     assert torch.allclose(out[0][1], out[1][1], rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("kind", [0, 1, 2])
 @pytest.mark.parametrize("B,Dh", [(5, 2), (40, 392)])
 def test_target_logp_grad(gpu, kind, B, Dh):
     torch.manual_seed(2)
@@ -176,7 +176,8 @@ def test_normal_fill(gpu):
 @pytest.mark.parametrize("kind", [0, 1, 2, 3])
 # 4_500_001: > 2 grid strides of float4 groups (the paired loop, the odd group and the scalar tail)
 @pytest.mark.parametrize("n", [1, 4099, 100_000, 4_500_001])
-def test_flat_optimizer(gpu, kind, n):
+@pytest.mark.parametrize("warmup", [0.0, 10.0])
+def test_flat_optimizer(gpu, kind, n, warmup):
     torch.manual_seed(4)
     p0 = torch.randn(n, device=gpu)
     g = torch.randn(n, device=gpu)
@@ -188,7 +189,7 @@ def test_flat_optimizer(gpu, kind, n):
         step = torch.tensor(3.0, device=gpu)
         gs = torch.tensor(0.5, device=gpu)
         f = torch.ops.vinf.flat_optimizer if impl == "native" else ref.flat_optimizer
-        f(kind, p, g, m, v, pbf, 1e-2, 0.9, 0.99, 1e-8, 0.01, step, 1.0, gs, 1.0, None)
+        f(kind, p, g, m, v, pbf, 1e-2, 0.9, 0.99, 1e-8, 0.01, step, 1.0, gs, 1.0, None, warmup)
         res.append((p, m, v, pbf))
     for a, b in zip(*res):
         _close(a, b, 1e-5 if a.dtype == torch.float32 else 1e-2)

@@ -146,14 +146,75 @@ def gradient_create(F, D, N, unpack_params):
     return variational_objective, gradient
 
 
+def compare_reconstruction(phi, theta, x_true, encode, decode, K, t, figname=None,
+                           variant: str = "paper", decode_is_logits: bool = False, seed=None):
+    """utils.py:25-38: encode one image, sample z through the K flows, decode, Bernoulli-sample
+    and save true-vs-reconstruction as ``figname.format(K, t)``. Returns the saved path.
+
+    ``decode`` output is read as probabilities (the reference's sigmoid "logits", Q9) unless
+    ``decode_is_logits``."""
+    from ..utils.paths import figname as default_figname
+    from ..viz.plots import _plt, plot_mnist
+
+    xt, _ = _t(x_true)
+    xt = xt.reshape(1, -1)
+    g = torch.Generator().manual_seed(int(seed)) if seed is not None else None
+    with torch.no_grad():
+        mu0, lsd0, W, U, b = encode(phi, xt)
+        z = DF.sample_from_pz(mu0, lsd0, W, U, b, W.shape[0], variant=variant, generator=g)
+        out = decode(theta, z)
+        p = torch.sigmoid(out) if decode_is_logits else out.clamp(0.0, 1.0)
+        xhat = torch.bernoulli((p + EPS).clamp(max=1.0), generator=g)
+    path = (figname or default_figname).format(K, t)
+    fig = plot_mnist(xt[0], xhat[0], path)
+    _plt().close(fig)
+    return path
+
+
+def get_samples_from_params(phi, theta, X, K, variant: str = "paper", seed=None):
+    """The capability of utils.py:16-22 (whose indexing is broken, Q11): sample z_K from the
+    flow parameters phi = (mu, log_sigma_diag, W, U, b) and decode it through the affine
+    likelihood theta = (mu_z, log_sigma_diag_pz, logit_pi, A, B) plus unit Gaussian noise:
+    Xhat = z_K A^T + B + eps, eps ~ N(0, I). Returns (Xhat, z_K) of the input's kind."""
+    (Xt, was_np) = _t(X)
+    N, D = Xt.shape
+    g = torch.Generator().manual_seed(int(seed)) if seed is not None else None
+    mu, lsd, W, U, b = [_t(a)[0] for a in phi]
+    ZK = DF.sample_from_pz(mu, lsd, W, U, b, K, variant=variant, generator=g)
+    A, B = _t(theta[3])[0], _t(theta[4])[0]
+    Xhat = DF_affine(ZK, A, B) + torch.randn(N, D, generator=g, dtype=ZK.dtype)
+    return _out(Xhat, was_np), _out(ZK, was_np)
+
+
+def DF_affine(Z, slope, intercept):
+    """transformations.affine: (slope @ Z^T)^T + intercept."""
+    slope = slope.reshape(-1, Z.shape[1]) if slope.dim() < 2 else slope
+    return (slope.to(Z.dtype) @ Z.T).T + intercept.to(Z.dtype)
+
+
 def optimize(logp, X, D, K, N, init_params, unpack_params, encode, decode, max_iter, batch_size,
              step_size, verbose=True, seed: int = 0, log_every: int = 100,
-             results_path=None, variant: str = "paper"):
+             results_path=None, variant: str = "paper", callback=None, recon_every: int = 200,
+             recon_index: int = 101, figname=None, decode_is_logits: bool = False):
     """Amortized planar-flow VI with the reference signature (optimization.py:40-121).
 
     ``encode(phi, X) -> (mu0, log_sigma_diag0, W (K,N,D), U, b (K,N))``, ``decode(theta, z)``
     and ``logp(X, z, decoded) -> (N,)`` must be torch-differentiable. Objective: the
     corrected free energy with the reference beta_t schedule; Adam(step_size).
+
+    The reference callback (optimization.py:97-116), made cheap (Q10: no extra gradient /
+    objective passes - the step's own F and gradient norm are reported):
+
+    * every ``log_every`` iterations (``verbose``): objective and gradient magnitude;
+    * every ``recon_every`` iterations (``verbose`` and ``figname`` or the default
+      ``utils.paths.figname``): a reconstruction figure of ``X[recon_index]``
+      (``compare_reconstruction``), written as ``figname.format(K, t)``;
+    * NaN capture: a non-finite objective or gradient prints the parameters (as the reference
+      does on its ``ValueError``) and the step is skipped instead of poisoning Adam;
+    * ``callback(params, t, g)`` - the user hook, the reference's ``adam(callback=...)``
+      signature - after every update;
+    * at the last iteration the final F is appended to ``results_path`` as "{K} flows: F".
+
     Returns ``unpack_params(final_params)``.
     """
     Xt, _ = _t(X)
@@ -163,6 +224,8 @@ def optimize(logp, X, D, K, N, init_params, unpack_params, encode, decode, max_i
     opt = torch.optim.Adam([params], lr=step_size)
     LOG2PI = math.log(2 * math.pi)
     F_val = math.nan
+    self_recon = verbose and recon_every > 0 and Xt.shape[0] > 0 and Xt.shape[1] == 784
+    n_nan = 0
     for t in range(max_iter):
         Xb = batch_iter(t)
         phi, theta = unpack_params(params)
@@ -175,10 +238,24 @@ def optimize(logp, X, D, K, N, init_params, unpack_params, encode, decode, max_i
         Fv = (lq0 - ldj - beta * logp(Xb, zK, decode(theta, zK))).mean()
         opt.zero_grad()
         Fv.backward()
-        opt.step()
         F_val = float(Fv)
+        gmag = float(params.grad.norm())
+        if not (math.isfinite(F_val) and math.isfinite(gmag)):
+            n_nan += 1
+            print(f"nan gradient at iteration {t} (objective {F_val}); step skipped")
+            print(params.detach())
+            print(unpack_params(params.detach()))
+        else:
+            opt.step()
         if verbose and t % log_every == 0:
-            print(f"Iteration {t}; objective: {F_val} gradient mag: {float(params.grad.norm()):.3f}")
+            print(f"Iteration {t}; objective: {F_val} gradient mag: {gmag:.3f}")
+        if self_recon and t % recon_every == 0:
+            xi = Xt[min(recon_index, Xt.shape[0] - 1)]
+            phi_d, theta_d = unpack_params(params.detach())
+            compare_reconstruction(phi_d, theta_d, xi, encode, decode, K, t, figname=figname,
+                                   variant=variant, decode_is_logits=decode_is_logits, seed=seed + t)
+        if callback is not None:
+            callback(params.detach(), t, params.grad.detach())
     if results_path is not None:
         from ..utils.metrics import append_free_energy
 

@@ -12,7 +12,6 @@ resume (params + optimizer + RNG + step), optional data-parallel gradient averag
 """
 from __future__ import annotations
 
-import math
 import time
 from dataclasses import dataclass, field
 
@@ -43,9 +42,29 @@ class NonFiniteError(RuntimeError):
 
 
 class Trainer:
-    """loss_fn(t, beta) -> FreeEnergy (F differentiable + stats dict)."""
+    """loss_fn(t, beta) -> FreeEnergy (F differentiable + stats dict).
 
-    def __init__(self, params, loss_fn, cfg: TrainConfig, logger=None, callback=None):
+    Gradients live in ONE flat buffer: every parameter's ``.grad`` is a view into it (the DDP
+    "gradient as bucket view" layout), so autograd accumulates straight into the buffer. Under
+    data parallelism:
+
+    * rank 0's parameters (and the optional ``buffers``) are broadcast at construction, so every
+      replica starts from the same model whatever each rank's seed was;
+    * a post-accumulate-grad hook per parameter marks it ready; a bucket of ~``bucket_mb``
+      (cut from the END of the buffer, i.e. the parameters backward reaches first) is
+      all-reduced asynchronously the moment its last parameter is ready, overlapping the rest of
+      backward (``parallel.reducer.BucketedAllReduce``);
+    * the non-finite guard is one fused sum-of-squares over the reduced buffer plus one slot that
+      holds ``0 * loss`` (NaN iff this rank's loss is non-finite, and reduced with the last
+      bucket): every rank reads the SAME reduced value, so all ranks skip together, and no
+      collective is ever skipped by one rank only;
+    * the 1/world average and the clip coefficient are one device-side multiplier
+      (``ops.fused.sumsq_guard``); the step costs one host read of the skip flag, not one per
+      parameter.
+    """
+
+    def __init__(self, params, loss_fn, cfg: TrainConfig, logger=None, callback=None,
+                 buffers=(), bucket_mb: float = 32.0):
         self.params = [p for p in params if p.requires_grad]
         self.loss_fn = loss_fn
         self.cfg = cfg
@@ -57,55 +76,100 @@ class Trainer:
         self.bad = 0
         self.n_skipped = 0
         self.history: list = []
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        if self.world > 1:
+            with torch.no_grad():
+                for t in list(self.params) + [b for b in buffers if b is not None]:
+                    dist.broadcast(t.data, 0)
+        self.flat = None
+        self.reducer = None
+        self._hooks = []
+        self._setup_flat(bucket_mb)
 
-    def beta(self, t: int) -> float:
-        return self.schedule(t, self.cfg.iters)
+    # ---------------------------------------------------------------- flat gradients
+    def _setup_flat(self, bucket_mb: float) -> None:
+        ps = self.params
+        if not ps or any(p.dtype != ps[0].dtype or p.device != ps[0].device for p in ps):
+            return   # mixed dtypes / devices: per-tensor fallback path
+        from ..parallel.reducer import BucketedAllReduce
 
-    def _grads_finite(self) -> bool:
-        tot = torch.zeros((), dtype=torch.float64)
+        dev, dt = ps[0].device, ps[0].dtype
+        # [loss slot (4) | param 0 | param 1 | ...], every slice 16-B aligned. The loss slot
+        # (0 * loss: non-finite iff the loss is) is unit 0, so it sits in the LAST bucket to be
+        # reduced, which fires only after the slot is written.
+        ranges, off = [], 4
+        for p in ps:
+            n = p.numel()
+            ranges.append((off, off + n))
+            off += (n + 3) // 4 * 4
+        self._loss_slot = 0
+        self.flat = torch.zeros(off, dtype=dt, device=dev)
+        for p, (a, b) in zip(ps, ranges):
+            p.grad = self.flat[a:b].view_as(p)
+        self._partials = torch.zeros(64, dtype=torch.float32, device=dev)
+        self._sumsq = torch.zeros((), dtype=torch.float32, device=dev)
+        self._skip = torch.zeros((), dtype=torch.float32, device=dev)
+        self._gscale = torch.ones((), dtype=torch.float32, device=dev)
+        if self.world > 1:
+            # units: the loss slot, then each parameter with its alignment padding
+            units = [(0, 4)] + [(a, ranges[i + 1][0] if i + 1 < len(ranges) else off)
+                                for i, (a, _) in enumerate(ranges)]
+            self.reducer = BucketedAllReduce(self.flat, units, bucket_cap_mb=bucket_mb)
+            for i, p in enumerate(ps):
+                self._hooks.append(p.register_post_accumulate_grad_hook(
+                    lambda _p, _u=i + 1: self.reducer.mark_ready(_u)))
+
+    def _zero_grads(self) -> None:
+        if self.flat is not None:
+            self.flat.zero_()
+            for p in self.params:   # a model may have replaced .grad (e.g. set_to_none)
+                if p.grad is None:
+                    raise RuntimeError("parameter .grad detached from the flat buffer")
+        else:
+            self.opt.zero_grad(set_to_none=True)
+
+    def _guard_flat(self, loss: torch.Tensor) -> bool:
+        from ..ops import fused
+
+        self.flat[self._loss_slot] = loss.detach().to(self.flat.dtype) * 0.0
+        if self.reducer is not None:
+            self.reducer.mark_ready(0)
+            self.reducer.flush_pending()   # buckets of parameters that got no gradient
+            self.reducer.finish()
+        x = self.flat if self.flat.dtype == torch.float32 else self.flat.float()
+        fused.sumsq_guard(x, self._partials, out_sumsq=self._sumsq, skip=self._skip,
+                          scale=self._gscale, max_norm=self.cfg.grad_clip,
+                          base_scale=1.0 / self.world)
+        if float(self._skip.item()) != 0.0:   # the one host sync of the step
+            return False
+        self.flat.mul_(self._gscale.to(self.flat.dtype))
+        return True
+
+    def _grads_finite_legacy(self, loss) -> bool:
+        tot = torch.zeros((), dtype=torch.float64, device=loss.device)
+        tot = tot + loss.detach().double() * 0.0
         for p in self.params:
             if p.grad is not None:
-                tot = tot + p.grad.detach().double().pow(2).sum().cpu()
+                tot = tot + p.grad.detach().double().pow(2).sum()
         if dist.is_initialized() and dist.get_world_size() > 1:
-            dist.all_reduce(tot)
+            dist.all_reduce(tot)           # every rank calls it: same decision everywhere
         return bool(torch.isfinite(tot))
-
-    def _allreduce_grads(self, bucket_mb: float = 64.0):
-        """Coalesced gradient averaging: grads are packed into flat buckets (one collective
-        per ~64 MB instead of one per tensor), all-reduced, and unpacked."""
-        if not (dist.is_initialized() and dist.get_world_size() > 1):
-            return
-        ws = dist.get_world_size()
-        grads = [p.grad for p in self.params if p.grad is not None]
-        cap = int(bucket_mb * 2 ** 20)
-        bucket, size = [], 0
-        for g in grads + [None]:
-            if g is not None and (not bucket or (size + g.numel() * g.element_size() <= cap
-                                                 and g.dtype == bucket[0].dtype)):
-                bucket.append(g)
-                size += g.numel() * g.element_size()
-                continue
-            if bucket:
-                flat = torch.cat([b.reshape(-1) for b in bucket])
-                dist.all_reduce(flat)
-                flat.div_(ws)
-                o = 0
-                for b in bucket:
-                    b.copy_(flat[o:o + b.numel()].view_as(b))
-                    o += b.numel()
-            bucket, size = ([g], g.numel() * g.element_size()) if g is not None else ([], 0)
 
     def step(self):
         t = self.t
         beta = self.beta(t)
         res = self.loss_fn(t, beta)
-        self.opt.zero_grad(set_to_none=True)
+        self._zero_grads()
+        if self.reducer is not None:
+            self.reducer.start_step()
         res.F.backward()
-        self._allreduce_grads()
-        ok = math.isfinite(res.item()) and self._grads_finite()
-        if ok:
-            if self.cfg.grad_clip > 0:
+        if self.flat is not None:
+            ok = self._guard_flat(res.F)
+        else:
+            ok = self._grads_finite_legacy(res.F)
+            if ok and self.cfg.grad_clip > 0:
                 torch.nn.utils.clip_grad_norm_(self.params, self.cfg.grad_clip)
+        if ok:
             self.opt.step()
             self.bad = 0
         else:
@@ -115,6 +179,9 @@ class Trainer:
                 raise NonFiniteError(f"{self.bad} consecutive non-finite steps at t={t}")
         self.t += 1
         return res, ok
+
+    def beta(self, t: int) -> float:
+        return self.schedule(t, self.cfg.iters)
 
     def fit(self, iters: int | None = None):
         iters = iters if iters is not None else self.cfg.iters

@@ -73,7 +73,7 @@ class MAFEngineConfig:
 class MAFEngine:
     def __init__(self, cfg: MAFEngineConfig, batch: int, device="cuda", seed: int = 0,
                  rank: int = 0, lr: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, max_grad_norm: float = 0.0):
+                 weight_decay: float = 0.0, max_grad_norm: float = 0.0, lr_warmup: float = 0.0):
         self.cfg = cfg
         self.B = int(batch)
         self.device = torch.device(device)
@@ -84,6 +84,7 @@ class MAFEngine:
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.opt_kind = fused.OPT_ADAM
         self.max_grad_norm = float(max_grad_norm)
+        self.lr_warmup = float(lr_warmup)
         self.grad_scale_host = 1.0
         self.unit_ready_hook = None
         self.data_override = None      # fixed data [B, D] (tests)
@@ -403,7 +404,7 @@ class MAFEngine:
         fused.flat_optimizer(self.opt_kind, P.master, P.grad, P.m, P.v,
                              pbf=None if P.compute is P.master else P.compute, lr=self.lr,
                              b1=b1, b2=b2, eps=self.eps, wd=self.wd, step=self.step_t,
-                             gscale=self.gscale, skip=self.skip)
+                             gscale=self.gscale, skip=self.skip, warmup=self.lr_warmup)
         self.n_skipped.add_(self.skip)
         if self.fp8:
             self.quantize_weights()

@@ -124,7 +124,18 @@ class Feedforward:
         return objective, gradient
 
     def fit(self, x_train, y_train, params: dict, reg_param=None):
-        """Adam with random restarts; keeps the best of the last 100 iterates (nn_models.py:108-164)."""
+        """Gradient-descent MLE with random restarts; keeps the best of the last 100 iterates of
+        the best restart (nn_models.py:108-164, with its never-updated ``optimal_obj`` fixed).
+
+        ``params`` keys (nn_models.py:119-138): ``step_size`` (0.01), ``max_iteration`` (5000),
+        ``check_point`` (100), ``init``, ``random_restarts`` (5), ``verbose``, and - honoured here,
+        parsed but ignored by the reference - ``optimizer`` ('adam' | 'sgd' | 'rmsprop'),
+        ``mass`` (momentum of 'sgd', autograd's ``sgd(mass=0.9)`` convention:
+        v = mass v - (1 - mass) g, w += step v) and ``call_back(weights, iteration, g)`` called
+        after every iteration with the flat (1, D) weights and their gradient (NumPy), like the
+        reference's ``adam(callback=...)`` hook. ``objective_trace`` / ``weight_trace`` hold every
+        iteration's objective and weights over all restarts.
+        """
         assert x_train.shape[0] == self.params["D_in"]
         assert y_train.shape[0] == self.params["D_out"]
         objective, _ = self.make_objective(x_train, y_train, reg_param)
@@ -133,22 +144,45 @@ class Feedforward:
         check_point = params.get("check_point", 100)
         weights_init = np.asarray(params.get("init", self.weights.reshape((1, -1))))
         restarts = params.get("random_restarts", 5)
+        optimizer = params.get("optimizer", "adam")
+        mass = params.get("mass", None)
+        user_cb = params.get("call_back", None)
+        if optimizer not in ("adam", "sgd", "rmsprop"):
+            raise ValueError(f"unknown optimizer {optimizer!r} (adam | sgd | rmsprop)")
         best = math.inf
         obj_trace, w_trace = [], []
         for _ in range(restarts):
             W = torch.tensor(weights_init, dtype=torch.float64, requires_grad=True)
-            opt = torch.optim.Adam([W], lr=step_size)
+            if optimizer == "adam":
+                opt = torch.optim.Adam([W], lr=step_size)
+            elif optimizer == "rmsprop":   # autograd rmsprop: gamma 0.9, eps 1e-8
+                opt = torch.optim.RMSprop([W], lr=step_size, alpha=0.9, eps=1e-8)
+            else:
+                opt = None
+                vel = torch.zeros_like(W)
+                m_ = 0.9 if mass is None else float(mass)
             local_o, local_w = [], []
             for it in range(max_iteration):
-                opt.zero_grad()
+                if opt is not None:
+                    opt.zero_grad()
+                elif W.grad is not None:
+                    W.grad = None
                 o = objective(W, it)
                 o.backward()
-                opt.step()
-                local_o.append(float(o))
+                g = W.grad.detach().clone()
+                if opt is not None:
+                    opt.step()
+                else:
+                    with torch.no_grad():
+                        vel.mul_(m_).sub_((1.0 - m_) * g)
+                        W.add_(step_size * vel)
+                local_o.append(float(o.detach()))
                 local_w.append(W.detach().numpy().copy())
                 if params.get("verbose", False) and it % check_point == 0:
                     print(f"Iteration {it} lower bound {float(o)}; gradient mag: "
-                          f"{float(W.grad.norm())}")
+                          f"{float(g.norm())}")
+                if user_cb is not None:
+                    user_cb(local_w[-1], it, g.numpy())
             obj_trace += local_o
             w_trace += local_w
             tail = np.asarray(local_o[-100:])

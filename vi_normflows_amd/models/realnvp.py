@@ -52,6 +52,10 @@ class RealNVPConfig:
     banana_sigma1: float = 1.0
     banana_sigma2: float = 0.5
     banana_bend: float = 0.5
+    # "interleaved": pairs (z_2i, z_2i+1), both inside one coupling half (the dependency has to
+    # be routed through the other half over several layers); "split": pairs (z_i, z_{D/2+i})
+    # straddle the coupling split
+    banana_pairing: str = "interleaved"
     gaussian_scale: float = 0.7
     learn_base: bool = True
     init_out_std: float = 1e-3     # small *random* output init (not zeros: see bench notes)
@@ -100,7 +104,8 @@ class RealNVPVI:
     def __init__(self, cfg: RealNVPConfig, batch: int, device="cuda",
                  compute_dtype: torch.dtype | None = None, seed: int = 0, rank: int = 0,
                  lr: float = 1e-4, optimizer: int = fused.OPT_ADAM, betas=(0.9, 0.999),
-                 eps: float = 1e-8, weight_decay: float = 0.0, max_grad_norm: float = 0.0):
+                 eps: float = 1e-8, weight_decay: float = 0.0, max_grad_norm: float = 0.0,
+                 lr_warmup: float = 0.0):
         self.cfg = cfg
         self.B = int(batch)
         self.device = torch.device(device)
@@ -111,6 +116,7 @@ class RealNVPVI:
         self.rank = int(rank)
         self.lr, self.opt_kind, self.betas, self.eps, self.wd = lr, optimizer, betas, eps, weight_decay
         self.max_grad_norm = float(max_grad_norm)
+        self.lr_warmup = float(lr_warmup)   # linear lr ramp over the first steps (device step)
         self.grad_scale_host = 1.0
         self.unit_ready_hook = None   # callable(unit_idx) after a unit's grads are final
         self.eps_override = None      # fixed base noise [B, D] (tests); None -> Philox sampler
@@ -275,7 +281,8 @@ class RealNVPVI:
             s1, s2 = cfg.banana_sigma1, cfg.banana_sigma2
             pairs = cfg.dim // 2
             cst = -pairs * (math.log(2 * math.pi) + math.log(s1) + math.log(s2))
-            return dict(kind=fused.TARGET_BANANA, params=None, p0=s1, p1=s2, p2=cfg.banana_bend,
+            kind = fused.TARGET_BANANA_SPLIT if cfg.banana_pairing == "split" else fused.TARGET_BANANA
+            return dict(kind=kind, params=None, p0=s1, p1=s2, p2=cfg.banana_bend,
                         cst=cst)
         if cfg.target == "gaussian":
             D, s = cfg.dim, cfg.gaussian_scale
@@ -559,7 +566,7 @@ class RealNVPVI:
         fused.flat_optimizer(self.opt_kind, P.master, P.grad, P.m, P.v,
                              pbf=None if P.compute is P.master else P.compute, lr=self.lr,
                              b1=b1, b2=b2, eps=self.eps, wd=self.wd, step=self.step_t,
-                             gscale=self.gscale, skip=self.skip)
+                             gscale=self.gscale, skip=self.skip, warmup=self.lr_warmup)
         self.n_skipped.add_(self.skip)
 
     # ------------------------------------------------------------------ step

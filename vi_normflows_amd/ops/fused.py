@@ -14,6 +14,7 @@ from ._ext import native
 
 TARGET_GAUSSIAN = 0
 TARGET_BANANA = 1
+TARGET_BANANA_SPLIT = 2   # twisted Gaussian with pairs (z_i, z_{D/2+i})
 
 OPT_ADAM = 0
 OPT_RMSPROP = 1
@@ -96,9 +97,12 @@ def normal_fill(out, seed=0, offset=None, offset_host=0, stream_id=0):
 
 
 def flat_optimizer(kind, p, g, m=None, v=None, pbf=None, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8,
-                   wd=0.0, step=None, step_host=1.0, gscale=None, gscale_host=1.0, skip=None):
+                   wd=0.0, step=None, step_host=1.0, gscale=None, gscale_host=1.0, skip=None,
+                   warmup=0.0):
+    """One fused update of a flat parameter buffer. ``warmup`` > 0 ramps the learning rate
+    linearly over the first ``warmup`` steps (read from the device ``step``)."""
     args = (int(kind), p, g, m, v, pbf, float(lr), float(b1), float(b2), float(eps), float(wd),
-            step, float(step_host), gscale, float(gscale_host), skip)
+            step, float(step_host), gscale, float(gscale_host), skip, float(warmup))
     if _gpu(p):
         native().flat_optimizer(*args)
     else:

@@ -62,7 +62,11 @@ def target_logp(kind, z, params=None, p0=1.0, p1=1.0, p2=0.0, cst=0.0):
         m, iv = params[:D], params[D:]
         return -0.5 * ((z - m) ** 2 * iv).sum(1) + cst
     s1, s2, bend = p0, p1, p2
-    x, yv = z[:, 0::2], z[:, 1::2]
+    if kind == 2:   # split pairing (z_i, z_{D/2+i})
+        Dh = z.shape[1] // 2
+        x, yv = z[:, :Dh], z[:, Dh:2 * Dh]
+    else:           # interleaved pairing (z_2i, z_2i+1)
+        x, yv = z[:, 0::2], z[:, 1::2]
     r = yv - bend * (x * x - s1 * s1)
     return -0.5 * ((x * x) / (s1 * s1) + (r * r) / (s2 * s2)).sum(1) + cst
 
@@ -135,10 +139,12 @@ def reparam_grad(g_lo, g_hi, eps, logvar, partial, gmu, glv):
 
 # ----------------------------------------------------------------- optimizer
 def flat_optimizer(kind, p, g, m, v, pbf, lr, b1, b2, eps, wd, step, step_host, gscale,
-                   gscale_host, skip):
+                   gscale_host, skip, warmup=0.0):
     if skip is not None and float(skip.reshape(())) != 0.0:
         return
     t = float(step.reshape(())) if step is not None else float(step_host)
+    if warmup > 0 and t < warmup:
+        lr = lr * max(t, 1.0) / warmup
     gs = float(gscale.reshape(())) if gscale is not None else float(gscale_host)
     gg = g * gs
     if kind == 0:

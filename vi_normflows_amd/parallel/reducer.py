@@ -42,11 +42,15 @@ class Bucket:
 
 class BucketedAllReduce:
     def __init__(self, flat_grad: torch.Tensor, unit_ranges: list, bucket_cap_mb: float = 32.0,
-                 group=None, compress_bf16: bool = False, ready_order: list | None = None):
+                 group=None, compress_bf16: bool = False, ready_order: list | None = None,
+                 force: bool = False):
         self.flat = flat_grad
         self.group = group
         self.compress = compress_bf16
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # force: issue the collectives even at world size 1 (a 1-rank RCCL communicator), so
+        # the bucketing / stream-ordering / graph-capture path runs on a one-GPU box
+        self.active = self.world > 1 or (force and dist.is_initialized())
         order = ready_order if ready_order is not None else list(range(len(unit_ranges)))[::-1]
         cap = int(bucket_cap_mb * 1024 * 1024 / flat_grad.element_size())
         self.buckets: list[Bucket] = []
@@ -86,12 +90,22 @@ class BucketedAllReduce:
             b.pending = len(b.units)
 
     def mark_ready(self, unit: int) -> None:
-        if self.world <= 1:
+        if not self.active:
             return
         b = self.buckets[self.unit_to_bucket[unit]]
         b.pending -= 1
         if b.pending == 0:
             self._launch(b)
+
+    def flush_pending(self) -> None:
+        """Launch, in bucket order, every bucket still waiting for units that produced no
+        gradient this step (unused parameters): their slices hold zeros."""
+        if not self.active:
+            return
+        for b in self.buckets:
+            if b.pending > 0:
+                b.pending = 0
+                self._launch(b)
 
     def _launch(self, b: Bucket) -> None:
         view = self.flat[b.start:b.end]
@@ -105,7 +119,7 @@ class BucketedAllReduce:
             self.works.append((w, None, None))
 
     def finish(self) -> None:
-        if self.world <= 1:
+        if not self.active:
             return
         for w, view, side in self.works:
             w.wait()

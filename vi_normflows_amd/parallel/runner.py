@@ -21,22 +21,48 @@ from .dist import DistInfo
 from .reducer import BucketedAllReduce
 
 
+def _init_single_rank_group(info: DistInfo) -> None:
+    """A world-size-1 process group on this rank's device (RCCL on a GPU, gloo on the CPU)."""
+    import socket
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+        s.close()
+    kw = {}
+    backend = "nccl" if info.device.type == "cuda" else "gloo"
+    if backend == "nccl":
+        kw["device_id"] = info.device
+    dist.init_process_group(backend=backend, rank=0, world_size=1, **kw)
+    info.backend = backend
+
+
 class DataParallelRunner:
+    """``force_reduce`` (or ``VINF_FORCE_REDUCE=1``) keeps the bucketed all-reduce on at world
+    size 1 when a process group exists: a 1-rank RCCL communicator then runs the exact
+    collective / stream-ordering / graph-capture path of the multi-GPU job on one GPU."""
+
     def __init__(self, engine, info: DistInfo, bucket_cap_mb: float = 32.0,
-                 compress_bf16: bool = False):
+                 compress_bf16: bool = False, force_reduce: bool = False):
         self.engine = engine
         self.info = info
         self.graph = None
         self.reducer = None
         self._t = int(engine.step_t.item())   # host step counter (fault injection only)
-        if info.world > 1:
+        force = force_reduce or os.environ.get("VINF_FORCE_REDUCE", "0") == "1"
+        if force and info.world == 1 and not dist.is_initialized():
+            _init_single_rank_group(info)
+        if info.world > 1 or (force and dist.is_initialized()):
             P = engine.params
-            dist.broadcast(P.master, 0)
-            P.sync_compute()
+            if info.world > 1:
+                dist.broadcast(P.master, 0)
+                P.sync_compute()
             engine.grad_scale_host = 1.0 / info.world
             self.reducer = BucketedAllReduce(P.grad, engine.layout.unit_ranges,
                                              bucket_cap_mb=bucket_cap_mb,
-                                             compress_bf16=compress_bf16)
+                                             compress_bf16=compress_bf16, force=force)
             engine.unit_ready_hook = self.reducer.mark_ready
 
     def _eager_step(self):
@@ -71,8 +97,10 @@ class DataParallelRunner:
         """Capture one training step into a hipGraph. Returns False if capture is unsupported."""
         if self.engine.device.type != "cuda":
             return False
-        if self.reducer is not None and os.environ.get("VINF_GRAPH_COLLECTIVES", "0") != "1":
-            # collectives inside a captured graph need RCCL graph support; opt-in
+        if self.reducer is not None and os.environ.get("VINF_GRAPH_COLLECTIVES", "1") != "1":
+            # RCCL all-reduces are captured into the step graph by default (tested on a 1-rank
+            # RCCL communicator: tests/test_distributed_gpu.py); VINF_GRAPH_COLLECTIVES=0 keeps
+            # DP steps eager
             return False
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())

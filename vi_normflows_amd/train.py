@@ -106,7 +106,16 @@ def run_planar_vae(cfg, out, info, logger):
     dev = _device(cfg, info)
     g = torch.Generator().manual_seed(rank_seed(cfg.seed, info.rank))
     if cfg.extra.get("data_path"):
-        X = torch.from_numpy(np.load(cfg.extra["data_path"], allow_pickle=False)).float()
+        from .utils.mnist_idx import is_mnist_dir, load_mnist
+
+        dp = cfg.extra["data_path"]
+        if is_mnist_dir(dp):   # the raw idx files: digits {0,1,4,7}, binarised (learning_mnist.py:44-54)
+            X = torch.from_numpy(load_mnist(dp)[0])
+        else:
+            X = torch.from_numpy(np.load(dp, allow_pickle=False)).float()
+        n = int(cfg.extra.get("n_data", 0))
+        if n and X.shape[0] > n:   # the reference trains on a 2000-image subsample (:115-121)
+            X = X[torch.randperm(X.shape[0], generator=torch.Generator().manual_seed(cfg.seed))[:n]]
     else:
         X = synthetic_binary_images(cfg.extra.get("n_data", 2000), cfg.dim, seed=cfg.seed)
     vae = PlanarVAE(VAEConfig(dim_x=cfg.dim, dim_z=cfg.dim_z, K=cfg.K, width=cfg.hidden,
