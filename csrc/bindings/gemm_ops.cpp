@@ -652,7 +652,15 @@ void gemm_fp8_nt(const at::Tensor& xq, const at::Tensor& sx, const at::Tensor& w
 
 void gemm_set_mode(int64_t mode, int64_t depth) { nf_gemm_set_mode((int)mode, (int)depth); }
 
+#ifdef NF_G256_STAMPS
+void nf_g256_set_stamps(void* p);
+void g256_set_stamps(const at::Tensor& buf) { nf_g256_set_stamps(buf.numel() ? buf.data_ptr() : nullptr); }
+#endif
+
 TORCH_LIBRARY_FRAGMENT(vinf, m) {
+#ifdef NF_G256_STAMPS
+  m.def("g256_set_stamps(Tensor buf) -> ()", &g256_set_stamps);
+#endif
   m.def("gemm_set_mode(int mode, int depth) -> ()", &gemm_set_mode);
   m.def("fp8_quant_rows(Tensor x, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("fp8_quant_tensor(Tensor x, Tensor(a!) q, Tensor amax_prev, Tensor(b!) scale, Tensor(c!) amax_cur) -> ()");

@@ -64,27 +64,39 @@ def _run(cmd: list[str]) -> None:
 
 
 def build(force: bool = False, jobs: int | None = None, debug: bool = False,
-          save_temps: bool = False, verbose: bool = True) -> Path:
+          save_temps: bool = False, verbose: bool = True, variant: str = "",
+          defines: list[str] | None = None, asan: bool = False) -> Path:
+    """Build the library. ``variant`` builds ``libvinf_hip_<variant>.so`` from its own object
+    directory (A/B experiments, loaded with ``VINF_NATIVE_LIB``); ``defines`` adds ``-D`` macros
+    to the kernel units; ``asan`` instruments the HOST code only (``-Xarch_host
+    -fsanitize=address``; device code is never sanitized on this pool) - run it with the
+    ASan runtime preloaded (``tools/asan_run.sh``)."""
     hipcc = _hipcc()
     incs, libdirs, abi = _torch_paths()
-    OBJ_DIR.mkdir(parents=True, exist_ok=True)
+    if asan and not variant:
+        variant = "asan"
+    obj_dir = OBJ_DIR / variant if variant else OBJ_DIR
+    out_lib = OUT_DIR / f"libvinf_hip_{variant}.so" if variant else OUT_LIB
+    obj_dir.mkdir(parents=True, exist_ok=True)
     OUT_DIR.mkdir(parents=True, exist_ok=True)
     headers = _headers()
     opt = ["-O0", "-g"] if debug else ["-O3"]
     common = ["-std=c++17", "-fPIC", f"-I{CSRC / 'include'}", "-Wno-unused-result",
-              "-Wno-deprecated-declarations"]
-    kernel_flags = common + opt + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+              "-Wno-deprecated-declarations"] + [f"-D{d}" for d in (defines or [])]
+    san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer", "-g"] \
+        if asan else []
+    kernel_flags = common + opt + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"] + san
     if save_temps:
         kernel_flags += ["-save-temps=obj"]
-    bind_flags = common + ["-O2", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
+    bind_flags = common + ["-O1" if asan else "-O2", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
                            f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
-                           "-DTORCH_API_INCLUDE_EXTENSION_H"] + [f"-I{p}" for p in incs]
+                           "-DTORCH_API_INCLUDE_EXTENSION_H"] + [f"-I{p}" for p in incs] + san
     jobs_list = []
     for src in sorted((CSRC / "kernels").glob("*.hip")):
-        obj = OBJ_DIR / (src.stem + ".o")
+        obj = obj_dir / (src.stem + ".o")
         jobs_list.append((src, obj, [hipcc, "-c", *kernel_flags, "-o", str(obj), str(src)]))
     for src in sorted((CSRC / "bindings").glob("*.cpp")):
-        obj = OBJ_DIR / ("bind_" + src.stem + ".o")
+        obj = obj_dir / ("bind_" + src.stem + ".o")
         jobs_list.append((src, obj, [hipcc, "-c", *bind_flags, "-o", str(obj), str(src)]))
     todo = [j for j in jobs_list if force or _stale(j[1], j[0], headers)]
     n = jobs or min(8, os.cpu_count() or 4)
@@ -97,17 +109,19 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False,
             for f in futs:
                 f.result()
     objs = [str(o) for _, o, _ in jobs_list]
-    need_link = force or not OUT_LIB.exists() or any(
-        Path(o).stat().st_mtime > OUT_LIB.stat().st_mtime for o in objs)
+    need_link = force or not out_lib.exists() or any(
+        Path(o).stat().st_mtime > out_lib.stat().st_mtime for o in objs)
     if need_link:
-        link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(OUT_LIB), *objs]
+        link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(out_lib), *objs]
+        if asan:
+            link += ["-fsanitize=address", "-shared-libasan"]
         for d in libdirs:
             link += [f"-L{d}", f"-Wl,-rpath,{d}"]
         link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lamdhip64"]
         _run(link)
         if verbose:
-            print(f"[vinf build] linked {OUT_LIB.relative_to(ROOT)}", file=sys.stderr)
-    return OUT_LIB
+            print(f"[vinf build] linked {out_lib.relative_to(ROOT)}", file=sys.stderr)
+    return out_lib
 
 
 def main() -> None:
@@ -116,8 +130,14 @@ def main() -> None:
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--save-temps", action="store_true")
+    ap.add_argument("--variant", default="", help="build libvinf_hip_<variant>.so")
+    ap.add_argument("-D", dest="defines", action="append", default=[],
+                    help="extra preprocessor define for the kernel units (repeatable)")
+    ap.add_argument("--asan", action="store_true",
+                    help="AddressSanitizer on the host code (bindings + launchers) only")
     a = ap.parse_args()
-    build(force=a.force, jobs=a.jobs, debug=a.debug, save_temps=a.save_temps)
+    build(force=a.force, jobs=a.jobs, debug=a.debug, save_temps=a.save_temps,
+          variant=a.variant, defines=a.defines, asan=a.asan)
 
 
 if __name__ == "__main__":

@@ -154,6 +154,14 @@ void nf_launch_planar_bwd(const float* saved, const float* W, const float* U, co
                           const float* gz, const float* gl, float* dz, float* dW, float* dU,
                           float* dB, int N, int D, int K, int per_sample, int broadcast,
                           hipStream_t stream);
+// shared parameters, D <= 16, K * per(D) <= 256: recompute-from-z0 backward with in-kernel
+// parameter-gradient reduction (part: nblk * K * (2 per + 1) floats)
+int nf_planar_shared_per(int D);
+int nf_planar_shared_blocks(int N);
+void nf_launch_planar_bwd_shared(const float* z0, const float* W, const float* U, const float* B,
+                                 const float* gz, const float* gl, float* dz, float* dW, float* dU,
+                                 float* dB, float* part, int nblk, int N, int D, int K,
+                                 int broadcast, hipStream_t stream);
 void nf_launch_radial_fwd(const float* z, const float* Z0, const float* AL, const float* BE,
                           float* zK, float* ldj, float* saved, int N, int D, int K,
                           int per_sample, hipStream_t stream);

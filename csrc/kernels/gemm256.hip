@@ -29,6 +29,25 @@
 // on each SIMD one wave issues its LDS reads / DMA while the other runs MFMAs.
 #include "gemm_tile.h"
 
+// Diagnostic build only (csrc/build.py --variant stamps -D NF_G256_STAMPS): every block records
+// s_memrealtime (100 MHz, chip-global) at body entry, after the prologue wait, after the main
+// loop, after issuing the epilogue, and after its stores have drained, into a buffer set with
+// torch.ops.vinf.g256_set_stamps (8 slots per block). The shipped library compiles none of it.
+#ifdef NF_G256_STAMPS
+__device__ unsigned long long* nf_g256_stamp_buf;
+#define NF_STAMP(i)                                                                            \
+  do {                                                                                         \
+    unsigned long long t_;                                                                     \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");             \
+    unsigned long long* b_ = nf_g256_stamp_buf;                                                \
+    if (threadIdx.x == 0 && b_) b_[((long)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = t_; \
+  } while (0)
+#else
+#define NF_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+
 namespace nf {
 namespace gemm {
 namespace g256 {
@@ -353,11 +372,13 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
     return c < 0 ? 0 : (c > D ? D : c);
   };
 
+  NF_STAMP(0);
   if (nkt > 0) {
 #pragma unroll
     for (int h = 0; h < 6 + X; ++h) issue_h(h);   // every half issued at phase <= 0
     vmwait_count<D>(outstanding(0));
     barrier();
+    NF_STAMP(1);
     if (wr == 1) barrier();
 
     v8s fa[4][2], fbl[2][2], fbh[2][2];
@@ -425,6 +446,7 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
     }
     if (wr == 0) barrier();
   }
+  NF_STAMP(2);
 
   // ---------------------------------------------------------------- epilogue
   // acc[i][j]: n = n0 + wc*64 + i*16 + (lane>>4)*4 + r, m = m0 + wr*128 + j*16 + (lane&15)
@@ -439,12 +461,22 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   if constexpr (EPI == EPI_CPL_FWD) {
     barrier();  // every wave is past its last operand read
     epi_coupling_fwd(a, acc, m0, n0, wr, wc, smem, lane);
+#ifdef NF_G256_STAMPS
+    NF_STAMP(3);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    NF_STAMP(4);
+#endif
     return;
   }
   if (a.staged) {
     barrier();  // every wave is past its last operand read; each wave reuses 16 KiB of LDS
     epi_tile_staged<EPI, 8, F8>(a, acc, m0 + wr * 128, n0 + wc * 64, split,
                                 smem + wave * 16384, lane);
+#ifdef NF_G256_STAMPS
+    NF_STAMP(3);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    NF_STAMP(4);
+#endif
     return;
   }
 #pragma unroll
@@ -861,3 +893,9 @@ void nf_launch_gemm256_tn_group(const GroupArgs& g, hipStream_t stream) {
                        stream, g);
   NF_HIP_CHECK(hipGetLastError());
 }
+
+#ifdef NF_G256_STAMPS
+void nf_g256_set_stamps(void* p) {
+  NF_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(nf_g256_stamp_buf), &p, sizeof(p)));
+}
+#endif

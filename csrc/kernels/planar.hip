@@ -18,6 +18,14 @@
 
 namespace nf {
 
+// log|psi| is evaluated as log(|psi| + eps) (the reference's guard, optimization.py:83,
+// get_data.py:107): psi = 1 + h' w.u_hat can reach 0 exactly, e.g. in the broadcast variant.
+// Its derivative sign(psi) / (|psi| + eps) stays finite there.
+constexpr float kPsiEps = 1e-7f;
+__device__ __forceinline__ float dlog_guard(float psi) {
+  return copysignf(1.f / (fabsf(psi) + kPsiEps), psi);
+}
+
 template <bool WROW>
 __device__ __forceinline__ float rsum(float v) {
   if (WROW) return wave_sum(v);
@@ -78,14 +86,14 @@ __global__ void __launch_bounds__(256) planar_fwd_kernel(PlanarArgs a) {
     const float b = a.per_sample ? a.Bv[(long)k * a.N + row] : a.Bv[k];
     float w[PER], u[PER];
     float dot = 0.f, su = 0.f, sw = 0.f, eta = 0.f;
-    float* sv = a.saved + ((long)k * a.N + row) * D;
+    float* sv = a.saved ? a.saved + ((long)k * a.N + row) * D : nullptr;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int j = elem<WROW, PER>(i, lane);
       if (j < D) {
         w[i] = a.W[pbase + j];
         u[i] = a.U[pbase + j];
-        sv[j] = z[i];
+        if (sv) sv[j] = z[i];
       } else {
         w[i] = 0.f;
         u[i] = 0.f;
@@ -111,7 +119,7 @@ __global__ void __launch_bounds__(256) planar_fwd_kernel(PlanarArgs a) {
 #pragma unroll
       for (int i = 0; i < PER; ++i) z[i] += u[i] * h;
     }
-    ldj += __logf(fabsf(psi));
+    ldj += __logf(fabsf(psi) + kPsiEps);
   }
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
@@ -169,7 +177,7 @@ __global__ void __launch_bounds__(256) planar_bwd_kernel(PlanarArgs a) {
       sw = rsum<WROW>(sw);
       gsum = rsum<WROW>(gsum);
       const float psi = 1.f + hp * su * sw;
-      const float ipsi = 1.f / psi;
+      const float ipsi = dlog_guard(psi);
       da = gsum * su * hp + c * hpp * su * sw * ipsi;
       const float du = gsum * h + c * hp * sw * ipsi;
       const float dwc = c * hp * su * ipsi;
@@ -185,8 +193,9 @@ __global__ void __launch_bounds__(256) planar_bwd_kernel(PlanarArgs a) {
       eta = rsum<WROW>(eta);
       gu = rsum<WROW>(gu);
       const float psi = 1.f + hp * eta;
-      const float r = c * hp / psi;
-      da = gu * hp + c * hpp * eta / psi;
+      const float ipsi = dlog_guard(psi);
+      const float r = c * hp * ipsi;
+      da = gu * hp + c * hpp * eta * ipsi;
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const int j = elem<WROW, PER>(i, lane);
@@ -205,6 +214,145 @@ __global__ void __launch_bounds__(256) planar_bwd_kernel(PlanarArgs a) {
     const int j = elem<WROW, PER>(i, lane);
     if (j < D) a.dz[row * D + j] = g[i];
   }
+}
+
+// Shared (non-amortized) parameters, D <= 16, K * PER <= 256: the backward recomputes every
+// layer's input from z0 into LDS (no [K][N][D] saved-state buffer in HBM) and reduces the
+// parameter gradients inside the kernel: one wave per block walks rows (grid-stride), each
+// layer's dU / dW / db contributions are wave-summed and accumulated in LDS, and every block
+// writes ONE partial [K][2 PER + 1] row; a fixed-order finalize sums the partials (bitwise
+// reproducible). HBM traffic per row: z0, gz, dz, one ldj-gradient scalar; O(K D) parameter
+// gradients instead of the O(K N D) per-row buffers of the generic path.
+template <int PER>
+__global__ void __launch_bounds__(64) planar_bwd_shared_kernel(PlanarArgs a, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x;
+  const int K = a.K, D = a.D;
+  constexpr int NV = 2 * PER + 1;
+  float* st = lds;                       // [K][PER][64]
+  float* acc = lds + K * PER * 64;       // [K][NV]
+  for (int i = lane; i < K * NV; i += 64) acc[i] = 0.f;
+  __syncthreads();
+  for (long row0 = (long)blockIdx.x * 64; row0 < a.N; row0 += (long)gridDim.x * 64) {
+    const long row = row0 + lane;
+    const bool valid = row < a.N;
+    float z[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) z[i] = (valid && i < D) ? a.z[row * D + i] : 0.f;
+    for (int k = 0; k < K; ++k) {        // forward recompute, inputs of every layer -> LDS
+      float dot = 0.f, su = 0.f;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        st[(k * PER + i) * 64 + lane] = z[i];
+        const float w = i < D ? a.W[k * D + i] : 0.f;
+        dot += z[i] * w;
+        su += i < D ? a.U[k * D + i] : 0.f;
+      }
+      const float h = tanhf(dot + a.Bv[k]);
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const float u = i < D ? a.U[k * D + i] : 0.f;
+        z[i] += (a.broadcast ? su : u) * h;
+      }
+    }
+    float g[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) g[i] = (valid && i < D) ? a.gz[row * D + i] : 0.f;
+    const float c = valid ? a.gl[row] : 0.f;
+    for (int k = K - 1; k >= 0; --k) {
+      float w[PER], u[PER];
+      float dot = 0.f, su = 0.f, sw = 0.f, eta = 0.f, gsum = 0.f, gu = 0.f;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        w[i] = i < D ? a.W[k * D + i] : 0.f;
+        u[i] = i < D ? a.U[k * D + i] : 0.f;
+        z[i] = st[(k * PER + i) * 64 + lane];
+        dot += z[i] * w[i];
+        su += u[i];
+        sw += w[i];
+        eta += w[i] * u[i];
+        gsum += g[i];
+        gu += g[i] * u[i];
+      }
+      const float h = tanhf(dot + a.Bv[k]);
+      const float hp = 1.f - h * h;
+      const float hpp = -2.f * h * hp;
+      float da, cu[PER], cw[PER];
+      if (a.broadcast) {
+        const float ipsi = dlog_guard(1.f + hp * su * sw);
+        da = gsum * su * hp + c * hpp * su * sw * ipsi;
+        const float du = gsum * h + c * hp * sw * ipsi;
+        const float dwc = c * hp * su * ipsi;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) { cu[i] = du; cw[i] = da * z[i] + dwc; }
+      } else {
+        const float ipsi = dlog_guard(1.f + hp * eta);
+        const float r = c * hp * ipsi;
+        da = gu * hp + c * hpp * eta * ipsi;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) { cu[i] = g[i] * h + r * w[i]; cw[i] = da * z[i] + r * u[i]; }
+      }
+      if (!valid) {
+        da = 0.f;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) cu[i] = cw[i] = 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        if (i < D) {
+          const float su_ = wave_sum(cu[i]);
+          const float sw_ = wave_sum(cw[i]);
+          if (lane == 0) {
+            acc[k * NV + i] += su_;
+            acc[k * NV + PER + i] += sw_;
+          }
+        }
+      }
+      const float sb = wave_sum(da);
+      if (lane == 0) acc[k * NV + 2 * PER] += sb;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) g[i] += da * w[i];
+    }
+    if (valid) {
+#pragma unroll
+      for (int i = 0; i < PER; ++i)
+        if (i < D) a.dz[row * D + i] = g[i];
+    }
+  }
+  __syncthreads();
+  for (int i = lane; i < K * NV; i += 64) part[(long)blockIdx.x * K * NV + i] = acc[i];
+}
+
+// dU[k][j], dW[k][j], dB[k] = sum over blocks of the partials, in block order (one block per
+// output value, strided partial sums + a fixed-shape tree)
+__global__ void __launch_bounds__(256) planar_shared_finalize_kernel(
+    const float* __restrict__ part, int nblk, int K, int D, int PER, float* dW, float* dU,
+    float* dB) {
+  __shared__ float scratch[16];
+  const int NV = 2 * PER + 1;
+  const int kv = blockIdx.x, k = kv / NV, v = kv % NV;
+  float acc = 0.f;
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x) acc += part[(long)b * K * NV + kv];
+  acc = block_sum(acc, scratch);
+  if (threadIdx.x == 0) {
+    if (v < PER) {
+      if (v < D) dU[k * D + v] = acc;
+    } else if (v < 2 * PER) {
+      if (v - PER < D) dW[k * D + (v - PER)] = acc;
+    } else {
+      dB[k] = acc;
+    }
+  }
+}
+
+template <int PER>
+static void launch_planar_shared(const PlanarArgs& a, float* part, int nblk, hipStream_t stream) {
+  const size_t lds = ((size_t)a.K * PER * 64 + (size_t)a.K * (2 * PER + 1)) * sizeof(float);
+  hipLaunchKernelGGL((planar_bwd_shared_kernel<PER>), dim3(nblk), dim3(64), lds, stream, a, part);
+  NF_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(planar_shared_finalize_kernel, dim3(a.K * (2 * PER + 1)), dim3(256), 0, stream,
+                     part, nblk, a.K, a.D, PER, a.dW, a.dU, a.dB);
+  NF_HIP_CHECK(hipGetLastError());
 }
 
 template <bool WROW, int PER>
@@ -255,4 +403,29 @@ void nf_launch_planar_bwd(const float* saved, const float* W, const float* U, co
   a.dW = dW; a.dU = dU; a.dB = dB;
   a.N = N; a.D = D; a.K = K; a.per_sample = per_sample; a.broadcast = broadcast;
   dispatch_planar(a, true, stream);
+}
+
+int nf_planar_shared_per(int D) { return D <= 2 ? 2 : D <= 4 ? 4 : D <= 8 ? 8 : D <= 16 ? 16 : 0; }
+
+int nf_planar_shared_blocks(int N) {
+  const long b = ((long)N + 63) / 64;
+  return (int)(b < 4096 ? (b < 1 ? 1 : b) : 4096);
+}
+
+void nf_launch_planar_bwd_shared(const float* z0, const float* W, const float* U, const float* B,
+                                 const float* gz, const float* gl, float* dz, float* dW, float* dU,
+                                 float* dB, float* part, int nblk, int N, int D, int K,
+                                 int broadcast, hipStream_t stream) {
+  if (N <= 0) return;
+  PlanarArgs a{};
+  a.z = z0; a.W = W; a.U = U; a.Bv = B; a.gz = gz; a.gl = gl; a.dz = dz;
+  a.dW = dW; a.dU = dU; a.dB = dB;
+  a.N = N; a.D = D; a.K = K; a.per_sample = 0; a.broadcast = broadcast;
+  switch (nf_planar_shared_per(D)) {
+    case 2: return launch_planar_shared<2>(a, part, nblk, stream);
+    case 4: return launch_planar_shared<4>(a, part, nblk, stream);
+    case 8: return launch_planar_shared<8>(a, part, nblk, stream);
+    case 16: return launch_planar_shared<16>(a, part, nblk, stream);
+    default: break;
+  }
 }

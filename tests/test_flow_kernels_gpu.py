@@ -93,3 +93,56 @@ def test_flow_vi_on_gpu_planar_u1(gpu):
                     device=gpu, log_every=100)
     assert r.final["free_energy"] > -r.final["logZ"] - 0.05   # KL floor
     assert r.history[-1]["F"] < r.history[0]["F"]
+
+
+def test_planar_shared_4m_samples_without_knd_buffers(gpu):
+    """U1-style non-amortized planar VI at 4 M samples per step: the shared-parameter path keeps
+    no [K, N, D] state or per-row gradient buffers (recompute in LDS, in-kernel reduction);
+    gradients match the fp64 composite."""
+    N, D, K = 4 * 1024 * 1024, 2, 32
+    torch.manual_seed(7)
+    z = torch.randn(N, D, device=gpu)
+    W = (torch.randn(K, D, device=gpu) * 0.7).requires_grad_(True)
+    U = (torch.randn(K, D, device=gpu) * 0.7).requires_grad_(True)
+    B = torch.randn(K, device=gpu).requires_grad_(True)
+    gz = torch.randn(N, D, device=gpu)
+    gl = torch.randn(N, device=gpu)
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats()
+    base = torch.cuda.memory_allocated()
+    zK, ldj = _PlanarStackFn.apply(z, W, get_uhat(U, W), B, False)
+    gW, gU, gB = torch.autograd.grad((zK * gz).sum() + (ldj * gl).sum(), [W, U, B])
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated() - base
+    knd = K * N * D * 4
+    assert peak < 0.5 * knd, (peak, knd)     # inputs/outputs are O(N D); no O(K N D) buffer
+    Wd, Ud, Bd = (t.detach().double().requires_grad_(True) for t in (W, U, B))
+    zr, lr = planar_stack_reference(z.double(), Wd, Ud, Bd, "paper", "exact")
+    rW, rU, rB = torch.autograd.grad((zr * gz.double()).sum() + (lr * gl.double()).sum(),
+                                     [Wd, Ud, Bd])
+    assert torch.allclose(zK.double(), zr, atol=2e-4, rtol=1e-4)
+    for a, b in ((gW, rW), (gU, rU), (gB, rB)):
+        assert (a.double() - b).abs().max() <= 1e-4 * (1 + b.abs().max()), (a.double() - b).abs().max()
+
+
+@pytest.mark.parametrize("per_sample", [False, True])
+def test_planar_psi_zero_is_guarded(gpu, per_sample):
+    """w.u_hat = -1 and a = 0 (h' = 1) give psi = 1 + h' w.u_hat = 0 exactly: the log-det is
+    log(0 + 1e-7) (the reference's eps guard) and every gradient stays finite."""
+    N, D = 64, 2
+    z = torch.zeros(N, D, device=gpu, requires_grad=True)
+    shp = (1, N, D) if per_sample else (1, D)
+    W = torch.zeros(*shp, device=gpu)
+    W[..., 0] = 1.0
+    U = torch.zeros(*shp, device=gpu)
+    U[..., 0] = -30.0            # m(w.u) = -1 + softplus(-30) == -1 in fp32 -> w.u_hat = -1
+    W.requires_grad_(True)
+    U.requires_grad_(True)
+    B = torch.zeros(*shp[:-1], device=gpu, requires_grad=True)
+    Uh = get_uhat(U, W)
+    assert float((W * Uh).sum(-1).flatten()[0]) == -1.0
+    zK, ldj = _PlanarStackFn.apply(z, W, Uh, B, False)
+    assert torch.isfinite(ldj).all() and abs(float(ldj[0]) - float(torch.log(torch.tensor(1e-7)))) < 1e-3
+    g = torch.autograd.grad(ldj.sum() + zK.sum(), [z, W, U, B])
+    for t in g:
+        assert torch.isfinite(t).all()

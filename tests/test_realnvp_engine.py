@@ -15,7 +15,7 @@ def autograd_free_energy(eng: RealNVPVI, params: dict, eps: torch.Tensor, beta: 
     z0 = mu + torch.exp(0.5 * lv) * eps
     logq0 = -0.5 * cfg.dim * math.log(2 * math.pi) - 0.5 * lv.sum() - 0.5 * (eps * eps).sum(1)
     h = [z0[:, Dh:], z0[:, :Dh]]
-    ldj = torch.zeros(eps.shape[0])
+    ldj = torch.zeros(eps.shape[0], device=eps.device, dtype=eps.dtype)
     for l in range(L):
         a = h[l + 1]
         for i in range(nh):

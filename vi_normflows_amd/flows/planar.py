@@ -83,13 +83,13 @@ def planar_stack_reference(z, W, U, B, variant="paper", ldj="exact", uhat_norm="
             if ldj == "reference":
                 ld = ld + torch.log(EPS + torch.abs(1.0 + hp * u.sum(-1) * sw))
             else:
-                ld = ld + torch.log(torch.abs(1.0 + hp * su * sw))
+                ld = ld + torch.log(EPS + torch.abs(1.0 + hp * su * sw))
             z = z + (su * hv).unsqueeze(-1)
         else:
             if ldj == "reference":
                 ld = ld + torch.log(EPS + torch.abs(1.0 + hp * (w * u).sum(-1)))
             else:
-                ld = ld + torch.log(torch.abs(1.0 + hp * (w * uh).sum(-1)))
+                ld = ld + torch.log(EPS + torch.abs(1.0 + hp * (w * uh).sum(-1)))
             z = z + uh * hv.unsqueeze(-1)
     if return_states:
         return z, ld, states
@@ -97,12 +97,20 @@ def planar_stack_reference(z, W, U, B, variant="paper", ldj="exact", uhat_norm="
 
 
 class _PlanarStackFn(torch.autograd.Function):
-    """Fused HIP planar stack (paper/broadcast update, exact log-det)."""
+    """Fused HIP planar stack (paper/broadcast update, exact log-det with the reference's
+    log(|psi| + 1e-7) guard).
+
+    Shared parameters with D <= 16 and K * per(D) <= 256 (the energy-potential / 1-D GMM
+    regimes, up to millions of MC samples) take the recompute path: the forward keeps no
+    per-layer states, and the backward kernel recomputes them from z0 in LDS and reduces the
+    parameter gradients in-kernel (O(K D) outputs + small per-block partials). Otherwise the
+    forward saves every layer's input [K, N, D] and the backward writes per-row gradients."""
 
     @staticmethod
     def forward(ctx, z, W, Uh, B, broadcast: bool):
         from ..ops._ext import native
 
+        ops = native()
         K = W.shape[0]
         N, D = z.shape
         per_sample = W.dim() == 3
@@ -110,26 +118,43 @@ class _PlanarStackFn(torch.autograd.Function):
         Wc, Uc, Bc = W.contiguous().float(), Uh.contiguous().float(), B.contiguous().float()
         zK = torch.empty_like(zc)
         ldj = torch.empty(N, device=z.device, dtype=torch.float32)
-        saved = torch.empty(K, N, D, device=z.device, dtype=torch.float32)
-        native().planar_stack_fwd(zc, Wc, Uc, Bc, per_sample, broadcast, zK, ldj, saved)
-        ctx.save_for_backward(saved, Wc, Uc, Bc)
-        ctx.flags = (per_sample, broadcast)
+        ws = -1 if per_sample else int(ops.planar_shared_workspace(N, D, K))
+        if ws > 0:
+            saved = torch.empty(0, device=z.device, dtype=torch.float32)
+            ops.planar_stack_fwd(zc, Wc, Uc, Bc, False, broadcast, zK, ldj, saved)
+            ctx.save_for_backward(zc, Wc, Uc, Bc)
+        else:
+            saved = torch.empty(K, N, D, device=z.device, dtype=torch.float32)
+            ops.planar_stack_fwd(zc, Wc, Uc, Bc, per_sample, broadcast, zK, ldj, saved)
+            ctx.save_for_backward(saved, Wc, Uc, Bc)
+        ctx.flags = (per_sample, broadcast, ws)
         return zK, ldj
 
     @staticmethod
     def backward(ctx, gz, gldj):
         from ..ops._ext import native
 
-        saved, W, Uh, B = ctx.saved_tensors
-        per_sample, broadcast = ctx.flags
-        K, N, D = saved.shape
+        first, W, Uh, B = ctx.saved_tensors
+        per_sample, broadcast, ws = ctx.flags
+        K = W.shape[0]
+        if ws > 0:
+            N, D = first.shape
+        else:
+            _, N, D = first.shape
         gz = (gz if gz is not None else torch.zeros(N, D, device=W.device)).contiguous().float()
         gl = (gldj if gldj is not None else torch.zeros(N, device=W.device)).contiguous().float()
         dz = torch.empty(N, D, device=W.device, dtype=torch.float32)
+        if ws > 0:
+            dW = torch.empty(K, D, device=W.device, dtype=torch.float32)
+            dU, dB = torch.empty_like(dW), torch.empty(K, device=W.device, dtype=torch.float32)
+            part = torch.empty(ws, device=W.device, dtype=torch.float32)
+            native().planar_stack_bwd_shared(first, W, Uh, B, broadcast, gz, gl, dz, dW, dU, dB,
+                                             part)
+            return dz, dW, dU, dB, None
         dW = torch.empty(K, N, D, device=W.device, dtype=torch.float32)
         dU = torch.empty(K, N, D, device=W.device, dtype=torch.float32)
         dB = torch.empty(K, N, device=W.device, dtype=torch.float32)
-        native().planar_stack_bwd(saved, W, Uh, B, per_sample, broadcast, gz, gl, dz, dW, dU, dB)
+        native().planar_stack_bwd(first, W, Uh, B, per_sample, broadcast, gz, gl, dz, dW, dU, dB)
         if not per_sample:
             dW, dU, dB = dW.sum(1), dU.sum(1), dB.sum(1)
         return dz, dW, dU, dB, None
