@@ -395,49 +395,63 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
       if (lane == 0) amax_slot_atomic(a.f8_q_amax_cur, qamax);
     }
   } else {
+    // fp32 path: passes of 32 rows (8 KiB of the wave's region). Every global operand a pass
+    // reads (old C, and for EPI_CPL_BWD s_hat and x) is loaded for all its rows before the LDS
+    // readback, from clamped addresses, so a pass waits out ONE load round trip. (Loading s_hat
+    // / x per row inside the readback loop serialised 32 round trips per wave: the fused
+    // coupling-backward epilogue took 52.6 us per tile, profiles/r2_g256_stamps_b65536.jsonl.)
+    constexpr int PJ = 2;             // 16-row accumulator blocks per pass
+    constexpr int PIT = PJ * 4;       // readback iterations (4 rows each) per pass
 #pragma unroll
-    for (int hj = 0; hj < NJ / 4; ++hj) {
+    for (int hj = 0; hj < NJ / PJ; ++hj) {
       if (hj) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
+      for (int jj = 0; jj < PJ; ++jj) {
         const int row = jj * 16 + c;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          *(LDS_AS v4f*)(region + row * 256 + (((i * 4 + g) ^ (row & 7)) << 4)) = acc[i][hj * 4 + jj];
+          *(LDS_AS v4f*)(region + row * 256 + (((i * 4 + g) ^ (row & 7)) << 4)) = acc[i][hj * PJ + jj];
       }
-      // old C (fp32 accumulate) rows, in flight while the LDS writes drain
+      // global operands of this pass's rows, in flight while the LDS writes drain
       const int q = lane & 15;
-      float4 cv[16];
+      float4 cv[PIT];
+      float4 xp[PIT];
+      ushort4 sp[PIT];
       if constexpr (EPI == EPI_F32_ACC || EPI == EPI_CPL_BWD) {
 #pragma unroll
-        for (int it = 0; it < 16; ++it) {
-          int m = m0 + hj * 64 + it * 4 + (lane >> 4), n = n0 + q * 4;
+        for (int it = 0; it < PIT; ++it) {
+          int m = m0 + hj * 16 * PJ + it * 4 + (lane >> 4), n = n0 + q * 4;
           m = m < a.M ? m : a.M - 1;
           n = n < a.N ? n : a.N - 4;
           cv[it] = *reinterpret_cast<const float4*>((const float*)a.C + (long)m * a.ldc + n);
+          if constexpr (EPI == EPI_CPL_BWD) {
+            const int nx = n < a.cpl_dh ? n : a.cpl_dh - 4;
+            sp[it] = *reinterpret_cast<const ushort4*>(a.aux + (long)m * a.ld_aux + nx);
+            xp[it] = *reinterpret_cast<const float4*>(a.cpl_x + (long)m * a.ld_cpl_x + nx);
+          }
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int it = 0; it < 16; ++it) {
+      for (int it = 0; it < PIT; ++it) {
         const int row = it * 4 + (lane >> 4);
         v4f v = *(const LDS_AS v4f*)(region + row * 256 + ((q ^ (row & 7)) << 4));
-        const int m = m0 + hj * 64 + row, n = n0 + q * 4;
+        const int m = m0 + hj * 16 * PJ + row, n = n0 + q * 4;
         if (m < a.M && n < a.N) {
           if constexpr (EPI == EPI_CPL_BWD) {
             const float4 o = cv[it];
             const float gy[4] = {o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]};
             bf16_t* drow = a.cpl_dst + (long)m * a.ld_cpl_dst;
             if (n < a.cpl_dh) {
-              const ushort4 sh = *reinterpret_cast<const ushort4*>(a.aux + (long)m * a.ld_aux + n);
-              const float4 xv = *reinterpret_cast<const float4*>(a.cpl_x + (long)m * a.ld_cpl_x + n);
+              const ushort4 sh = sp[it];
+              const float4 xv = xp[it];
               const float shv[4] = {bf2f(sh.x), bf2f(sh.y), bf2f(sh.z), bf2f(sh.w)};
               const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
               const float inv = 1.0f / a.cpl_scale;
               float gx[4], dsh[4];
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
-                const float sv = a.cpl_scale * tanhf(shv[e]);
+                const float sv = a.cpl_scale * fast_tanhf(shv[e]);
                 const float es = __expf(sv);
                 const float ds = fmaf(gy[e] * xs[e], es, a.cpl_c);
                 dsh[e] = ds * (a.cpl_scale - sv * sv * inv);

@@ -75,6 +75,15 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
   return r;
 }
 
+// tanh for the affine-coupling scale s = c tanh(s_hat): sign(x) (1 - 2 / (1 + e^{2|x|})), one
+// v_exp_f32 + one v_rcp_f32 (libm tanhf is a ~25-instruction branchy sequence, and the fused
+// coupling epilogues evaluate it for every element of a 256-row tile while no MFMA runs).
+// Absolute error ~1e-7 (the s_hat it reads is bf16); e^{2|x|} = inf gives exactly +-1.
+__device__ __forceinline__ float fast_tanhf(float x) {
+  const float e = __expf(2.f * fabsf(x));
+  return copysignf(1.f - __fdividef(2.f, 1.f + e), x);
+}
+
 // Numerically stable softplus and log(1+x) helpers used by flow kernels.
 __device__ __forceinline__ float softplusf(float x) {
   return x > 20.f ? x : log1pf(__expf(x));

@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(256) coupling_fwd_kernel(
   for (int j = lane; j < Dh; j += 64) {
     const float sh = ld_st<TS>(st_r, j);
     const float t = ld_st<TS>(st_r, j + Dh);
-    const float s = scale * tanhf(sh);
+    const float s = scale * fast_tanhf(sh);
     const float xv = x_r[j];
     float yv;
     if (INVERSE) {
@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(256) coupling_fwd_vec_kernel(
     ld4(x + row * ld_x + j, xv);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      sv[e] = scale * tanhf(sh[e]);
+      sv[e] = scale * fast_tanhf(sh[e]);
       yv[e] = INVERSE ? (xv[e] - t[e]) * __expf(-sv[e]) : fmaf(xv[e], __expf(sv[e]), t[e]);
       acc += sv[e];
     }
@@ -175,7 +175,7 @@ __global__ void __launch_bounds__(256) coupling_bwd_vec_kernel(
     if (SH) {
       ld4(reinterpret_cast<const bf16_t*>(s_in) + row * ld_s + j, sv);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) sv[e] = scale * tanhf(sv[e]);
+      for (int e = 0; e < 4; ++e) sv[e] = scale * fast_tanhf(sv[e]);
     } else {
       ld4(reinterpret_cast<const float*>(s_in) + row * ld_s + j, sv);
     }

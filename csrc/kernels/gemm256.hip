@@ -243,7 +243,7 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
           const unsigned us = sh[e >> 1], ut = tt[e >> 1];
           const float shv = __uint_as_float((e & 1) ? (us & 0xffff0000u) : (us << 16));
           const float tv = __uint_as_float((e & 1) ? (ut & 0xffff0000u) : (ut << 16));
-          const float sv = a.cf_scale * tanhf(shv);
+          const float sv = a.cf_scale * fast_tanhf(shv);
           y[e] = fmaf(xs[e], __expf(sv), tv);
           part += sv;
         }
@@ -382,10 +382,25 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
     if (wr == 1) barrier();
 
     v8s fa[4][2], fbl[2][2], fbh[2][2];
-    for (int t = 0; t < nkt; ++t) {
-      const bool two = F8 || (t >= n1 ? (kend2 - (kbeg2 + (t - n1) * BK)) > 32
-                                       : (kend - (kbeg + t * BK)) > 32);
+    // One K-tile (4 phases). STEADY: every half this K-tile issues exists (t + 2 < nkt) and
+    // the K-tile is a whole 64-deep step, so the issue bound checks, the runtime vmcnt ladder
+    // and the tail branch inside the MFMA cluster all fold away (straight-line phases with a
+    // fixed vmcnt(2D)); the generic form runs the last two K-tiles.
+    auto ktile = [&](int t, auto steady_c) {
+      constexpr bool S = decltype(steady_c)::value;
+      const bool two = S || F8 ||
+                       (t >= n1 ? (kend2 - (kbeg2 + (t - n1) * BK)) > 32
+                                : (kend - (kbeg + t * BK)) > 32);
       const int P = 4 * t;
+      auto issue_wait = [&](int h, int p) {
+        if constexpr (S) {
+          issue(h >> 2, h & 3);
+          vmwait<2 * D>();
+        } else {
+          issue_h(h);
+          vmwait_count<D>(outstanding(p));
+        }
+      };
       // ---- r1: M0-3 x N0-1
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -397,8 +412,7 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
           fa[j][ks] = read_frag<A_KMAJOR>(slot(t, H_ALO), wr * 64 + j * 16, ks, lane);
-      issue_h(4 * t + 6 + X);
-      vmwait_count<D>(outstanding(P + 1));
+      issue_wait(4 * t + 6 + X, P + 1);
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
@@ -412,8 +426,7 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
           fbh[i][ks] = read_frag<B_KMAJOR>(slot(t, H_BHI), wc * 32 + i * 16, ks, lane);
-      issue_h(4 * t + 7 + X);
-      vmwait_count<D>(outstanding(P + 2));
+      issue_wait(4 * t + 7 + X, P + 2);
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
@@ -426,8 +439,7 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
           fa[j][ks] = read_frag<A_KMAJOR>(slot(t, H_AHI), wr * 64 + j * 16, ks, lane);
-      issue_h(4 * t + 8 + X);
-      vmwait_count<D>(outstanding(P + 3));
+      issue_wait(4 * t + 8 + X, P + 3);
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
@@ -436,14 +448,23 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
       __builtin_amdgcn_s_setprio(0);
       barrier();
       // ---- r4: M4-7 x N0-1 (no LDS reads)
-      issue_h(4 * t + 9 + X);
-      vmwait_count<D>(outstanding(P + 4));
+      issue_wait(4 * t + 9 + X, P + 4);
       barrier();
       __builtin_amdgcn_s_setprio(1);
       NF_G256_QUAD(0, 4, fbl);
       __builtin_amdgcn_s_setprio(0);
       barrier();
-    }
+    };
+    // steady K-tiles: t + 2 < nkt, and (two K segments) not the first segment's last K-tile,
+    // whose second 32-deep step may be absent
+    int nsteady = nkt - 2;
+    if (n2 > 0 && nsteady > n1 - 1) nsteady = n1 - 1;
+#ifdef NF_G256_NO_STEADY   // A/B build (csrc/build.py --variant nosteady -D NF_G256_NO_STEADY)
+    nsteady = 0;
+#endif
+    int t = 0;
+    for (; t < nsteady; ++t) ktile(t, std::true_type{});
+    for (; t < nkt; ++t) ktile(t, std::false_type{});
     if (wr == 0) barrier();
   }
   NF_STAMP(2);
