@@ -236,8 +236,10 @@ __device__ __forceinline__ v4u bf_stage_fix(v4u v, bool swapped) {
 // acc[i][j]: n = n0 + i*16 + (lane>>4)*4 + r, m = m0 + j*16 + (lane&15)  (m0/n0 = the wave's
 // sub-tile origin), i < 4, j < NJ (WM = 16*NJ). Requires N % 8 == 0, ldc % 8 == 0 (bf16) /
 // ldc % 4 == 0 (fp32) and a 16-B aligned C (checked by the launchers).
-template <int EPI, int NJ, bool F8 = false>
-__device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&acc)[4][NJ],
+// J0 / NJA: the rows handled are accumulator blocks [J0, J0 + NJ) of a [4][NJA] array (m0 is the
+// origin of block J0), so a caller short of LDS can stage a sub-tile in several calls.
+template <int EPI, int NJ, bool F8 = false, int J0 = 0, int NJA = NJ>
+__device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&acc)[4][NJA],
                                                 int m0, int n0, int split, char* region,
                                                 int lane) {
   const int g = lane >> 4, c = lane & 15;
@@ -287,10 +289,10 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
       const int row = j * 16 + c;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float v0 = fmaf(acc[i][j][0], smj[j] * sn[i][0], bv[i][0]);
-        float v1 = fmaf(acc[i][j][1], smj[j] * sn[i][1], bv[i][1]);
-        float v2 = fmaf(acc[i][j][2], smj[j] * sn[i][2], bv[i][2]);
-        float v3 = fmaf(acc[i][j][3], smj[j] * sn[i][3], bv[i][3]);
+        float v0 = fmaf(acc[i][J0 + j][0], smj[j] * sn[i][0], bv[i][0]);
+        float v1 = fmaf(acc[i][J0 + j][1], smj[j] * sn[i][1], bv[i][1]);
+        float v2 = fmaf(acc[i][J0 + j][2], smj[j] * sn[i][2], bv[i][2]);
+        float v3 = fmaf(acc[i][J0 + j][3], smj[j] * sn[i][3], bv[i][3]);
         if (relu) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
         const unsigned lo = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
         const unsigned hi = (unsigned)f2bf(v2) | ((unsigned)f2bf(v3) << 16);
@@ -410,7 +412,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
         const int row = jj * 16 + c;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          *(LDS_AS v4f*)(region + row * 256 + (((i * 4 + g) ^ (row & 7)) << 4)) = acc[i][hj * PJ + jj];
+          *(LDS_AS v4f*)(region + row * 256 + (((i * 4 + g) ^ (row & 7)) << 4)) = acc[i][J0 + hj * PJ + jj];
       }
       // global operands of this pass's rows, in flight while the LDS writes drain
       const int q = lane & 15;

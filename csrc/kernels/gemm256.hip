@@ -165,37 +165,23 @@ __device__ __forceinline__ void vmwait_count(int cnt) {
   else vmwait<0>();
 }
 
-// EPI_CPL_FWD epilogue (GemmArgs::cf_*). 1) every wave parks bf16(acc + bias) of its 128 x 64
-// sub-tile in its own 16 KiB LDS region (the staged-epilogue image); 2) after a block barrier
-// the 512 threads walk the 256 rows x 128 features, thread = (row of 32, 16-B chunk of 8
+// EPI_CPL_FWD epilogue (GemmArgs::cf_*), in NP row passes. Per pass: 1) every wave parks
+// bf16(acc + bias) of 128 / NP of its rows x 64 columns in its own LDS region
+// (region_of(wave), 16 KiB / NP, the staged-epilogue image); 2) after a block barrier the 512
+// threads walk the pass's 256 / NP rows x 128 features, thread = (row of 32, 16-B chunk of 8
 // features), reading s_hat from the region of wave (wr, c/64) and t from wave (wr, 2 + c/64).
+// NP = 2 lets the persistent kernel stage through the 64 KiB its LDS-DMA stream leaves free.
+template <int NP, typename RegionFn>
 __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&acc)[4][8],
-                                                 int m0, int n0, int wr, int wc, char* smem,
-                                                 int lane) {
+                                                 int m0, int n0, int wr, int wc,
+                                                 RegionFn region_of, int lane) {
+  constexpr int RJ = 8 / NP, RROWS = 16 * RJ, ITS = 8 / NP;
   const int g = lane >> 4, c = lane & 15;
   const int j0 = n0 >> 1, tn = n0 / BN;
-  char* region = smem + (wr * 4 + wc) * 16384;
-  // readback mapping, and its x rows / previous log-det partials fetched up front: the 8 rows'
-  // loads are all in flight while the accumulators are parked (the epilogue runs on every CU at
-  // once, so a load round trip per row pair would sit exposed after the main loop)
   const int tid = threadIdx.x, f8 = tid & 15, rsub = tid >> 4;
   const int ws = f8 >> 3, q = f8 & 7;
   const int jf = j0 + f8 * 8;                                    // first of this thread's 8 features
   const bool fok = jf < a.cf_dh;
-  float4 xv[8][2];
-  float lold[8];
-#pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int m = m0 + it * 32 + rsub;
-    xv[it][0] = xv[it][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-    lold[it] = 0.f;
-    if (m < a.M && fok) {
-      const float* xr = a.cf_x + (long)m * a.ld_cf_x + jf;
-      xv[it][0] = *reinterpret_cast<const float4*>(xr);
-      xv[it][1] = *reinterpret_cast<const float4*>(xr + 4);
-    }
-    if (!a.cf_ldj_init && f8 == 0 && m < a.M) lold[it] = a.cf_ldj[(long)tn * a.ld_cf_ldj + m];
-  }
   float bv[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -209,69 +195,93 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
       bv[i][0] = bv[i][1] = bv[i][2] = bv[i][3] = 0.f;
     }
   }
+  char* region = region_of(wr * 4 + wc);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int row = j * 16 + c;
+  for (int p = 0; p < NP; ++p) {
+    if (p) barrier();   // every wave's readback of the previous pass is done (its values were used)
+    // this pass's x rows / previous log-det partials fetched up front: all in flight while the
+    // accumulators are parked (the epilogue runs on every CU at once, so a load round trip per
+    // row pair would sit exposed after the main loop)
+    float4 xv[ITS][2];
+    float lold[ITS];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const unsigned lo = (unsigned)f2bf(acc[i][j][0] + bv[i][0]) |
-                          ((unsigned)f2bf(acc[i][j][1] + bv[i][1]) << 16);
-      const unsigned hi = (unsigned)f2bf(acc[i][j][2] + bv[i][2]) |
-                          ((unsigned)f2bf(acc[i][j][3] + bv[i][3]) << 16);
-      const int slot = i * 4 + g;
-      *(LDS_AS v2u*)(region + bf_stage_off(row, slot)) = (v2u){lo, hi};
+    for (int it = 0; it < ITS; ++it) {
+      const int lrow = it * 32 + rsub, wrr = lrow / RROWS, r = lrow % RROWS;
+      const int m = m0 + wrr * 128 + p * RROWS + r;
+      xv[it][0] = xv[it][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      lold[it] = 0.f;
+      if (m < a.M && fok) {
+        const float* xr = a.cf_x + (long)m * a.ld_cf_x + jf;
+        xv[it][0] = *reinterpret_cast<const float4*>(xr);
+        xv[it][1] = *reinterpret_cast<const float4*>(xr + 4);
+      }
+      if (!a.cf_ldj_init && f8 == 0 && m < a.M) lold[it] = a.cf_ldj[(long)tn * a.ld_cf_ldj + m];
     }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  barrier();
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int lrow = it * 32 + rsub, m = m0 + lrow;
-    const int wrr = lrow >> 7, r = lrow & 127;
-    float part = 0.f;
-    if (m < a.M) {
-      if (fok) {
-        const int off = r * 128 + ((q ^ (r & 7)) << 4);
-        const bool swp = (r >> 3) & 1;   // bf_stage_off's half swap
-        const v4u sh = bf_stage_fix(*(const LDS_AS v4u*)(smem + (wrr * 4 + ws) * 16384 + off), swp);
-        const v4u tt = bf_stage_fix(*(const LDS_AS v4u*)(smem + (wrr * 4 + 2 + ws) * 16384 + off), swp);
-        const float4 x0 = xv[it][0], x1 = xv[it][1];
-        const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        float y[8];
+    for (int jj = 0; jj < RJ; ++jj) {
+      const int j = p * RJ + jj;
+      const int row = jj * 16 + c;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const unsigned us = sh[e >> 1], ut = tt[e >> 1];
-          const float shv = __uint_as_float((e & 1) ? (us & 0xffff0000u) : (us << 16));
-          const float tv = __uint_as_float((e & 1) ? (ut & 0xffff0000u) : (ut << 16));
-          const float sv = a.cf_scale * fast_tanhf(shv);
-          y[e] = fmaf(xs[e], __expf(sv), tv);
-          part += sv;
-        }
-        float* yr = a.cf_y + (long)m * a.ld_cf_y + jf;
-        *reinterpret_cast<float4*>(yr) = make_float4(y[0], y[1], y[2], y[3]);
-        *reinterpret_cast<float4*>(yr + 4) = make_float4(y[4], y[5], y[6], y[7]);
-        if (a.cf_yb) {
-          uint4 o;
-          o.x = (unsigned)f2bf(y[0]) | ((unsigned)f2bf(y[1]) << 16);
-          o.y = (unsigned)f2bf(y[2]) | ((unsigned)f2bf(y[3]) << 16);
-          o.z = (unsigned)f2bf(y[4]) | ((unsigned)f2bf(y[5]) << 16);
-          o.w = (unsigned)f2bf(y[6]) | ((unsigned)f2bf(y[7]) << 16);
-          *reinterpret_cast<uint4*>(a.cf_yb + (long)m * a.ld_cf_yb + jf) = o;
-        }
-        *reinterpret_cast<uint4*>((bf16_t*)a.C + (long)m * a.ldc + jf) =
-            make_uint4(sh[0], sh[1], sh[2], sh[3]);
-      } else if (a.cf_yb && jf < a.cf_yb_width) {   // zero the next operand's pad columns
-        *reinterpret_cast<uint4*>(a.cf_yb + (long)m * a.ld_cf_yb + jf) = make_uint4(0, 0, 0, 0);
+      for (int i = 0; i < 4; ++i) {
+        const unsigned lo = (unsigned)f2bf(acc[i][j][0] + bv[i][0]) |
+                            ((unsigned)f2bf(acc[i][j][1] + bv[i][1]) << 16);
+        const unsigned hi = (unsigned)f2bf(acc[i][j][2] + bv[i][2]) |
+                            ((unsigned)f2bf(acc[i][j][3] + bv[i][3]) << 16);
+        const int slot = i * 4 + g;
+        *(LDS_AS v2u*)(region + bf_stage_off(row, slot)) = (v2u){lo, hi};
       }
     }
-    // sum of s over this block's 128 features: the 16 threads of a row are 16 adjacent lanes
-    part += __shfl_xor(part, 8);
-    part += __shfl_xor(part, 4);
-    part += __shfl_xor(part, 2);
-    part += __shfl_xor(part, 1);
-    if (f8 == 0 && m < a.M) {
-      float* lp = a.cf_ldj + (long)tn * a.ld_cf_ldj + m;
-      *lp = part + lold[it];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier();
+#pragma unroll
+    for (int it = 0; it < ITS; ++it) {
+      const int lrow = it * 32 + rsub, wrr = lrow / RROWS, r = lrow % RROWS;
+      const int m = m0 + wrr * 128 + p * RROWS + r;
+      float part = 0.f;
+      if (m < a.M) {
+        if (fok) {
+          const int off = r * 128 + ((q ^ (r & 7)) << 4);
+          const bool swp = (r >> 3) & 1;   // bf_stage_off's half swap
+          const v4u sh = bf_stage_fix(*(const LDS_AS v4u*)(region_of(wrr * 4 + ws) + off), swp);
+          const v4u tt = bf_stage_fix(*(const LDS_AS v4u*)(region_of(wrr * 4 + 2 + ws) + off), swp);
+          const float4 x0 = xv[it][0], x1 = xv[it][1];
+          const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          float y[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const unsigned us = sh[e >> 1], ut = tt[e >> 1];
+            const float shv = __uint_as_float((e & 1) ? (us & 0xffff0000u) : (us << 16));
+            const float tv = __uint_as_float((e & 1) ? (ut & 0xffff0000u) : (ut << 16));
+            const float sv = a.cf_scale * fast_tanhf(shv);
+            y[e] = fmaf(xs[e], __expf(sv), tv);
+            part += sv;
+          }
+          float* yr = a.cf_y + (long)m * a.ld_cf_y + jf;
+          *reinterpret_cast<float4*>(yr) = make_float4(y[0], y[1], y[2], y[3]);
+          *reinterpret_cast<float4*>(yr + 4) = make_float4(y[4], y[5], y[6], y[7]);
+          if (a.cf_yb) {
+            uint4 o;
+            o.x = (unsigned)f2bf(y[0]) | ((unsigned)f2bf(y[1]) << 16);
+            o.y = (unsigned)f2bf(y[2]) | ((unsigned)f2bf(y[3]) << 16);
+            o.z = (unsigned)f2bf(y[4]) | ((unsigned)f2bf(y[5]) << 16);
+            o.w = (unsigned)f2bf(y[6]) | ((unsigned)f2bf(y[7]) << 16);
+            *reinterpret_cast<uint4*>(a.cf_yb + (long)m * a.ld_cf_yb + jf) = o;
+          }
+          *reinterpret_cast<uint4*>((bf16_t*)a.C + (long)m * a.ldc + jf) =
+              make_uint4(sh[0], sh[1], sh[2], sh[3]);
+        } else if (a.cf_yb && jf < a.cf_yb_width) {   // zero the next operand's pad columns
+          *reinterpret_cast<uint4*>(a.cf_yb + (long)m * a.ld_cf_yb + jf) = make_uint4(0, 0, 0, 0);
+        }
+      }
+      // sum of s over this block's 128 features: the 16 threads of a row are 16 adjacent lanes
+      part += __shfl_xor(part, 8);
+      part += __shfl_xor(part, 4);
+      part += __shfl_xor(part, 2);
+      part += __shfl_xor(part, 1);
+      if (f8 == 0 && m < a.M) {
+        float* lp = a.cf_ldj + (long)tn * a.ld_cf_ldj + m;
+        *lp = part + lold[it];
+      }
     }
   }
 }
@@ -481,7 +491,8 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   }
   if constexpr (EPI == EPI_CPL_FWD) {
     barrier();  // every wave is past its last operand read
-    epi_coupling_fwd(a, acc, m0, n0, wr, wc, smem, lane);
+    epi_coupling_fwd<1>(a, acc, m0, n0, wr, wc,
+                        [&](int w) { return smem + w * 16384; }, lane);
 #ifdef NF_G256_STAMPS
     NF_STAMP(3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -511,6 +522,203 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
       epi_store<EPI>(a, acc[i][j], m, n, split);
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Persistent form for the plain products (no K ranges, no split-K, no bias gradient): grid =
+// min(tiles, CUs) blocks of the same 8-phase schedule; block b computes tiles b, b + G, ...
+// (XCD-remapped ids, so a block's tiles stay in its XCD's contiguous id range). The K-tiles of
+// all of a block's tiles form ONE LDS-DMA stream (half h of the stream is issued at phase h - 5
+// and lives in ring slot h % 8, exactly as inside one tile), so when a tile's last K-tile is
+// done the next tile's first six half-tiles are already in flight: its prologue burst and the
+// block turnover of the one-tile-per-block launch (~1.8 + 2.1 us per tile,
+// profiles/r2_g256_stamps_b65536.jsonl) are gone, and the epilogue is the only per-tile cost
+// outside the MFMA loop.
+// LDS at a tile boundary (last K-tile T): halves 4T+4 .. 4T+9 are live in their slots; the slots
+// of the last K-tile's B-hi / A-hi halves ((4T+2) % 8, (4T+3) % 8: read in its phases r2 / r3,
+// restaged only in phases 1 / 2 of the next tile) and the 32 KiB above the ring are free.
+// The epilogue stages through them: 8 KiB per wave (waves 0-3 in the free slot pair, 4-7 above
+// the ring), i.e. bf16 outputs in two 64-row passes, fp32 outputs in their usual 32-row
+// passes. WAR on the slot pair: every wave's staging reads are consumed by its own stores
+// before the barrier that ends the epilogue, and the DMA into those slots is issued after it.
+template <bool A_KMAJOR, bool B_KMAJOR, int EPI>
+__device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char* smem) {
+  constexpr int D = 4, NSLOT = 8;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  const int ntiles = ntm * ntn;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int ns = (ntiles - b + G - 1) / G;          // tiles of this block
+  const int nkt = (a.K + BK - 1) / BK;              // K-tiles per tile
+  auto tile_org = [&](int s, int& m0, int& n0) {
+    const int id = xcd_remap(b + s * G, ntiles);
+    m0 = (id / ntn) * BM;
+    n0 = (id % ntn) * BN;
+  };
+  // stage half j of K-tile tk of the tile at (tm0, tn0) into the ring slot of stream half
+  // 4 Tg + j
+  auto issue_to = [&](int Tg, int tm0, int tn0, int tk, int j) {
+    char* dst = smem + ((4 * Tg + j) & (NSLOT - 1)) * HALF_BYTES;
+    const int k0 = tk * BK;
+    if (j == H_ALO || j == H_AHI)
+      stage_half<A_KMAJOR>(a.A, a.lda, tm0, a.M, k0, a.K, true, j == H_AHI, dst, wave, lane);
+    else if constexpr (EPI == EPI_CPL_FWD)
+      stage_half<B_KMAJOR>(a.B, a.ldb, tn0, a.cf_b_rows, k0, a.K, false, j == H_BHI, dst, wave,
+                           lane, a.cf_dh);
+    else
+      stage_half<B_KMAJOR>(a.B, a.ldb, tn0, a.N, k0, a.K, false, j == H_BHI, dst, wave, lane);
+  };
+
+  v4f acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+  v8s fa[4][2], fbl[2][2], fbh[2][2];
+
+  // One K-tile (stream index T, index t in its tile) of the 8-phase schedule. Phase q issues
+  // half 4T + 5 + q of the schedule: (t+1, B-hi), (t+1, A-hi), (t+2, A-lo), (t+2, B-lo) - only
+  // while those are K-tiles of this tile. The next tile's first six halves are issued in one
+  // burst at the tile boundary instead (they land during the epilogue), so the tile's last
+  // K-tiles issue less and retire by the counts of the one-tile schedule's tail:
+  //   MODE 0: t + 2 < nkt, four issues, vmcnt(2D) each phase (branch-free)
+  //   MODE 1: t = nkt - 2, issues in phases 1-2, then vmcnt 6 / 4
+  //   MODE 2: t = nkt - 1, no issues, vmcnt 2 / 0 / 0 / 0
+  // FULL: the K-tile has both 32-deep k-steps (false only on a tile's last K-tile when
+  //       K % 64 == 32, then `two` is the runtime answer).
+  auto ktile = [&](int T, int t, int m0, int n0, bool two_rt, auto mode_c, auto full_c) {
+    constexpr int MODE = decltype(mode_c)::value;
+    const bool two = decltype(full_c)::value || two_rt;
+    constexpr bool F8 = false;
+    auto slot = [&](int j) { return smem + ((4 * T + j) & (NSLOT - 1)) * HALF_BYTES; };
+    auto issue_wait = [&](auto q_c) {   // q = 1..4
+      constexpr int q = decltype(q_c)::value;
+      constexpr int j = q == 1 ? H_BHI : q == 2 ? H_AHI : q == 3 ? H_ALO : H_BLO;
+      if constexpr (MODE == 0 || (MODE == 1 && q <= 2)) {
+        issue_to(q <= 2 ? T + 1 : T + 2, m0, n0, q <= 2 ? t + 1 : t + 2, j);
+        vmwait<2 * D>();
+      } else if constexpr (MODE == 1) {
+        vmwait<q == 3 ? 6 : 4>();
+      } else {
+        vmwait<q == 1 ? 2 : 0>();
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        fbl[i][ks] = read_frag<B_KMAJOR>(slot(H_BLO), wc * 32 + i * 16, ks, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        fa[j][ks] = read_frag<A_KMAJOR>(slot(H_ALO), wr * 64 + j * 16, ks, lane);
+    issue_wait(std::integral_constant<int, 1>{});
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+    NF_G256_QUAD(0, 0, fbl);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        fbh[i][ks] = read_frag<B_KMAJOR>(slot(H_BHI), wc * 32 + i * 16, ks, lane);
+    issue_wait(std::integral_constant<int, 2>{});
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+    NF_G256_QUAD(2, 0, fbh);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        fa[j][ks] = read_frag<A_KMAJOR>(slot(H_AHI), wr * 64 + j * 16, ks, lane);
+    issue_wait(std::integral_constant<int, 3>{});
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+    NF_G256_QUAD(2, 4, fbh);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    issue_wait(std::integral_constant<int, 4>{});
+    barrier();
+    __builtin_amdgcn_s_setprio(1);
+    NF_G256_QUAD(0, 4, fbl);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+  };
+
+  if (ns <= 0) return;
+  int m0, n0;
+  tile_org(0, m0, n0);
+  // prologue: the stream's first six halves (K-tile 0, and K-tile 1's A-lo / B-lo; nkt >= 2)
+#pragma unroll
+  for (int h = 0; h < 6; ++h) issue_to(h >> 2, m0, n0, h >> 2, h & 3);
+  vmwait<0>();
+  barrier();
+  const bool tail_half = (a.K - (nkt - 1) * BK) <= 32;   // a tile's last K-tile has one k-step
+  int T = 0;
+  for (int s = 0; s < ns; ++s) {
+    const bool has_next = s + 1 < ns;
+    if (wr == 1) barrier();
+    for (int t = 0; t < nkt - 2; ++t, ++T)
+      ktile(T, t, m0, n0, true, std::integral_constant<int, 0>{}, std::true_type{});
+    ktile(T, nkt - 2, m0, n0, true, std::integral_constant<int, 1>{}, std::true_type{});
+    ++T;
+    ktile(T, nkt - 1, m0, n0, !tail_half, std::integral_constant<int, 2>{}, std::false_type{});
+    ++T;
+    // the next tile's K-tile 0 and K-tile 1's A-lo / B-lo: stream halves 4T .. 4T+5, i.e. the
+    // slots of K-tiles T-2 (all four, read long ago) and T-1's A-lo / B-lo (read in its phase
+    // r1) - not the free pair the epilogue stages through
+    int m0n = 0, n0n = 0;
+    if (has_next) {
+      tile_org(s + 1, m0n, n0n);
+#pragma unroll
+      for (int h = 0; h < 6; ++h) issue_to(T + (h >> 2), m0n, n0n, h >> 2, h & 3);
+    }
+    if (wr == 0) barrier();
+    // ---- epilogue of tile s through the free LDS (see above)
+    const int fs = (4 * (T - 1) + 2) & (NSLOT - 1);   // free slot pair of the last K-tile
+    char* region = wave < 4 ? smem + fs * HALF_BYTES + wave * 8192
+                            : smem + NSLOT * HALF_BYTES + (wave - 4) * 8192;
+    if constexpr (EPI == EPI_CPL_FWD) {
+      epi_coupling_fwd<2>(a, acc, m0, n0, wr, wc,
+                          [&](int w) {
+                            return w < 4 ? smem + fs * HALF_BYTES + w * 8192
+                                         : smem + NSLOT * HALF_BYTES + (w - 4) * 8192;
+                          },
+                          lane);
+    } else if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK) {
+      epi_tile_staged<EPI, 4, false, 0, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, 0, region, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own readback done before re-staging
+      epi_tile_staged<EPI, 4, false, 4, 8>(a, acc, m0 + wr * 128 + 64, n0 + wc * 64, 0, region,
+                                           lane);
+    } else {
+      epi_tile_staged<EPI, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, 0, region, lane);
+    }
+    // the next tile's six halves (and this epilogue's stores) retired, and every wave's staging
+    // reads done before the stream restages the slot pair
+    vmwait<0>();
+    barrier();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+    m0 = m0n;
+    n0 = n0n;
+  }
+}
+
+template <bool A_KMAJOR, bool B_KMAJOR, int EPI>
+__global__ void __launch_bounds__(NTHR, 1) gemm256_persistent_kernel(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[8 * HALF_BYTES + 8 * 4096];
+  gemm256_persistent_body<A_KMAJOR, B_KMAJOR, EPI>(a, smem);
 }
 
 // Streamed K-tiles of column tile tn under a MADE K-range plan (one or two ranges).
@@ -642,6 +850,22 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
   }();
   a.pair_tiles = pair_env && a.krange && splits == 1 && ntn % 2 == 0 &&
                  (pair_env == 2 || (long)ntm * (ntn / 2) >= device_cus_256());
+  // plain products run persistent (one continuous LDS-DMA stream per block, see
+  // gemm256_persistent_body); VINF_G256_PERSIST=0 restores one tile per block
+  static const int persist_env = [] {
+    const char* e = getenv("VINF_G256_PERSIST");
+    return e ? atoi(e) : 1;
+  }();
+  const bool staged_epi = EPI == EPI_CPL_FWD || a.staged;
+  if (persist_env && !DB && splits == 1 && !a.krange && !a.skip && !a.pair_tiles && staged_epi &&
+      g_depth != 6 && a.K > BK) {
+    const int ntiles = ntm * ntn, cus = device_cus_256();
+    const int G = ntiles < cus ? ntiles : cus;
+    hipLaunchKernelGGL((gemm256_persistent_kernel<AK, BK_, EPI>), dim3(G), dim3(NTHR), 0, stream,
+                       a);
+    NF_HIP_CHECK(hipGetLastError());
+    return;
+  }
   dim3 grid(a.pair_tiles ? ntm * (ntn / 2) : ntm * ntn, splits), block(NTHR);
   if (g_depth != 6)
     hipLaunchKernelGGL((gemm256_kernel<AK, BK_, EPI, 4, DB>), grid, block, 0, stream, a);

@@ -1,0 +1,129 @@
+"""Persistent 256x256 GEMM (csrc/kernels/gemm256.hip gemm256_persistent_body): products with
+more tiles than CUs, so every block streams several tiles through ONE LDS-DMA ring and stages
+each epilogue through the LDS the stream leaves free. Uneven tile counts per block, K tails
+(K % 64 == 32), N / M edges and every epilogue kind the plain launches use, against fp32
+PyTorch on the same bf16 inputs, plus a bitwise race screen across tile boundaries."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(*shape, device, scale=1.0):
+    return (torch.randn(*shape, device=device) * scale).to(torch.bfloat16)
+
+
+def _check(out, ref, tol):
+    err = (out.float() - ref).abs().max().item()
+    mag = ref.abs().max().item() + 1e-6
+    assert err <= tol * mag, (err, mag)
+
+
+def _pack_bits(pos: torch.Tensor) -> torch.Tensor:
+    M, N = pos.shape
+    w = (2 ** torch.arange(8, device=pos.device, dtype=torch.int32))
+    return (pos.view(M, N // 8, 8).to(torch.int32) * w).sum(-1).to(torch.uint8)
+
+
+# M = 70000 -> 274 row tiles: with N = 1024 1096 tiles (4-5 per block on 256 CUs)
+@pytest.mark.parametrize("M,N,K", [(70000, 1024, 416), (66000, 800, 1024), (65536, 1024, 96)])
+def test_persistent_nt_bias_relu_mask(gpu, M, N, K):
+    torch.manual_seed(M + K)
+    x, W, b = _bf(M, K, device=gpu), _bf(N, K, device=gpu, scale=0.05), _bf(N, device=gpu)
+    y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    mask = torch.full((M, N // 8), 0xAA, device=gpu, dtype=torch.uint8)
+    torch.ops.vinf.gemm_nt(x, W, b, y, 1, mask)
+    _check(y, (x.float() @ W.float().t() + b.float()).clamp_min(0), 1e-2)
+    assert torch.equal(mask, _pack_bits(y > 0))
+
+
+@pytest.mark.parametrize("M,N,K", [(70000, 1024, 800), (66000, 416, 1024)])
+def test_persistent_dgrad_bits_nt(gpu, M, N, K):
+    from vi_normflows_amd.ops import gemm
+
+    torch.manual_seed(3)
+    dy, W = _bf(M, K, device=gpu), _bf(K, N, device=gpu, scale=0.05)
+    act = _bf(M, N, device=gpu)
+    bits = _pack_bits(act > 0)
+    out = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    gemm.linear_dgrad(dy, W, out, relu_of=act, relu_bits=bits, Wt=W.t().contiguous())
+    _check(out, (dy.float() @ W.float()) * (act.float() > 0), 1e-2)
+
+
+def test_persistent_f32_accumulate(gpu):
+    torch.manual_seed(4)
+    M, N, K = 70000, 416, 1024
+    dy, W = _bf(M, K, device=gpu), _bf(K, N, device=gpu, scale=0.05)
+    base = torch.randn(M, N, device=gpu)
+    out = base.clone()
+    torch.ops.vinf.gemm_nn(dy, W, None, out, True)
+    _check(out, dy.float() @ W.float() + base, 2e-2)
+
+
+def test_persistent_fused_coupling_fwd_bwd(gpu):
+    """EPI_CPL_FWD (two staged row passes) and EPI_CPL_BWD (fp32 passes) at a multi-tile M."""
+    from vi_normflows_amd.ops import gemm
+
+    torch.manual_seed(9)
+    M, K, Dh = 66000, 1024, 392
+    h = _bf(M, K, device=gpu)
+    W = torch.zeros(800, K, device=gpu)
+    W[:2 * Dh] = torch.randn(2 * Dh, K, device=gpu) * 0.03
+    W = W.to(torch.bfloat16)
+    b = (torch.randn(800, device=gpu) * 0.1).to(torch.bfloat16)
+    x = torch.randn(M, Dh, device=gpu)
+    outs = []
+    for backend in ("mfma", "blas"):
+        gemm.set_backend(backend)
+        try:
+            st = torch.zeros(M, 800, device=gpu, dtype=torch.bfloat16)
+            y = torch.empty(M, Dh, device=gpu)
+            yb = torch.full((M, 416), 3.0, device=gpu).to(torch.bfloat16)
+            ldjp = torch.full((4, M), 9.0, device=gpu)
+            gemm.linear_fwd_coupling(h, W, b, st, x, y, yb, ldjp, True, 1.0)
+            outs.append((st[:, :Dh].float(), y, yb.float(), ldjp.sum(0)))
+        finally:
+            gemm.set_backend("mfma")
+    (s1, y1, b1, l1), (s2, y2, b2, l2) = outs
+    assert (b1[:, Dh:] == 0).all()
+    for u, v in ((s1, s2), (y1, y2), (b1, b2), (l1, l2)):
+        err = (u - v).abs().max().item()
+        assert err <= 2e-2 * v.abs().max().item() + 1e-3, err
+
+    N = 416
+    dy = _bf(M, K, device=gpu)
+    Wd = (torch.randn(K, N, device=gpu) * 0.05).to(torch.bfloat16)
+    G = torch.randn(M, N, device=gpu)
+    G[:, Dh:] = 0
+    s_hat = _bf(M, 800, device=gpu)
+    res = []
+    for backend in ("mfma", "blas"):
+        gemm.set_backend(backend)
+        try:
+            o = [torch.full((M, 800), 5.0, device=gpu).to(torch.bfloat16),
+                 torch.full((M, Dh), 5.0, device=gpu)]
+            gemm.linear_dgrad_coupling(dy, Wd, G, s_hat[:, :Dh], x, o[0], o[1], 1.0, -1e-3,
+                                       Wt=Wd.t().contiguous() if backend == "mfma" else None)
+            res.append(o)
+        finally:
+            gemm.set_backend("mfma")
+    assert (res[0][0][:, 2 * Dh:] == 0).all()
+    for o, r in zip(res[0], res[1]):
+        err = (o.float() - r.float()).abs().max().item()
+        assert err <= 2e-2 * r.float().abs().max().item(), err
+
+
+def test_persistent_repeatable(gpu):
+    """Race screen across tile boundaries: 10 repeats bitwise identical (the next tile's
+    LDS-DMA lands while the previous tile's epilogue stages through the free slots)."""
+    torch.manual_seed(5)
+    M, N, K = 70000, 1024, 416
+    x, W, b = _bf(M, K, device=gpu), _bf(N, K, device=gpu, scale=0.05), _bf(N, device=gpu)
+    y0 = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    m0 = torch.empty(M, N // 8, device=gpu, dtype=torch.uint8)
+    torch.ops.vinf.gemm_nt(x, W, b, y0, 1, m0)
+    y = torch.empty_like(y0)
+    m = torch.empty_like(m0)
+    for _ in range(10):
+        torch.ops.vinf.gemm_nt(x, W, b, y, 1, m)
+        assert torch.equal(y, y0) and torch.equal(m, m0)
