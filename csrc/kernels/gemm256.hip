@@ -655,6 +655,8 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
   };
 
   if (ns <= 0) return;
+  if (a.desync && (b & 1))
+    for (int i = 0; i < a.desync; ++i) __builtin_amdgcn_s_sleep(127);
   int m0, n0;
   tile_org(0, m0, n0);
   // prologue: the stream's first six halves (K-tile 0, and K-tile 1's A-lo / B-lo; nkt >= 2)
@@ -859,6 +861,11 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
   const bool staged_epi = EPI == EPI_CPL_FWD || a.staged;
   if (persist_env && !DB && splits == 1 && !a.krange && !a.skip && !a.pair_tiles && staged_epi &&
       g_depth != 6 && a.K > BK) {
+    static const int desync_env = [] {
+      const char* e = getenv("VINF_G256_DESYNC");
+      return e ? atoi(e) : 0;
+    }();
+    a.desync = desync_env;
     const int ntiles = ntm * ntn, cus = device_cus_256();
     const int G = ntiles < cus ? ntiles : cus;
     hipLaunchKernelGGL((gemm256_persistent_kernel<AK, BK_, EPI>), dim3(G), dim3(NTHR), 0, stream,
