@@ -200,3 +200,32 @@ void nf_launch_iaf_gate_bwd(const float* gy, long ldg, const float* gl, const fl
 void nf_launch_fp8_quant_rows_strided(const void* x, int x_is_bf16, long ldx, long layer_stride,
                                       int rows_per, int R, int C, void* q, long ldq, int Cq,
                                       float* scale, hipStream_t stream);
+
+// vae.hip: whole training step of the amortized planar-flow VAE (reference main workload):
+// phase 1 row-parallel forward + input-gradient chain, phase 2 batch-reduction weight gradients
+struct NfVaeParams {
+  const float* enc_W[4];
+  const float* enc_b[4];
+  const float* enc_Wo;
+  const float* enc_bo;
+  const float* dec_W[4];
+  const float* dec_b[4];
+  const float* dec_Wo;
+  const float* dec_bo;
+};
+struct NfVaeGrads {
+  float* enc_W[4];
+  float* enc_b[4];
+  float* enc_Wo;
+  float* enc_bo;
+  float* dec_W[4];
+  float* dec_b[4];
+  float* dec_Wo;
+  float* dec_bo;
+};
+size_t nf_vae_rows_lds_bytes(int Din, int dz, int K, int De);
+void nf_launch_vae_step(const NfVaeParams& prm, const float* x, const float* eps_in, unsigned seed,
+                        const long* offset, const float* beta, int B, int Din, int dz, int K,
+                        int L, float* ws_eact, float* ws_egrad, float* ws_gphi, float* ws_zk,
+                        float* ws_dact, float* ws_dgrad, float* ws_dl, float* frow, float* loss,
+                        float* zk_out, float* ldj_out, const NfVaeGrads& grd, hipStream_t stream);

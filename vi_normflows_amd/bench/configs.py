@@ -56,6 +56,25 @@ def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: b
         from ..models.vae import PlanarVAE, VAEConfig, synthetic_binary_images
 
         B = batch or 128
+        if impl == "engine" and dev.type == "cuda" and info.world == 1:
+            # models/vae_engine.py: two HIP launches (row-parallel fwd + input-gradient chain,
+            # batch-reduction weight gradients) + fused guard + flat Adam, one hipGraph
+            from ..models.vae_engine import PlanarVAEEngine
+
+            eng = PlanarVAEEngine(VAEConfig(dim_x=784, dim_z=40, K=4, width=64, hidden_layers=3),
+                                  batch=B, device=dev, seed=info.rank, lr=1e-3)
+            X = synthetic_binary_images(max(2000, 4 * B), 784, seed=info.rank).to(dev)
+            eng.set_batch(X[:B])
+            g = eng.capture(warmup=2) if graph else None
+            it = [0]
+
+            def step():
+                i = it[0] % (X.shape[0] // B)
+                it[0] += 1
+                eng.set_batch(X[i * B:(i + 1) * B])
+                g.replay() if g is not None else eng.train_step()
+            return step, B, dev, "fp32 PlanarVAE engine (vae.hip two-launch step + flat Adam)" + (
+                ", hipGraph" if g is not None else "")
         model = PlanarVAE(VAEConfig(dim_x=784, dim_z=40, K=4, width=64, hidden_layers=3))
         model.init_reference(generator=torch.Generator().manual_seed(0))
         model = model.to(dev)

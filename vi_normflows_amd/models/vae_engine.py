@@ -1,0 +1,198 @@
+"""Explicit-step engine for the reference's main workload: the amortized planar-flow VAE.
+
+Reference: ``src/learning_mnist.py:89-99`` (encoder 784 -> 64 x3 -> 2dz + 2dz K + K, K
+per-sample planar flows, Bernoulli decoder dz -> 64 x3 -> 784, Adam lr 1e-3, batch 128) and
+the annealed objective ``normflows/normflows/optimization.py:66-92`` with the estimator fixes
+of :mod:`..inference.elbo` (exact log-det of the applied transform with the reference's
+log(|psi| + 1e-7) guard, base entropy kept, Bernoulli from logits, per-sample terms averaged).
+
+The model is tiny (145k parameters) and the reference batch is 128, so the autograd module
+path (:class:`..models.vae.PlanarVAE`) is bound by ~60 kernel launches per step even inside a
+hipGraph. This engine runs a training step as:
+
+* ``vinf::vae_step`` (``csrc/kernels/vae.hip``): phase 1 - one block per 8 rows does the whole
+  forward (in-kernel Philox noise) and the input-gradient chain with every activation in LDS;
+  phase 2 - every weight / bias gradient as a batch-reduction tile kernel (plain stores, no
+  atomics) plus the loss;
+* the fused non-finite guard and the flat Adam kernel over ONE fp32 parameter buffer;
+* device-side step / noise-offset / beta updates, so the whole step captures into a hipGraph.
+
+Parameters live in a flat fp32 buffer whose per-layer views have the FlatMLP shapes, so the
+engine imports / exports :class:`PlanarVAE` modules (and through them the reference's
+``models/*/weights_*.npy`` checkpoints). On CPU the same step runs through the autograd module
+(the numerics reference the GPU tests compare against).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..ops import fused
+from ..utils.flat import FlatLayout, FlatParams
+from .vae import PlanarVAE, VAEConfig
+
+_H = 64
+
+
+def _mlp_names(prefix: str, L: int):
+    return ([f"{prefix}.W{l}" for l in range(L)] + [f"{prefix}.b{l}" for l in range(L)]
+            + [f"{prefix}.Wo", f"{prefix}.bo"])
+
+
+class PlanarVAEEngine:
+    """Flat-buffer planar-flow VAE trainer (GPU: two-launch HIP step + fused Adam)."""
+
+    def __init__(self, cfg: VAEConfig | None = None, batch: int = 128, device="cuda",
+                 seed: int = 0, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 anneal: str = "none", anneal_iters: int = 10000, init_scale: float = 0.05):
+        cfg = cfg or VAEConfig()
+        if cfg.flow_variant != "paper" or cfg.encode_layout != "paper":
+            raise ValueError("the engine implements the paper planar update / encoder layout")
+        if cfg.width != _H:
+            raise ValueError("the engine's kernels assume width 64 (one wave)")
+        self.cfg = cfg
+        self.B = int(batch)
+        self.device = torch.device(device)
+        self.seed = int(seed)
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.anneal, self.anneal_iters = anneal, anneal_iters
+        dz, K, L, Din = cfg.dim_z, cfg.K, cfg.hidden_layers, cfg.dim_x
+        self.De = 2 * dz + 2 * dz * K + K
+        layout = FlatLayout()
+        dims_e = [Din] + [_H] * L
+        dims_d = [dz] + [_H] * L
+        for prefix, dims, dout in (("dec", dims_d, Din), ("enc", dims_e, self.De)):
+            ts = [(f"{prefix}.W{l}", (_H, dims[l])) for l in range(L)]
+            ts += [(f"{prefix}.b{l}", (_H,)) for l in range(L)]
+            ts += [(f"{prefix}.Wo", (dout, _H)), (f"{prefix}.bo", (dout,))]
+            layout.add_unit(ts)
+        self.layout = layout
+        self.params = FlatParams(layout, self.device, torch.float32)
+        self.offs = [layout.slots[n].offset for n in _mlp_names("enc", L) + _mlp_names("dec", L)]
+        dev = self.device
+        self.x = torch.zeros(self.B, Din, device=dev)
+        self.step_t = torch.zeros((), device=dev)
+        self.rng_offset = torch.zeros((), dtype=torch.int64, device=dev)
+        self.beta = torch.ones((), device=dev)
+        self.loss = torch.zeros((), device=dev)
+        self.frow = torch.zeros(self.B, device=dev)
+        self.gnorm2 = torch.zeros((), device=dev)
+        self.skip = torch.zeros((), device=dev)
+        self.gscale = torch.ones((), device=dev)
+        self._partials = torch.zeros(512, device=dev)
+        self.ws = torch.zeros(4 * L * self.B * _H + self.B * (self.De + dz + Din), device=dev)
+        self.eps_override = None
+        self.zk_out = self.ldj_out = None
+        g = torch.Generator().manual_seed(int(seed))
+        with torch.no_grad():
+            for n in layout.order:       # get_init_params: every weight ~ N(0, 1) * 0.05
+                self.params.p(n).copy_(torch.randn(self.params.p(n).shape, generator=g) * init_scale)
+
+    # ------------------------------------------------------------------ module interop
+    def _module_pairs(self, model: PlanarVAE):
+        L = self.cfg.hidden_layers
+        pairs = []
+        for prefix, mlp in (("enc", model.encoder), ("dec", model.decoder)):
+            for l in range(L):
+                pairs += [(f"{prefix}.W{l}", mlp.linears[l].weight), (f"{prefix}.b{l}", mlp.linears[l].bias)]
+            pairs += [(f"{prefix}.Wo", mlp.linears[L].weight), (f"{prefix}.bo", mlp.linears[L].bias)]
+        return pairs
+
+    @torch.no_grad()
+    def load_module(self, model: PlanarVAE) -> "PlanarVAEEngine":
+        for n, t in self._module_pairs(model):
+            self.params.p(n).copy_(t.detach().to(self.params.p(n)))
+        return self
+
+    @torch.no_grad()
+    def to_module(self, model: PlanarVAE | None = None) -> PlanarVAE:
+        model = model or PlanarVAE(self.cfg)
+        for n, t in self._module_pairs(model):
+            t.copy_(self.params.p(n).to(t))
+        return model
+
+    def set_batch(self, x: torch.Tensor) -> None:
+        self.x.copy_(x)
+
+    # ------------------------------------------------------------------ step
+    def _update_schedule(self):
+        self.step_t.add_(1.0)
+        self.rng_offset.add_(1)
+        if self.anneal == "reference":   # beta_t = min(1, 0.001 + t / min(max_iter/4, 1e4))
+            cool = min(self.anneal_iters / 4.0, 1e4)
+            torch.clamp((self.step_t - 1.0) * (1.0 / cool) + 0.001, max=1.0, out=self.beta)
+
+    def forward_backward(self):
+        """Loss into ``self.loss`` and every parameter gradient into the flat grad buffer."""
+        cfg = self.cfg
+        if self.device.type == "cuda":
+            from ..ops._ext import native
+
+            native().vae_step(self.params.master, self.params.grad, self.offs, self.x,
+                              self.eps_override, self.seed, self.rng_offset, self.beta, self.B,
+                              cfg.dim_x, cfg.dim_z, cfg.K, cfg.hidden_layers, self.ws, self.frow,
+                              self.loss, self.zk_out, self.ldj_out)
+            return
+        self._reference_forward_backward()
+
+    def _reference_forward_backward(self):
+        """Autograd through the PlanarVAE composite on views of the flat buffer (CPU path and
+        the GPU tests' fp32 reference)."""
+        model = self.to_module(PlanarVAE(self.cfg).to(self.device))
+        eps = self.eps_override
+        if eps is None:
+            gen = torch.Generator(device=self.device).manual_seed(self.seed + int(self.step_t.item()))
+            eps = torch.randn(self.B, self.cfg.dim_z, generator=gen, device=self.device)
+        mu, lv, fp = model.encode(self.x)
+        z0 = mu + torch.exp(0.5 * lv) * eps
+        dz = self.cfg.dim_z
+        lq0 = -0.5 * dz * math.log(2 * math.pi) - 0.5 * lv.sum(1) - 0.5 * (eps * eps).sum(1)
+        zK, ldj = model.flow(z0, fp)
+        lp = model.log_joint(self.x, zK)
+        frow = lq0 - ldj - self.beta * lp
+        F = frow.mean()
+        model.zero_grad(set_to_none=True)
+        F.backward()
+        with torch.no_grad():
+            self.loss.copy_(F.detach())
+            self.frow.copy_(frow.detach())
+            if self.zk_out is not None:
+                self.zk_out.copy_(zK.detach())
+            if self.ldj_out is not None:
+                self.ldj_out.copy_(ldj.detach())
+            self.params.grad.zero_()
+            for n, t in self._module_pairs(model):
+                self.params.g(n).copy_(t.grad)
+
+    def optimizer_step(self):
+        P = self.params
+        fused.sumsq_guard(P.grad, self._partials, out_sumsq=self.gnorm2, skip=self.skip,
+                          scale=self.gscale, max_norm=0.0, base_scale=1.0)
+        b1, b2 = self.betas
+        fused.flat_optimizer(fused.OPT_ADAM, P.master, P.grad, P.m, P.v, pbf=None, lr=self.lr,
+                             b1=b1, b2=b2, eps=self.eps, wd=0.0, step=self.step_t,
+                             gscale=self.gscale, skip=self.skip)
+
+    def train_step(self):
+        self._update_schedule()
+        self.forward_backward()
+        self.optimizer_step()
+
+    def capture(self, warmup: int = 2):
+        """Capture one train_step into a hipGraph (static x buffer: refill it with set_batch)."""
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.train_step()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.train_step()
+        self._graph = g
+        return g
+
+    def n_params(self) -> int:
+        return self.layout.n_params()
