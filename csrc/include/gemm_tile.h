@@ -239,7 +239,9 @@ __device__ __forceinline__ v4u bf_stage_fix(v4u v, bool swapped) {
 // ldc % 4 == 0 (fp32) and a 16-B aligned C (checked by the launchers).
 // J0 / NJA: the rows handled are accumulator blocks [J0, J0 + NJ) of a [4][NJA] array (m0 is the
 // origin of block J0), so a caller short of LDS can stage a sub-tile in several calls.
-template <int EPI, int NJ, bool F8 = false, int J0 = 0, int NJA = NJ>
+// SPLITN (fp32 outputs only): the wave's 64 columns are two 32-column groups, n0 + [0, 32) and
+// n0 + 128 + [0, 32) (contiguous-B-half weight-gradient tiles, gemm256.hip stage_half BCONTIG)
+template <int EPI, int NJ, bool F8 = false, int J0 = 0, int NJA = NJ, bool SPLITN = false>
 __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&acc)[4][NJA],
                                                 int m0, int n0, int split, char* region,
                                                 int lane) {
@@ -423,7 +425,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
       if constexpr (EPI == EPI_F32_ACC || EPI == EPI_CPL_BWD) {
 #pragma unroll
         for (int it = 0; it < PIT; ++it) {
-          int m = m0 + hj * 16 * PJ + it * 4 + (lane >> 4), n = n0 + q * 4;
+          int m = m0 + hj * 16 * PJ + it * 4 + (lane >> 4), n = n0 + q * 4 + (SPLITN && q >= 8 ? 96 : 0);
           m = m < a.M ? m : a.M - 1;
           n = n < a.N ? n : a.N - 4;
           cv[it] = *reinterpret_cast<const float4*>((const float*)a.C + (long)m * a.ldc + n);
@@ -439,7 +441,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
       for (int it = 0; it < PIT; ++it) {
         const int row = it * 4 + (lane >> 4);
         v4f v = *(const LDS_AS v4f*)(region + row * 256 + ((q ^ (row & 7)) << 4));
-        const int m = m0 + hj * 16 * PJ + row, n = n0 + q * 4;
+        const int m = m0 + hj * 16 * PJ + row, n = n0 + q * 4 + (SPLITN && q >= 8 ? 96 : 0);
         if (m < a.M && n < a.N) {
           if constexpr (EPI == EPI_CPL_BWD) {
             const float4 o = cv[it];

@@ -102,7 +102,12 @@ __device__ __forceinline__ v8i cat16(v8s lo, v8s hi) {
 // 128 bytes either way (64 bf16 or 128 e4m3 k-values per row).
 // pair_dh > 0 (EPI_CPL_FWD, B operand): tile row c < 128 -> weight row row0/2 + c, c >= 128 ->
 // pair_dh + row0/2 + c - 128 (the s_hat and t rows of the same 128 features)
-template <bool KMAJOR, int EB = 2>
+// BCONTIG (mn-major B of the weight-gradient products): B-lo / B-hi are the tile's column
+// halves [0, 128) / [128, 256) instead of {wc*64 + 0..31} / {wc*64 + 32..63}, so every k-row
+// of a half is 256 contiguous bytes - whole 128-B lines - where the split halves fetched each
+// line in two 64-B pieces at different times. Wave wc then owns tile columns
+// {wc*32 + 0..31} (N0-1) and {128 + wc*32 + 0..31} (N2-3); the epilogue maps them back.
+template <bool KMAJOR, int EB = 2, bool BCONTIG = false>
 __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long ld, int row0,
                                            int rows_total, int k0, int K, bool is_a, bool hi,
                                            char* dst, int wave, int lane, int pair_dh = 0) {
@@ -126,7 +131,7 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long
       const int lc = (lane & 15) ^ mn_swz(kr);
       int gk = k0 + kr;
       gk = gk < K ? gk : K - 1;
-      int gm = row0 + half_row(is_a, hi, lc * 8);
+      int gm = row0 + ((BCONTIG && !is_a) ? lc * 8 + (hi ? 128 : 0) : half_row(is_a, hi, lc * 8));
       gm = gm < rows_total ? gm : rows_total - 8;
       src = base + (long)gk * ld + gm;
     }
@@ -290,11 +295,18 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
 // of 128 bytes in place of the two bf16 16x16x32 steps - the same LDS image and fragment reads
 // (a lane's 32 k-bytes are the chunks g and g + 4 the bf16 steps read), 2x the FLOPs per
 // MFMA cycle; block scales fixed at 2^0, the per-row / per-tensor scales applied in the epilogue.
-template <bool A_KMAJOR, bool B_KMAJOR, int EPI, int D, bool DB, bool F8 = false>
-__device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int split, char* smem) {
+template <bool A_KMAJOR, bool B_KMAJOR, int EPI, int D, bool DB, bool F8, bool DODB>
+__device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int split,
+                                                  char* smem) {
   constexpr int BKE = F8 ? 2 * BK : BK;  // K-tile in elements
   constexpr int EB = F8 ? 1 : 2;
   constexpr int X = ring_extra(D), NSLOT = 8 + X;
+  // weight-gradient products (both operands mn-major): contiguous B halves (stage_half)
+#ifdef NF_G256_NO_BCONTIG   // A/B build: split B halves on the weight-gradient products too
+  constexpr bool BSPLIT = false;
+#else
+  constexpr bool BSPLIT = !A_KMAJOR && !B_KMAJOR;
+#endif
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -337,23 +349,25 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
-  // bias gradient db[m] = sum_k Aop(m,k) (weight-gradient launches): an MFMA of a ones
-  // fragment against an A fragment the tn == 0 blocks already hold; wave wc takes row group
-  // j == wc of each A half (4 extra MFMAs per K-tile on every wave of those blocks, instead of
-  // 256 VALU on one wave that the block barriers then wait for)
-  const bool do_db = DB && a.dbias != nullptr && tn == 0;
+  // bias gradient db[m] = sum_k Aop(m,k) (weight-gradient launches, tn == 0 blocks: the DODB
+  // instantiation): an MFMA of a ones fragment against A fragment j == wc of each A half, read
+  // once more from LDS with a wave-uniform offset (2 / 4 extra reads and 4 extra MFMAs per
+  // K-tile per wave; selecting fa[wc] from registers compiled to a branch ladder per MFMA)
+  constexpr bool do_db = DODB;
   v4f accb[2] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
   v8s ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;
-  auto db_mfma = [&](v4f& acc_b, const v8s (&f)[4][2], bool two_) {
+  v8s fdb[2];
+  auto db_read = [&](const char* half) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) fdb[ks] = read_frag<A_KMAJOR>(half, wr * 64 + wc * 16, ks, lane);
+  };
+  auto db_mfma = [&](v4f& acc_b, bool two_) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       if (ks == 1 && !two_) break;
-      if (wc == 0) acc_b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f[0][ks], acc_b, 0, 0, 0);
-      else if (wc == 1) acc_b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f[1][ks], acc_b, 0, 0, 0);
-      else if (wc == 2) acc_b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f[2][ks], acc_b, 0, 0, 0);
-      else acc_b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f[3][ks], acc_b, 0, 0, 0);
+      acc_b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fdb[ks], acc_b, 0, 0, 0);
     }
   };
 
@@ -371,7 +385,8 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
       stage_half<B_KMAJOR, EB>(a.B, a.ldb, n0, a.cf_b_rows, k0, ke, false, j == H_BHI, dst, wave,
                                lane, a.cf_dh);
     else
-      stage_half<B_KMAJOR, EB>(a.B, a.ldb, n0, a.N, k0, ke, false, j == H_BHI, dst, wave, lane);
+      stage_half<B_KMAJOR, EB, BSPLIT>(a.B, a.ldb, n0, a.N, k0, ke, false, j == H_BHI, dst, wave,
+                                       lane);
   };
   auto issue_h = [&](int h) { issue(h >> 2, h & 3); };
   // valid halves issued at global phases (P - D, P]; half (t, j) is issued at 4t - 5 - X + j
@@ -422,12 +437,13 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
           fa[j][ks] = read_frag<A_KMAJOR>(slot(t, H_ALO), wr * 64 + j * 16, ks, lane);
+      if constexpr (do_db) db_read(slot(t, H_ALO));
       issue_wait(4 * t + 6 + X, P + 1);
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
       NF_G256_QUAD(0, 0, fbl);
-      if (do_db) db_mfma(accb[0], fa, two);
+      if constexpr (do_db) db_mfma(accb[0], two);
       __builtin_amdgcn_s_setprio(0);
       barrier();
       // ---- r2: M0-3 x N2-3
@@ -449,12 +465,13 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
           fa[j][ks] = read_frag<A_KMAJOR>(slot(t, H_AHI), wr * 64 + j * 16, ks, lane);
+      if constexpr (do_db) db_read(slot(t, H_AHI));
       issue_wait(4 * t + 8 + X, P + 3);
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
       NF_G256_QUAD(2, 4, fbh);
-      if (do_db) db_mfma(accb[1], fa, two);
+      if constexpr (do_db) db_mfma(accb[1], two);
       __builtin_amdgcn_s_setprio(0);
       barrier();
       // ---- r4: M4-7 x N0-1 (no LDS reads)
@@ -482,7 +499,7 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   // ---------------------------------------------------------------- epilogue
   // acc[i][j]: n = n0 + wc*64 + i*16 + (lane>>4)*4 + r, m = m0 + wr*128 + j*16 + (lane&15)
   const int g = lane >> 4, c = lane & 15;
-  if (do_db && g == 0) {  // accb[h]: m = wr*128 + h*64 + wc*16 + (lane & 15), any of the 4 rows
+  if (do_db && a.dbias != nullptr && g == 0) {  // accb[h]: m = wr*128 + h*64 + wc*16 + (lane & 15), any of the 4 rows
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int m = m0 + wr * 128 + h * 64 + wc * 16 + c;
@@ -502,8 +519,12 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
   }
   if (a.staged) {
     barrier();  // every wave is past its last operand read; each wave reuses 16 KiB of LDS
-    epi_tile_staged<EPI, 8, F8>(a, acc, m0 + wr * 128, n0 + wc * 64, split,
-                                smem + wave * 16384, lane);
+    if constexpr (BSPLIT)
+      epi_tile_staged<EPI, 8, F8, 0, 8, true>(a, acc, m0 + wr * 128, n0 + wc * 32, split,
+                                              smem + wave * 16384, lane);
+    else
+      epi_tile_staged<EPI, 8, F8>(a, acc, m0 + wr * 128, n0 + wc * 64, split,
+                                  smem + wave * 16384, lane);
 #ifdef NF_G256_STAMPS
     NF_STAMP(3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -517,11 +538,24 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
     if (m >= a.M) continue;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int n = n0 + wc * 64 + i * 16 + g * 4;
+      const int n = BSPLIT ? n0 + wc * 32 + (i & 1) * 16 + (i >> 1) * 128 + g * 4
+                           : n0 + wc * 64 + i * 16 + g * 4;
       if (n >= a.N) continue;
       epi_store<EPI>(a, acc[i][j], m, n, split);
     }
   }
+}
+
+template <bool A_KMAJOR, bool B_KMAJOR, int EPI, int D, bool DB, bool F8 = false>
+__device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int split, char* smem) {
+  if constexpr (DB) {
+    const int ntn = (a.N + BN - 1) / BN;
+    if (a.dbias != nullptr && wg % ntn == 0) {
+      gemm256_body_impl<A_KMAJOR, B_KMAJOR, EPI, D, DB, F8, true>(a, wg, split, smem);
+      return;
+    }
+  }
+  gemm256_body_impl<A_KMAJOR, B_KMAJOR, EPI, D, DB, F8, false>(a, wg, split, smem);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -859,7 +893,8 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
     return e ? atoi(e) : 1;
   }();
   const bool staged_epi = EPI == EPI_CPL_FWD || a.staged;
-  if (persist_env && !DB && splits == 1 && !a.krange && !a.skip && !a.pair_tiles && staged_epi &&
+  if constexpr (!DB && AK) {
+  if (persist_env && splits == 1 && !a.krange && !a.skip && !a.pair_tiles && staged_epi &&
       g_depth != 6 && a.K > BK) {
     static const int desync_env = [] {
       const char* e = getenv("VINF_G256_DESYNC");
@@ -872,6 +907,7 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
                        a);
     NF_HIP_CHECK(hipGetLastError());
     return;
+  }
   }
   dim3 grid(a.pair_tiles ? ntm * (ntn / 2) : ntm * ntn, splits), block(NTHR);
   if (g_depth != 6)

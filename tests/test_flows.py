@@ -28,12 +28,12 @@ def _jac_logdet(f, z):
     return torch.stack(out)
 
 
-def _check_ldj(flow, D=4, N=6, **kw):
+def _check_ldj(flow, D=4, N=6, atol=1e-8, **kw):
     torch.manual_seed(0)
     z = torch.randn(N, D)
     y, ldj = flow(z, **kw)
     ref = _jac_logdet(lambda x: flow(x, **kw), z)
-    assert torch.allclose(ldj, ref, atol=1e-8), (ldj, ref)
+    assert torch.allclose(ldj, ref, atol=atol), (ldj, ref)
     return y
 
 
@@ -45,7 +45,9 @@ def test_planar_stack_ldj_exact(variant):
         f.W.normal_()
         f.U.normal_()
         f.B.normal_()
-    _check_ldj(f)
+    # each layer's log|psi| carries the reference objective's guard, log(|psi| + 1e-7)
+    # (optimization.py:83): 3 layers with |psi| ~ 1 differ from the exact Jacobian by ~1e-7 each
+    _check_ldj(f, atol=2e-6)
 
 
 def test_planar_uhat_guarantees_invertibility():

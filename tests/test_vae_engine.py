@@ -86,3 +86,17 @@ def test_vae_engine_graph_trains(gpu):
     assert eng.step_t.item() == 203
     assert math.isfinite(eng.loss.item())
     assert eng.loss.item() < first - 50.0, (first, eng.loss.item())
+
+
+@pytest.mark.gpu
+def test_train_cli_planar_vae_uses_engine(gpu, tmp_path):
+    """train.py's planar_vae task on GPU runs the engine (annealed objective, hipGraph) and
+    still writes the reference-format weights + free_energy.txt."""
+    from vi_normflows_amd.train import main
+
+    final = main(["--config", "mnist_planar_vae", "iters=120", "log_every=40",
+                  f"out_dir={tmp_path}", "name=vae_eng", "extra.n_data=300"])
+    assert final["engine"] == "vae_engine"
+    assert math.isfinite(final["free_energy_per_sample"])
+    out = tmp_path / "vae_eng"
+    assert (out / "weights_phi_4.npy").exists() and (out / "free_energy.txt").exists()

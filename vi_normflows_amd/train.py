@@ -118,11 +118,48 @@ def run_planar_vae(cfg, out, info, logger):
             X = X[torch.randperm(X.shape[0], generator=torch.Generator().manual_seed(cfg.seed))[:n]]
     else:
         X = synthetic_binary_images(cfg.extra.get("n_data", 2000), cfg.dim, seed=cfg.seed)
-    vae = PlanarVAE(VAEConfig(dim_x=cfg.dim, dim_z=cfg.dim_z, K=cfg.K, width=cfg.hidden,
-                              hidden_layers=cfg.n_hidden))
+    vcfg = VAEConfig(dim_x=cfg.dim, dim_z=cfg.dim_z, K=cfg.K, width=cfg.hidden,
+                     hidden_layers=cfg.n_hidden)
+    vae = PlanarVAE(vcfg)
     vae.init_reference(generator=torch.Generator().manual_seed(cfg.seed))
     vae.to(dev)
     it = make_batch_iter(X, cfg.batch, cfg.iters, generator=g, rank=info.rank, world=info.world)
+    engine_ok = (dev.type == "cuda" and info.world == 1 and cfg.optimizer == "adam"
+                 and cfg.schedule in ("none", "reference") and cfg.hidden == 64
+                 and 1 <= cfg.n_hidden <= 4 and cfg.dim_z % 4 == 0 and cfg.dim_z <= 64
+                 and cfg.K <= 8 and cfg.dim % 4 == 0 and cfg.dim <= 1024
+                 and cfg.extra.get("engine", True))
+    if engine_ok:
+        # models/vae_engine.py: the whole step in two HIP launches + flat Adam, one hipGraph
+        from .models.vae_engine import PlanarVAEEngine
+
+        eng = PlanarVAEEngine(vcfg, batch=cfg.batch, device=dev, seed=rank_seed(cfg.seed, info.rank),
+                              lr=cfg.lr, anneal=cfg.schedule, anneal_iters=cfg.iters)
+        eng.load_module(vae)
+
+        def full(xb):   # the graph has a static batch: a short last batch is topped up by
+            n = xb.shape[0]   # repeating its own rows (same expectation, slightly reweighted)
+            return xb if n == cfg.batch else xb[torch.arange(cfg.batch) % n]
+
+        eng.set_batch(full(it(0)).to(dev))
+        graph = eng.capture(warmup=1)
+        eng.params.m.zero_()           # the capture warm-up stepped Adam: start from the init
+        eng.params.v.zero_()
+        eng.load_module(vae)
+        eng.step_t.zero_()
+        F = float("nan")
+        for t in range(cfg.iters):
+            eng.set_batch(full(it(t)).to(dev))
+            graph.replay()
+            if (t + 1) % max(cfg.log_every, 1) == 0 or t + 1 == cfg.iters:
+                F = eng.loss.item()
+                if logger is not None:
+                    logger.log({"step": t + 1, "F": F, "beta": eng.beta.item()})
+        if info.is_main:
+            vae = eng.to_module(vae)
+            vae.cpu().save_reference(out / f"weights_phi_{cfg.K}.npy", out / f"weights_theta_{cfg.K}.npy")
+            append_free_energy(out / "free_energy.txt", cfg.K, F * cfg.batch)
+        return {"free_energy_per_sample": F, "engine": "vae_engine"}
     gd = torch.Generator(device=dev).manual_seed(rank_seed(cfg.seed, info.rank))
 
     def loss_fn(t, beta):
