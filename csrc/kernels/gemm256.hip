@@ -302,10 +302,13 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
   constexpr int EB = F8 ? 1 : 2;
   constexpr int X = ring_extra(D), NSLOT = 8 + X;
   // weight-gradient products (both operands mn-major): contiguous B halves (stage_half)
-#ifdef NF_G256_NO_BCONTIG   // A/B build: split B halves on the weight-gradient products too
-  constexpr bool BSPLIT = false;
-#else
+  // contiguous B halves for the weight-gradient products (stage_half BCONTIG): measured 4.5 %
+  // slower on the grouped weight-gradient launch (428 -> 447 us, profiles/r2_bcontig_ab.txt),
+  // kept as an opt-in A/B build (-D NF_G256_BCONTIG)
+#ifdef NF_G256_BCONTIG
   constexpr bool BSPLIT = !A_KMAJOR && !B_KMAJOR;
+#else
+  constexpr bool BSPLIT = false;
 #endif
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
