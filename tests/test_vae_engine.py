@@ -100,3 +100,23 @@ def test_train_cli_planar_vae_uses_engine(gpu, tmp_path):
     assert math.isfinite(final["free_energy_per_sample"])
     out = tmp_path / "vae_eng"
     assert (out / "weights_phi_4.npy").exists() and (out / "free_energy.txt").exists()
+
+
+@pytest.mark.gpu
+def test_fused_bernoulli_loglik_matches_composite(gpu):
+    """PlanarVAE.log_joint's fused HIP likelihood (elbo.hip, value + gradient in one pass) vs
+    the softplus composite, value and gradient."""
+    from vi_normflows_amd.distributions.functional import log_bern_logits
+    from vi_normflows_amd.ops.fused import bernoulli_loglik
+
+    torch.manual_seed(0)
+    x = synthetic_binary_images(96, 784, seed=3).to(gpu)
+    l1 = (torch.randn(96, 784, device=gpu) * 4).requires_grad_()
+    l2 = l1.detach().clone().requires_grad_()
+    w = torch.randn(96, device=gpu)
+    a = bernoulli_loglik(l1, x)
+    b = log_bern_logits(x, l2)
+    (a * w).sum().backward()
+    (b * w).sum().backward()
+    assert torch.allclose(a, b, rtol=1e-5, atol=1e-3)
+    assert torch.allclose(l1.grad, l2.grad, rtol=1e-5, atol=1e-6)

@@ -82,7 +82,12 @@ class PlanarVAE(nn.Module):
         return torch.sigmoid(self.decoder(z))
 
     def log_joint(self, x, z):
-        return log_bern_logits(x, self.decode_logits(z)) + log_std_norm(z)
+        logits = self.decode_logits(z)
+        if logits.is_cuda and logits.dim() == 2:   # fused HIP likelihood + gradient (elbo.hip)
+            from ..ops.fused import bernoulli_loglik
+
+            return bernoulli_loglik(logits, x) + log_std_norm(z)
+        return log_bern_logits(x, logits) + log_std_norm(z)
 
     def loss(self, x, beta: float = 1.0, generator=None, with_stats: bool = True):
         res, _ = amortized_free_energy(x, self.encode, self.flow, self.log_joint, beta, generator,

@@ -149,7 +149,10 @@ class PlanarVAEEngine:
         dz = self.cfg.dim_z
         lq0 = -0.5 * dz * math.log(2 * math.pi) - 0.5 * lv.sum(1) - 0.5 * (eps * eps).sum(1)
         zK, ldj = model.flow(z0, fp)
-        lp = model.log_joint(self.x, zK)
+        # pure torch composite (the module path's log_joint uses the fused elbo.hip kernel)
+        from ..distributions.functional import log_bern_logits, log_std_norm
+
+        lp = log_bern_logits(self.x, model.decode_logits(zK)) + log_std_norm(zK)
         frow = lq0 - ldj - self.beta * lp
         F = frow.mean()
         model.zero_grad(set_to_none=True)

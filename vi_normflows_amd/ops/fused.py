@@ -139,3 +139,36 @@ def maf_bwd(gu, u, o, dout, gx, bound=5.0, c_ldj=0.0):
         native().maf_bwd(gu, u, o, float(bound), float(c_ldj), dout, gx)
     else:
         ref.maf_bwd(gu, u, o, float(bound), float(c_ldj), dout, gx)
+
+
+class BernoulliLogitsLL(torch.autograd.Function):
+    """Per-row Bernoulli log-likelihood from logits, sum_j x_j l_j - softplus(l_j), with its
+    gradient dL/dl = x - sigmoid(l) produced by the SAME HIP pass (csrc/kernels/elbo.hip
+    bernoulli_logits) and scaled by the incoming per-row gradient in the backward: the
+    module-path PlanarVAE's likelihood (reference distributions.py:86-89, Q9 fixed) in one
+    kernel instead of the softplus / mul / sub / sum composite and its autograd graph."""
+
+    @staticmethod
+    def forward(ctx, logits, x):
+        lg = logits.contiguous()
+        xc = x.contiguous().float()
+        dl = torch.empty_like(lg)
+        lp = torch.empty(lg.shape[0], device=lg.device, dtype=torch.float32)
+        bernoulli_logits(lg, xc, dlogits=dl, coef_host=1.0, logpx=lp)
+        ctx.save_for_backward(dl)
+        return lp
+
+    @staticmethod
+    def backward(ctx, g):
+        (dl,) = ctx.saved_tensors
+        return dl * g.to(dl.dtype).unsqueeze(1), None
+
+
+def bernoulli_loglik(logits, x):
+    """log p(x | logits) per row; fused HIP kernel (with its gradient) for 2-D fp32 / bf16 GPU
+    logits, torch composite otherwise."""
+    if (_gpu(logits) and logits.dim() == 2 and logits.dtype in (torch.float32, torch.bfloat16)
+            and x.shape == logits.shape):
+        return BernoulliLogitsLL.apply(logits, x)
+    ll = x * logits - torch.nn.functional.softplus(logits)
+    return ll.reshape(ll.shape[0], -1).sum(1)
