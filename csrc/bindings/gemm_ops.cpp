@@ -651,6 +651,11 @@ void gemm_fp8_nt(const at::Tensor& xq, const at::Tensor& sx, const at::Tensor& w
 }
 
 void gemm_set_mode(int64_t mode, int64_t depth) { nf_gemm_set_mode((int)mode, (int)depth); }
+int64_t gemm_persist(int64_t on) {   // on < 0: query only; returns the previous setting
+  const int prev = nf_gemm256_get_persist();
+  if (on >= 0) nf_gemm256_set_persist((int)on);
+  return prev;
+}
 
 #ifdef NF_G256_STAMPS
 void nf_g256_set_stamps(void* p);
@@ -662,6 +667,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("g256_set_stamps(Tensor buf) -> ()", &g256_set_stamps);
 #endif
   m.def("gemm_set_mode(int mode, int depth) -> ()", &gemm_set_mode);
+  m.def("gemm_persist(int on) -> int", &gemm_persist);
   m.def("fp8_quant_rows(Tensor x, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("fp8_quant_tensor(Tensor x, Tensor(a!) q, Tensor amax_prev, Tensor(b!) scale, Tensor(c!) amax_cur) -> ()");
   m.def("gemm_fp8_nt(Tensor xq, Tensor sx, Tensor wq, Tensor sw, Tensor? b, Tensor(a!) y, int relu, Tensor? krange, Tensor(b!)? yq=None, Tensor? q_amax_prev=None, Tensor(c!)? q_scale=None, Tensor(d!)? q_amax_cur=None, Tensor? krange256=None) -> ()");

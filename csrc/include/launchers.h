@@ -94,6 +94,8 @@ void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, co
                           int N, int K, hipStream_t stream, int aux_is_bits = 0,
                           const int* krange = nullptr, int krange_segs = 1, int w_kmajor = 0);
 void nf_gemm256_set_depth(int d);
+void nf_gemm256_set_persist(int on);
+int nf_gemm256_get_persist();
 // input gradient with W given transposed (Wt [N][K]): NT instantiation, bf16 (ReLU-mask) epilogue
 void nf_launch_gemm256_nt_dgrad(const void* dy, long lddy, const void* Wt, long ldwt,
                                 const void* aux, long ld_aux, int aux_is_bits, void* dx,

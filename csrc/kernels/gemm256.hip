@@ -858,6 +858,14 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
   gemm256_body<false, false, EPI_F32, D, true>(a, local, 0, smem);
 }
 
+// persistent plain products: VINF_G256_PERSIST at load, or nf_gemm256_set_persist (the DP
+// runner turns it off for multi-rank jobs: RCCL kernels take CUs while a grid of exactly one
+// block per CU runs, and a persistent block that cannot start delays its whole tile list)
+static int g_persist = [] {
+  const char* e = getenv("VINF_G256_PERSIST");
+  return e ? atoi(e) : 1;
+}();
+
 static int g_depth = [] {
   const char* e = getenv("VINF_G256_DEPTH");
   return e && atoi(e) == 6 ? 6 : 4;
@@ -891,10 +899,7 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
                  (pair_env == 2 || (long)ntm * (ntn / 2) >= device_cus_256());
   // plain products run persistent (one continuous LDS-DMA stream per block, see
   // gemm256_persistent_body); VINF_G256_PERSIST=0 restores one tile per block
-  static const int persist_env = [] {
-    const char* e = getenv("VINF_G256_PERSIST");
-    return e ? atoi(e) : 1;
-  }();
+  const int persist_env = g_persist;
   const bool staged_epi = EPI == EPI_CPL_FWD || a.staged;
   if constexpr (!DB && AK) {
   if (persist_env && splits == 1 && !a.krange && !a.skip && !a.pair_tiles && staged_epi &&
@@ -929,6 +934,8 @@ using namespace nf::gemm;
 // 4 (default): 8-slot LDS ring, 128 KiB; 6: 10-slot ring, 160 KiB, half-tiles issued 2 phases
 // earlier (VINF_G256_DEPTH at load, or set_mode's depth argument)
 void nf_gemm256_set_depth(int d) { g256::g_depth = d == 6 ? 6 : 4; }
+void nf_gemm256_set_persist(int on) { g256::g_persist = on ? 1 : 0; }
+int nf_gemm256_get_persist() { return g256::g_persist; }
 
 // y[M][N] = act(x[M][K] W[N][K]^T + bias) -> bf16
 void nf_launch_gemm256_nt(const void* x, long ldx, const void* W, long ldw, const void* bias,

@@ -127,3 +127,21 @@ def test_persistent_repeatable(gpu):
     for _ in range(10):
         torch.ops.vinf.gemm_nt(x, W, b, y, 1, m)
         assert torch.equal(y, y0) and torch.equal(m, m0)
+
+
+def test_persistent_switch_bitwise(gpu):
+    """gemm_persist(0) (what the DP runner sets for multi-rank jobs) launches one block per tile;
+    each tile's K order is the same, so both forms give bitwise-identical outputs."""
+    torch.manual_seed(6)
+    M, N, K = 70000, 1024, 1024
+    x, W, b = _bf(M, K, device=gpu), _bf(N, K, device=gpu, scale=0.05), _bf(N, device=gpu)
+    y1 = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    y0 = torch.empty_like(y1)
+    prev = torch.ops.vinf.gemm_persist(1)
+    try:
+        torch.ops.vinf.gemm_nt(x, W, b, y1, 1, None)
+        torch.ops.vinf.gemm_persist(0)
+        torch.ops.vinf.gemm_nt(x, W, b, y0, 1, None)
+    finally:
+        torch.ops.vinf.gemm_persist(prev)
+    assert torch.equal(y0, y1)

@@ -54,6 +54,13 @@ class DataParallelRunner:
         force = force_reduce or os.environ.get("VINF_FORCE_REDUCE", "0") == "1"
         if force and info.world == 1 and not dist.is_initialized():
             _init_single_rank_group(info)
+        if info.world > 1 and engine.device.type == "cuda" and os.environ.get("VINF_DP_PERSIST", "0") != "1":
+            # multi-rank: RCCL kernels run on CUs beside the step's GEMMs; a persistent GEMM
+            # grid (one block per CU, each owning a fixed tile list) would wait for every CU an
+            # all-reduce holds, so the products launch one block per tile instead
+            from ..ops._ext import native
+
+            native().gemm_persist(0)
         if info.world > 1 or (force and dist.is_initialized()):
             P = engine.params
             if info.world > 1:
