@@ -99,6 +99,7 @@ struct GemmArgs {
   int cf_dh, cf_b_rows;
   float cf_scale;
   int desync;                  // persistent gemm256: s_sleep(127) rounds odd blocks wait up front
+  int no_rot;                  // persistent gemm256: keep each block on one column (A/B knob)
 };
 
 // LDS-staged epilogue switch (VINF_GEMM_STAGED_EPI=0 restores the fragment-layout stores) and

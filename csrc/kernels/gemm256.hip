@@ -589,10 +589,18 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
   const int G = gridDim.x, b = blockIdx.x;
   const int ns = (ntiles - b + G - 1) / G;          // tiles of this block
   const int nkt = (a.K + BK - 1) / BK;              // K-tiles per tile
+  // Column rotation: with every block holding the same number of tiles and each XCD's step-s
+  // ids a run of whole tile rows, block b's s-th tile takes column (tn + s) % ntn - still one
+  // tile per (row, column) per step, same rows in flight per XCD, but every block now meets
+  // each column tile once. Without it the blocks whose ids sit on the last column get ALL of
+  // its cheap edge tiles (the coupling products' 8-feature / 136-column remainders) and the
+  // others all of the full ones, and the launch lasts as long as the full-tile blocks.
+  const bool rot = !a.no_rot && (G & 7) == 0 && ntiles % G == 0 && ((ntiles >> 3) % ntn) == 0 &&
+                   ((G >> 3) % ntn) == 0;
   auto tile_org = [&](int s, int& m0, int& n0) {
     const int id = xcd_remap(b + s * G, ntiles);
     m0 = (id / ntn) * BM;
-    n0 = (id % ntn) * BN;
+    n0 = (rot ? (id % ntn + s) % ntn : id % ntn) * BN;
   };
   // stage half j of K-tile tk of the tile at (tm0, tn0) into the ring slot of stream half
   // 4 Tg + j
@@ -908,7 +916,12 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
       const char* e = getenv("VINF_G256_DESYNC");
       return e ? atoi(e) : 0;
     }();
+    static const int rot_env = [] {
+      const char* e = getenv("VINF_G256_ROT");
+      return e ? atoi(e) : 1;
+    }();
     a.desync = desync_env;
+    a.no_rot = rot_env ? 0 : 1;
     const int ntiles = ntm * ntn, cus = device_cus_256();
     const int G = ntiles < cus ? ntiles : cus;
     hipLaunchKernelGGL((gemm256_persistent_kernel<AK, BK_, EPI>), dim3(G), dim3(NTHR), 0, stream,

@@ -60,12 +60,15 @@ def test_persistent_f32_accumulate(gpu):
     _check(out, dy.float() @ W.float() + base, 2e-2)
 
 
-def test_persistent_fused_coupling_fwd_bwd(gpu):
+# M = 65536: 256 row tiles, every block holds the same tile count -> the column rotation is on
+# (each block meets the 8-feature / 136-column edge tiles once); 66000: uneven, rotation off
+@pytest.mark.parametrize("M", [66000, 65536])
+def test_persistent_fused_coupling_fwd_bwd(gpu, M):
     """EPI_CPL_FWD (two staged row passes) and EPI_CPL_BWD (fp32 passes) at a multi-tile M."""
     from vi_normflows_amd.ops import gemm
 
     torch.manual_seed(9)
-    M, K, Dh = 66000, 1024, 392
+    K, Dh = 1024, 392
     h = _bf(M, K, device=gpu)
     W = torch.zeros(800, K, device=gpu)
     W[:2 * Dh] = torch.randn(2 * Dh, K, device=gpu) * 0.03
