@@ -43,8 +43,9 @@ def test_optimizers_follow_autograd_rules():
         x = x + lr * v
         ref.append(x.clone())
     assert torch.allclose(_opt_trace("sgd", lr), torch.stack(ref))
-    # autograd rmsprop: avg = g avg + (1-g) grad^2 ; x -= lr grad / (sqrt(avg) + eps)
-    x, avg, gam, eps = torch.tensor([1.0, -2.0], dtype=torch.float64), torch.zeros(2, dtype=torch.float64), 0.9, 1e-8
+    # autograd rmsprop: avg = g avg + (1-g) grad^2 ; x -= lr grad / (sqrt(avg) + eps), with the
+    # accumulator starting at np.ones(len(x))
+    x, avg, gam, eps = torch.tensor([1.0, -2.0], dtype=torch.float64), torch.ones(2, dtype=torch.float64), 0.9, 1e-8
     ref = []
     for _ in range(5):
         g = 2 * x * torch.tensor([1.0, 3.0], dtype=torch.float64)
@@ -52,6 +53,15 @@ def test_optimizers_follow_autograd_rules():
         x = x - 0.01 * g / (torch.sqrt(avg) + eps)
         ref.append(x.clone())
     assert torch.allclose(_opt_trace("rmsprop", 0.01), torch.stack(ref))
+    # the torch rule (zero-initialised accumulator) stays available under its own name
+    x, avg = torch.tensor([1.0, -2.0], dtype=torch.float64), torch.zeros(2, dtype=torch.float64)
+    ref = []
+    for _ in range(5):
+        g = 2 * x * torch.tensor([1.0, 3.0], dtype=torch.float64)
+        avg = gam * avg + (1 - gam) * g * g
+        x = x - 0.01 * g / (torch.sqrt(avg) + eps)
+        ref.append(x.clone())
+    assert torch.allclose(_opt_trace("rmsprop_torch", 0.01), torch.stack(ref))
 
 
 def test_bbvi_matches_closed_form_posterior(reference_dir):

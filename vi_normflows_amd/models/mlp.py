@@ -155,8 +155,10 @@ class Feedforward:
             W = torch.tensor(weights_init, dtype=torch.float64, requires_grad=True)
             if optimizer == "adam":
                 opt = torch.optim.Adam([W], lr=step_size)
-            elif optimizer == "rmsprop":   # autograd rmsprop: gamma 0.9, eps 1e-8
-                opt = torch.optim.RMSprop([W], lr=step_size, alpha=0.9, eps=1e-8)
+            elif optimizer == "rmsprop":   # autograd rmsprop: gamma 0.9, eps 1e-8, ones-init
+                from ..inference.optimizers import AutogradRMSprop
+
+                opt = AutogradRMSprop([W], lr=step_size)
             else:
                 opt = None
                 vel = torch.zeros_like(W)
