@@ -39,6 +39,8 @@ void chk_q(const at::Tensor& t, const char* n) {
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, n, " must be 16-B aligned");
 }
 
+void chk_ranges(const at::Tensor& r, long ntiles, const char* n);
+
 // y = act(x W^T + b): x [M,K], W [N,K], b [N] (bf16), y [M,N] bf16
 void gemm_nt(const at::Tensor& x, const at::Tensor& W, const c10::optional<at::Tensor>& b,
              const at::Tensor& y, int64_t relu, const c10::optional<at::Tensor>& mask) {
@@ -343,17 +345,203 @@ void gemm_nn_cpl(const at::Tensor& dy, const at::Tensor& W, const at::Tensor& G,
                            use_wt ? 1 : 0);
 }
 
+// MAF layer l's second MADE product with the layer's transform fused (gemm256.hip
+// nf_launch_gemm256_maf_fwd): bf16 operands, or e4m3 (h / W float8 with hs = h's per-tensor
+// scale, ws = W's per-row scales, optional e4m3 copy uq of u under a delayed scale).
+void maf_gemm_fwd(const at::Tensor& h, const c10::optional<at::Tensor>& hs, const at::Tensor& W,
+                  const c10::optional<at::Tensor>& ws, const c10::optional<at::Tensor>& b,
+                  const at::Tensor& krange, const at::Tensor& s_out, const at::Tensor& x,
+                  const at::Tensor& u, const c10::optional<at::Tensor>& ubf, const at::Tensor& ldjp,
+                  bool ldj_init, double bound, const c10::optional<at::Tensor>& uq,
+                  const c10::optional<at::Tensor>& q_amax_prev,
+                  const c10::optional<at::Tensor>& q_scale,
+                  const c10::optional<at::Tensor>& q_amax_cur) {
+  const bool f8 = h.scalar_type() != at::kBFloat16;
+  if (f8) {
+    chk_q(h, "h");
+    chk_q(W, "W");
+    TORCH_CHECK(hs && hs->defined() && ws && ws->defined(), "fp8 operands need hs and ws");
+    TORCH_CHECK(hs->is_cuda() && hs->scalar_type() == at::kFloat && hs->numel() >= 1, "hs");
+    TORCH_CHECK(ws->is_cuda() && ws->scalar_type() == at::kFloat && ws->is_contiguous() &&
+                    ws->numel() == W.size(0), "ws: fp32 [2D]");
+  } else {
+    chk_mat(h, "h", at::kBFloat16);
+    chk_mat(W, "W", at::kBFloat16);
+  }
+  chk_mat(s_out, "s_out", at::kBFloat16);
+  chk_mat(x, "x", at::kFloat);
+  chk_mat(u, "u", at::kFloat);
+  const int M = h.size(0), K = h.size(1), D = x.size(1);
+  TORCH_CHECK(W.size(0) == 2 * D && W.size(1) == K, "W must be [2D, K]");
+  TORCH_CHECK(D % 128 == 0 && x.size(0) == M && u.size(0) == M && u.size(1) == D &&
+                  s_out.size(0) == M && s_out.size(1) == D, "maf_gemm_fwd shapes (D % 128 == 0)");
+  chk_ranges(krange, D / 128, "krange");
+  TORCH_CHECK(ldjp.is_cuda() && ldjp.scalar_type() == at::kFloat && ldjp.dim() == 2 &&
+                  ldjp.size(0) >= D / 128 && ldjp.size(1) == M && ldjp.stride(1) == 1,
+              "ldjp: fp32 [D/128, M]");
+  const void* bp = nullptr;
+  if (b && b->defined()) {
+    TORCH_CHECK(b->scalar_type() == at::kBFloat16 && b->numel() == 2 * D && b->is_contiguous(),
+                "b: bf16 [2D]");
+    bp = b->data_ptr();
+  }
+  void* ubp = nullptr;
+  long ldub = 0;
+  if (ubf && ubf->defined()) {
+    chk_mat(*ubf, "ubf", at::kBFloat16);
+    TORCH_CHECK(ubf->size(0) == M && ubf->size(1) == D, "ubf shape");
+    ubp = ubf->data_ptr();
+    ldub = ld2(*ubf);
+  }
+  void* qp = nullptr;
+  long ldq = 0;
+  const float* qap = nullptr;
+  float* qs = nullptr;
+  float* qac = nullptr;
+  if (uq && uq->defined()) {
+    TORCH_CHECK(f8, "the e4m3 copy of u belongs to the fp8 path");
+    chk_q(*uq, "uq");
+    TORCH_CHECK(uq->size(0) == M && uq->size(1) == D, "uq shape");
+    TORCH_CHECK(q_amax_prev && q_scale && q_amax_cur, "uq needs the delayed-scale state");
+    chk_amax_slots(*q_amax_cur);
+    qp = uq->data_ptr();
+    ldq = ld2(*uq);
+    qap = q_amax_prev->data_ptr<float>();
+    qs = q_scale->data_ptr<float>();
+    qac = q_amax_cur->data_ptr<float>();
+  }
+  nf_launch_gemm256_maf_fwd(h.data_ptr(), ld2(h), f8 ? 1 : 0, f8 ? hs->data_ptr<float>() : nullptr,
+                            W.data_ptr(), ld2(W), f8 ? ws->data_ptr<float>() : nullptr, bp,
+                            krange.data_ptr<int>(), s_out.data_ptr(), ld2(s_out), M, K, D,
+                            x.data_ptr<float>(), ld2(x), u.data_ptr<float>(), ld2(u), ubp, ldub,
+                            ldjp.data_ptr<float>(), ldjp.stride(0), ldj_init, (float)bound, qp, ldq,
+                            qap, qs, qac, cur_stream());
+}
+
+// MAF layer l's first MADE product input gradient (gy = G + dy (W1*M1), NT against Wt = (W1*M1)^T,
+// never stored) fused with the MAF backward of layer l-1: dst = [dmu | ds_raw] (bf16 [M, 2D]),
+// gx = gy e^-alpha (fp32); s_raw / u are layer l-1's (u = the input of layer l).
+// fp8: dy / Wt e4m3 with sa (dy's per-tensor scale) and sb (Wt's per-row scales), and
+// optionally the e4m3 copy dstq of dst under a delayed scale.
+struct F8Out {
+  void* q = nullptr;
+  long ldq = 0;
+  const float* ap = nullptr;
+  float* qs = nullptr;
+  float* ac = nullptr;
+};
+F8Out f8_out(const c10::optional<at::Tensor>& q, const c10::optional<at::Tensor>& amax_prev,
+             const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& amax_cur,
+             long rows, long cols) {
+  F8Out o;
+  if (!(q && q->defined())) return o;
+  chk_q(*q, "q");
+  TORCH_CHECK(q->size(0) == rows && q->size(1) == cols, "e4m3 copy shape");
+  TORCH_CHECK(amax_prev && scale && amax_cur && amax_prev->defined() && scale->defined() &&
+                  amax_cur->defined(), "the e4m3 copy needs the delayed-scale state");
+  chk_amax_slots(*amax_cur);
+  o.q = q->data_ptr();
+  o.ldq = ld2(*q);
+  o.ap = amax_prev->data_ptr<float>();
+  o.qs = scale->data_ptr<float>();
+  o.ac = amax_cur->data_ptr<float>();
+  return o;
+}
+
+void chk_scales(const c10::optional<at::Tensor>& sa, const c10::optional<at::Tensor>& sb,
+                long nb) {
+  TORCH_CHECK(sa && sa->defined() && sb && sb->defined(), "fp8 operands need sa and sb");
+  TORCH_CHECK(sa->is_cuda() && sa->scalar_type() == at::kFloat && sa->numel() >= 1, "sa");
+  TORCH_CHECK(sb->is_cuda() && sb->scalar_type() == at::kFloat && sb->is_contiguous() &&
+                  sb->numel() == nb && ((uintptr_t)sb->data_ptr() & 15) == 0,
+              "sb: fp32 per-row scales, 16-B aligned");
+}
+
+// masked input gradient on e4m3 operands with the ReLU-mask epilogue (gemm256.hip
+// nf_launch_gemm256_fp8_dgrad): dx = relu'(h) * (dyq sa)(Wtq sb)^T (bf16) + optional e4m3 dxq
+void fp8_dgrad(const at::Tensor& dyq, const at::Tensor& sa, const at::Tensor& Wtq,
+               const at::Tensor& sb, const at::Tensor& h, const at::Tensor& dx,
+               const at::Tensor& krange256, const c10::optional<at::Tensor>& dxq,
+               const c10::optional<at::Tensor>& q_amax_prev,
+               const c10::optional<at::Tensor>& q_scale,
+               const c10::optional<at::Tensor>& q_amax_cur) {
+  chk_q(dyq, "dyq");
+  chk_q(Wtq, "Wtq");
+  chk_mat(h, "h", at::kBFloat16);
+  chk_mat(dx, "dx", at::kBFloat16);
+  const int M = dyq.size(0), K = dyq.size(1), N = Wtq.size(0);
+  TORCH_CHECK(Wtq.size(1) == K && K % 128 == 0 && N % 8 == 0, "Wtq [N, K], K % 128 == 0");
+  TORCH_CHECK(h.size(0) == M && h.size(1) == N && dx.size(0) == M && dx.size(1) == N, "h / dx");
+  chk_scales(sa, sb, N);
+  const long nt = (N + 255) / 256;
+  const int segs = krange256.numel() == 4 * nt ? 2 : 1;
+  chk_ranges(krange256, segs * nt, "krange256");
+  const F8Out o = f8_out(dxq, q_amax_prev, q_scale, q_amax_cur, M, N);
+  nf_launch_gemm256_fp8_dgrad(dyq.data_ptr(), ld2(dyq), sa.data_ptr<float>(), Wtq.data_ptr(),
+                              ld2(Wtq), sb.data_ptr<float>(), h.data_ptr(), ld2(h), 0,
+                              dx.data_ptr(), ld2(dx), M, N, K, krange256.data_ptr<int>(), segs,
+                              o.q, o.ldq, o.ap, o.qs, o.ac, cur_stream());
+}
+
+void maf_gemm_bwd(const at::Tensor& dy, const at::Tensor& Wt, const at::Tensor& krange256,
+                  const at::Tensor& G, const at::Tensor& s_raw, const at::Tensor& u,
+                  const at::Tensor& dst, const at::Tensor& gx, double bound, double c,
+                  const c10::optional<at::Tensor>& sa, const c10::optional<at::Tensor>& sb,
+                  const c10::optional<at::Tensor>& dstq,
+                  const c10::optional<at::Tensor>& q_amax_prev,
+                  const c10::optional<at::Tensor>& q_scale,
+                  const c10::optional<at::Tensor>& q_amax_cur) {
+  const bool f8 = dy.scalar_type() != at::kBFloat16;
+  if (f8) {
+    chk_q(dy, "dy");
+    chk_q(Wt, "Wt");
+    chk_scales(sa, sb, Wt.size(0));
+  } else {
+    chk_mat(dy, "dy", at::kBFloat16);
+    chk_mat(Wt, "Wt", at::kBFloat16);
+    TORCH_CHECK(!(dstq && dstq->defined()), "the e4m3 copy of dst belongs to the fp8 path");
+  }
+  chk_mat(s_raw, "s_raw", at::kBFloat16);
+  chk_mat(dst, "dst", at::kBFloat16);
+  chk_mat(G, "G", at::kFloat);
+  chk_mat(u, "u", at::kFloat);
+  chk_mat(gx, "gx", at::kFloat);
+  const int M = dy.size(0), K = dy.size(1), D = Wt.size(0);
+  TORCH_CHECK(Wt.size(1) == K && K % 32 == 0 && D % 8 == 0, "Wt must be [D, K], K % 32 == 0");
+  for (const at::Tensor* t : {&G, &s_raw, &u, &gx})
+    TORCH_CHECK(t->size(0) == M && t->size(1) == D, "G / s_raw / u / gx: [M, D]");
+  TORCH_CHECK(dst.size(0) == M && dst.size(1) == 2 * D, "dst: bf16 [M, 2D]");
+  const long nt = (D + 255) / 256;
+  const int segs = krange256.numel() == 4 * nt ? 2 : 1;
+  chk_ranges(krange256, segs * nt, "krange256");
+  NfF8Operands fo{};
+  if (f8) {
+    const F8Out o = f8_out(dstq, q_amax_prev, q_scale, q_amax_cur, M, 2 * D);
+    fo.sa = sa->data_ptr<float>();
+    fo.sb = sb->data_ptr<float>();
+    fo.q = o.q; fo.ldq = o.ldq;
+    fo.q_amax_prev = o.ap; fo.q_scale_out = o.qs; fo.q_amax_cur = o.ac;
+  }
+  nf_launch_gemm256_nn_cpl(dy.data_ptr(), ld2(dy), Wt.data_ptr(), ld2(Wt), G.data_ptr<float>(),
+                           ld2(G), M, D, K, s_raw.data_ptr(), ld2(s_raw), u.data_ptr<float>(),
+                           ld2(u), dst.data_ptr(), ld2(dst), 2 * D, gx.data_ptr<float>(), ld2(gx),
+                           D, (float)bound, (float)c, cur_stream(), 1, krange256.data_ptr<int>(),
+                           segs, 1, f8 ? &fo : nullptr);
+}
+
 // all `layers` weights of one kind (rows_per x C each, layer_stride elements apart in the flat
 // fp32 buffer starting at x) quantised per row in one launch
 void fp8_quant_rows_strided(const at::Tensor& x, int64_t layer_stride, int64_t rows_per,
                             int64_t layers, int64_t C, const at::Tensor& q, const at::Tensor& scale) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(), "x fp32 GPU");
+  TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16) &&
+                  x.is_contiguous(), "x fp32 / bf16 GPU");
   TORCH_CHECK(x.numel() >= (layers - 1) * layer_stride + rows_per * C, "x too small");
   chk_q(q, "q");
   TORCH_CHECK(q.size(0) == rows_per * layers && q.size(1) >= C && q.size(1) % 4 == 0, "q shape");
   TORCH_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat &&
                   scale.numel() == rows_per * layers, "scale");
-  nf_launch_fp8_quant_rows_strided(x.data_ptr(), 0, C, layer_stride, (int)rows_per,
+  nf_launch_fp8_quant_rows_strided(x.data_ptr(), x.scalar_type() == at::kBFloat16, C,
+                                   layer_stride, (int)rows_per,
                                    (int)(rows_per * layers), (int)C, q.data_ptr(), ld2(q), q.size(1),
                                    scale.data_ptr<float>(), cur_stream());
 }
@@ -406,15 +594,18 @@ void maf_bwd(const at::Tensor& gu, const at::Tensor& u, const at::Tensor& o, dou
   chk_mat(dout, "dout", at::kBFloat16);
   chk_mat(gx, "gx", at::kFloat);
   const int B = gu.size(0), D = gu.size(1);
-  TORCH_CHECK(D % 4 == 0 && u.size(0) == B && u.size(1) == D && o.size(1) == 2 * D &&
-                  dout.size(1) == 2 * D && gx.size(1) == D, "maf_bwd shapes");
+  // o = [mu | s_raw] [B, 2D], or the s_raw half alone [B, D] (the fused engine keeps only s)
+  TORCH_CHECK(D % 4 == 0 && u.size(0) == B && u.size(1) == D && o.size(0) == B &&
+                  (o.size(1) == 2 * D || o.size(1) == D) && dout.size(1) == 2 * D &&
+                  gx.size(1) == D, "maf_bwd shapes");
+  const void* sp = static_cast<const at::BFloat16*>(o.data_ptr()) + (o.size(1) == 2 * D ? D : 0);
   const float* cr = nullptr;
   if (c_row && c_row->defined()) {
     TORCH_CHECK(c_row->is_cuda() && c_row->scalar_type() == at::kFloat &&
                     c_row->is_contiguous() && c_row->numel() == B, "c_row: fp32 [B]");
     cr = c_row->data_ptr<float>();
   }
-  nf_launch_maf_bwd(gu.data_ptr<float>(), ld2(gu), u.data_ptr<float>(), ld2(u), o.data_ptr(),
+  nf_launch_maf_bwd(gu.data_ptr<float>(), ld2(gu), u.data_ptr<float>(), ld2(u), sp,
                     ld2(o), B, D, (float)bound, (float)c_ldj, dout.data_ptr(), ld2(dout),
                     gx.data_ptr<float>(), ld2(gx), cur_stream(), cr);
 }
@@ -682,6 +873,9 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("gemm_tn_multi(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles, Tensor?[] tiles, Tensor?[] cmask) -> ()");
   m.def("gemm_nt_cpl(Tensor h, Tensor W, Tensor? b, Tensor(a!) st, Tensor x, Tensor(b!) y, Tensor(c!)? yb, Tensor(d!) ldjp, bool ldj_init, float scale) -> ()");
   m.def("gemm_nn_cpl(Tensor dy, Tensor W, Tensor G, Tensor s_hat, Tensor x, Tensor(a!) dst, Tensor(b!) gx, float scale, float c, Tensor? Wt=None) -> ()");
+  m.def("maf_gemm_fwd(Tensor h, Tensor? hs, Tensor W, Tensor? ws, Tensor? b, Tensor krange, Tensor(a!) s_out, Tensor x, Tensor(b!) u, Tensor(c!)? ubf, Tensor(d!) ldjp, bool ldj_init, float bound, Tensor(e!)? uq=None, Tensor? q_amax_prev=None, Tensor(f!)? q_scale=None, Tensor(g!)? q_amax_cur=None) -> ()");
+  m.def("maf_gemm_bwd(Tensor dy, Tensor Wt, Tensor krange256, Tensor G, Tensor s_raw, Tensor u, Tensor(a!) dst, Tensor(b!) gx, float bound, float c, Tensor? sa=None, Tensor? sb=None, Tensor(c!)? dstq=None, Tensor? q_amax_prev=None, Tensor(d!)? q_scale=None, Tensor(e!)? q_amax_cur=None) -> ()");
+  m.def("fp8_dgrad(Tensor dyq, Tensor sa, Tensor Wtq, Tensor sb, Tensor h, Tensor(a!) dx, Tensor krange256, Tensor(b!)? dxq=None, Tensor? q_amax_prev=None, Tensor(c!)? q_scale=None, Tensor(d!)? q_amax_cur=None) -> ()");
   m.def("fp8_quant_rows_strided(Tensor x, int layer_stride, int rows_per, int layers, int C, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("maf_fwd(Tensor x, Tensor o, float bound, Tensor(a!) u, Tensor(b!)? ubf, Tensor(c!)? uq, Tensor? amax_prev, Tensor(d!)? scale, Tensor(e!)? amax_cur, Tensor(f!) ldj, bool ldj_init) -> ()");
   m.def("iaf_gate_fwd(Tensor o, Tensor z, float gate_bias, Tensor(a!) y, Tensor(b!) ldj) -> ()");
@@ -704,6 +898,9 @@ TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
   m.impl("fp8_quant_rows", &fp8_quant_rows);
   m.impl("fp8_quant_rows_strided", &fp8_quant_rows_strided);
   m.impl("maf_fwd", &maf_fwd);
+  m.impl("maf_gemm_fwd", &maf_gemm_fwd);
+  m.impl("maf_gemm_bwd", &maf_gemm_bwd);
+  m.impl("fp8_dgrad", &fp8_dgrad);
   m.impl("maf_bwd", &maf_bwd);
   m.impl("iaf_gate_fwd", &iaf_gate_fwd);
   m.impl("iaf_gate_bwd", &iaf_gate_bwd);

@@ -69,6 +69,10 @@ struct GemmArgs {
   bf16_t* cpl_dst; long ld_cpl_dst;    // conditioner output gradient of layer l-1
   int cpl_dh, cpl_pad;
   float cpl_scale, cpl_c;
+  // cpl_mode 1: the backward of MAF layer l-1 instead (models/maf_engine.py, csrc/kernels/maf.hip)
+  //   u = (x - mu) e^-alpha, alpha = b tanh(s_raw / b)   (b = cpl_scale, s_raw = aux, x = u_{l-1})
+  //   gx = gy e^-alpha,  dst = [dmu | ds_raw] = [-gx | (cpl_c - gy u)(1 - tanh^2)]
+  int cpl_mode;
   // e4m3 operands (gemm256.hip FP8 instantiation, EPI_BF16): y = acc * f8_sa[m | 0] * f8_sb[n]
   // + bias, and optionally an e4m3 copy of the stored bf16 y with a delayed per-tensor scale
   // (q = e4m3(sat(y / s)), s = amax_prev / 448, amax_cur = max |y|) - the next fp8 GEMM's operand
@@ -98,6 +102,13 @@ struct GemmArgs {
   int cf_ldj_init;
   int cf_dh, cf_b_rows;
   float cf_scale;
+  // cf_pair: weight / bias / f8_sb row offset of tile columns 128..255 (coupling: cf_dh).
+  // cf_mode 1: the MAF transform of the same layer instead of the coupling (B, bias, f8_sb
+  // point at the s_raw rows, cf_pair = -D reaches the mu rows): columns 0..127 = s_raw,
+  // 128..255 = mu, y = u = (x - mu) e^-alpha, alpha = cf_scale tanh(s_raw / cf_scale), the
+  // ldj share is -sum alpha, C = s_raw; with f8_cq also the e4m3 copy of u (delayed scale)
+  int cf_pair;
+  int cf_mode;
   int desync;                  // persistent gemm256: s_sleep(127) rounds odd blocks wait up front
   int no_rot;                  // persistent gemm256: keep each block on one column (A/B knob)
 };
@@ -266,7 +277,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
     const bool relu = EPI == EPI_BF16 && a.relu;
     // fp8 operands: rank-1 dequantisation factor sa[m] * sb[n] (1 for bf16 operands)
     float sn[4][4], smj[NJ];
-    constexpr bool f8 = F8 && EPI == EPI_BF16;
+    constexpr bool f8 = F8 && (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -328,7 +339,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
       }
     }
     float qinv = 1.f, qamax = 0.f;
-    const bool f8out = F8 && EPI == EPI_BF16 && a.f8_cq != nullptr;
+    const bool f8out = F8 && (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK) && a.f8_cq != nullptr;
     if (f8out) {
       const float ap = *a.f8_q_amax_prev;
       const float qs = ap > 0.f ? ap / 448.f : 1.f;
@@ -406,8 +417,20 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
     // readback, from clamped addresses, so a pass waits out ONE load round trip. (Loading s_hat
     // / x per row inside the readback loop serialised 32 round trips per wave: the fused
     // coupling-backward epilogue took 52.6 us per tile, profiles/r2_g256_stamps_b65536.jsonl.)
-    constexpr int PJ = 2;             // 16-row accumulator blocks per pass
+    // 16-row accumulator blocks per pass (e4m3 fused backward: 1 - its loop leaves fewer
+    // registers for the pass's preloaded operands, 264 B/lane of scratch at 2)
+    constexpr int PJ = (F8 && EPI == EPI_CPL_BWD) ? 1 : 2;
     constexpr int PIT = PJ * 4;       // readback iterations (4 rows each) per pass
+    // e4m3 operands (EPI_CPL_BWD): acc * f8_sa[0] * f8_sb[n], and with f8_cq the e4m3 copy of
+    // dst = [dS | dT] (the next fp8 input-gradient product's operand) under a delayed scale
+    constexpr bool f8c = F8 && EPI == EPI_CPL_BWD;
+    float qinv = 1.f, qamax = 0.f;
+    if (f8c && a.f8_cq) {
+      const float ap = *a.f8_q_amax_prev;
+      const float qs = ap > 0.f ? ap / 448.f : 1.f;
+      qinv = 1.f / qs;
+      if (blockIdx.x == 0 && threadIdx.x == 0) *a.f8_q_scale_out = qs;
+    }
 #pragma unroll
     for (int hj = 0; hj < NJ / PJ; ++hj) {
       if (hj) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -437,11 +460,22 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
           }
         }
       }
+      float sc8[4] = {1.f, 1.f, 1.f, 1.f};
+      if constexpr (f8c) {
+        int n = n0 + q * 4;
+        n = n < a.N ? n : a.N - 4;
+        const float4 t = *reinterpret_cast<const float4*>(a.f8_sb + n);
+        const float s0 = a.f8_sa[0];
+        sc8[0] = s0 * t.x; sc8[1] = s0 * t.y; sc8[2] = s0 * t.z; sc8[3] = s0 * t.w;
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int it = 0; it < PIT; ++it) {
         const int row = it * 4 + (lane >> 4);
         v4f v = *(const LDS_AS v4f*)(region + row * 256 + ((q ^ (row & 7)) << 4));
+        if constexpr (f8c) {
+          v[0] *= sc8[0]; v[1] *= sc8[1]; v[2] *= sc8[2]; v[3] *= sc8[3];
+        }
         const int m = m0 + hj * 16 * PJ + row, n = n0 + q * 4 + (SPLITN && q >= 8 ? 96 : 0);
         if (m < a.M && n < a.N) {
           if constexpr (EPI == EPI_CPL_BWD) {
@@ -454,22 +488,50 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
               const float shv[4] = {bf2f(sh.x), bf2f(sh.y), bf2f(sh.z), bf2f(sh.w)};
               const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
               const float inv = 1.0f / a.cpl_scale;
-              float gx[4], dsh[4];
+              float gx[4], dsh[4], d1v[4];
+              if (a.cpl_mode) {   // MAF: dst = [dmu | ds_raw], x = u of layer l-1
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float sv = a.cpl_scale * fast_tanhf(shv[e]);
-                const float es = __expf(sv);
-                const float ds = fmaf(gy[e] * xs[e], es, a.cpl_c);
-                dsh[e] = ds * (a.cpl_scale - sv * sv * inv);
-                gx[e] = gy[e] * es;
+                for (int e = 0; e < 4; ++e) {
+                  const float t = fast_tanhf(shv[e] * inv);
+                  gx[e] = gy[e] * __expf(-a.cpl_scale * t);
+                  dsh[e] = -gx[e];
+                  d1v[e] = (a.cpl_c - gy[e] * xs[e]) * (1.f - t * t);
+                }
+              } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const float sv = a.cpl_scale * fast_tanhf(shv[e]);
+                  const float es = __expf(sv);
+                  const float ds = fmaf(gy[e] * xs[e], es, a.cpl_c);
+                  dsh[e] = ds * (a.cpl_scale - sv * sv * inv);
+                  gx[e] = gy[e] * es;
+                  d1v[e] = gy[e];
+                }
               }
               *reinterpret_cast<float4*>(a.cpl_gx + (long)m * a.ld_cpl_gx + n) =
                   make_float4(gx[0], gx[1], gx[2], gx[3]);
               ushort4 d0, d1;
               d0.x = f2bf(dsh[0]); d0.y = f2bf(dsh[1]); d0.z = f2bf(dsh[2]); d0.w = f2bf(dsh[3]);
-              d1.x = f2bf(gy[0]); d1.y = f2bf(gy[1]); d1.z = f2bf(gy[2]); d1.w = f2bf(gy[3]);
+              d1.x = f2bf(d1v[0]); d1.y = f2bf(d1v[1]); d1.z = f2bf(d1v[2]); d1.w = f2bf(d1v[3]);
               *reinterpret_cast<ushort4*>(drow + n) = d0;
               *reinterpret_cast<ushort4*>(drow + a.cpl_dh + n) = d1;
+              if (f8c && a.f8_cq) {
+                float f0[4], f1[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  qamax = fmaxf(qamax, fmaxf(fabsf(dsh[e]), fabsf(d1v[e])));
+                  f0[e] = fminf(fmaxf(dsh[e] * qinv, -448.f), 448.f);
+                  f1[e] = fminf(fmaxf(d1v[e] * qinv, -448.f), 448.f);
+                }
+                int q0 = 0, q1 = 0;
+                q0 = __builtin_amdgcn_cvt_pk_fp8_f32(f0[0], f0[1], q0, false);
+                q0 = __builtin_amdgcn_cvt_pk_fp8_f32(f0[2], f0[3], q0, true);
+                q1 = __builtin_amdgcn_cvt_pk_fp8_f32(f1[0], f1[1], q1, false);
+                q1 = __builtin_amdgcn_cvt_pk_fp8_f32(f1[2], f1[3], q1, true);
+                unsigned char* qr = a.f8_cq + (long)m * a.ld_f8_cq;
+                *reinterpret_cast<int*>(qr + n) = q0;
+                *reinterpret_cast<int*>(qr + a.cpl_dh + n) = q1;
+              }
             } else if (a.cpl_dh + n < a.cpl_pad) {   // zero the dst pad columns [2 Dh, pad)
               *reinterpret_cast<ushort4*>(drow + a.cpl_dh + n) = make_ushort4(0, 0, 0, 0);
             }
@@ -488,6 +550,11 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
           }
         }
       }
+    }
+    if (f8c && a.f8_cq) {   // one (mostly skipped) atomic per wave into the block's amax slot
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) qamax = fmaxf(qamax, __shfl_xor(qamax, off));
+      if (lane == 0) amax_slot_atomic(a.f8_q_amax_cur, qamax);
     }
   }
 }

@@ -111,11 +111,36 @@ void nf_launch_gemm256_nt_cpl(const void* h, long ldh, const void* W, long ldw, 
                               hipStream_t stream);
 // input gradient of coupling layer l's conditioner (fp32, + G) fused with coupling layer l-1's
 // backward: writes dst (bf16 [dS_hat | dT | 0]) and gx; G itself is not written
+// e4m3 operand scales of an fp8 product: sa (A, per-tensor), sb (B, per-row) and the optional
+// e4m3 copy q of the output under a delayed per-tensor scale (ops/fp8.py DelayedScale)
+struct NfF8Operands {
+  const float* sa;
+  const float* sb;
+  void* q;
+  long ldq;
+  const float* q_amax_prev;
+  float* q_scale_out;
+  float* q_amax_cur;
+};
 void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw, const float* G,
                               long ldg, int M, int N, int K, const void* s_hat, long ld_s,
                               const float* x, long ld_x, void* dst, long ld_dst, int dst_pad,
                               float* gx, long ld_gx, int Dh, float scale, float c,
-                              hipStream_t stream, int w_kmajor = 0);
+                              hipStream_t stream, int w_kmajor = 0, const int* krange = nullptr,
+                              int krange_segs = 1, int mode = 0, const NfF8Operands* f8 = nullptr);
+void nf_launch_gemm256_fp8_dgrad(const void* dyq, long lddy, const float* sa, const void* wtq,
+                                 long ldwt, const float* sb, const void* aux, long ld_aux,
+                                 int aux_bits, void* dx, long lddx, int M, int N, int K,
+                                 const int* krange, int krange_segs, void* dxq, long lddxq,
+                                 const float* q_amax_prev, float* q_scale_out, float* q_amax_cur,
+                                 hipStream_t stream);
+void nf_launch_gemm256_maf_fwd(const void* h, long ldh, int f8, const float* hs, const void* W,
+                               long ldw, const float* ws, const void* bias, const int* krange,
+                               void* s_out, long ld_s, int M, int K, int D, const float* x,
+                               long ld_x, float* u, long ld_u, void* ubf, long ld_ub, float* ldjp,
+                               long ld_ldjp, int ldj_init, float bound, void* uq, long lduq,
+                               const float* q_amax_prev, float* q_scale_out, float* q_amax_cur,
+                               hipStream_t stream);
 int nf_launch_gemm256_tn_partials(const void* dy, long lddy, const void* x, long ldx, float* C,
                                   long ldc, long slab_stride, float* dbias, int M, int N, int K,
                                   int splits, hipStream_t stream);
@@ -189,9 +214,9 @@ void nf_launch_maf_fwd(const float* x, long ldx, const void* o, long ldo, int B,
                        float* u, long ldu, void* ubf, long ldub, void* uq, long lduq,
                        const float* amax_prev, float* scale_out, float* amax_cur, float* ldj,
                        int ldj_init, hipStream_t stream);
-void nf_launch_maf_bwd(const float* gu, long ldg, const float* u, long ldu, const void* o, long ldo,
-                       int B, int D, float bound, float c_ldj, void* dout, long lddo, float* gx,
-                       long ldgx, hipStream_t stream, const float* c_row = nullptr);
+void nf_launch_maf_bwd(const float* gu, long ldg, const float* u, long ldu, const void* s_raw,
+                       long lds, int B, int D, float bound, float c_ldj, void* dout, long lddo,
+                       float* gx, long ldgx, hipStream_t stream, const float* c_row = nullptr);
 // maf.hip: gated IAF update (o = [m | s] bf16 from the MADE GEMM)
 void nf_launch_iaf_gate_fwd(const void* o, long ldo, const float* z, long ldz, int B, int D,
                             float gate_bias, float* y, long ldy, float* ldj, hipStream_t stream);

@@ -176,7 +176,9 @@ __device__ __forceinline__ void vmwait_count(int cnt) {
 // threads walk the pass's 256 / NP rows x 128 features, thread = (row of 32, 16-B chunk of 8
 // features), reading s_hat from the region of wave (wr, c/64) and t from wave (wr, 2 + c/64).
 // NP = 2 lets the persistent kernel stage through the 64 KiB its LDS-DMA stream leaves free.
-template <int NP, typename RegionFn>
+// F8: e4m3 operands, acc dequantised by f8_sa[0] * f8_sb[weight row] before the bias.
+// cf_mode 1 (MAF): see GemmArgs::cf_mode; the e4m3 copy of u (f8_cq) is quantised from fp32 u.
+template <int NP, bool F8 = false, typename RegionFn>
 __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&acc)[4][8],
                                                  int m0, int n0, int wr, int wc,
                                                  RegionFn region_of, int lane) {
@@ -187,18 +189,32 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
   const int ws = f8 >> 3, q = f8 & 7;
   const int jf = j0 + f8 * 8;                                    // first of this thread's 8 features
   const bool fok = jf < a.cf_dh;
-  float bv[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  const bool maf = a.cf_mode != 0;
+  // bias (and e4m3 dequantisation scale) of the 4 columns of fragment i: read where they are
+  // used (cached; 32 more live registers across the parking loop spilled the e4m3 build)
+  auto col_params = [&](int i, float (&bv)[4], float (&sv)[4]) {
     const int tc = wc * 64 + i * 16 + g * 4;                     // tile column (4 consecutive)
     const int f = j0 + (tc & 127);                               // feature
-    const int row = tc < 128 ? f : a.cf_dh + f;                  // weight / bias row
+    const int row = tc < 128 ? f : a.cf_pair + f;                // weight / bias row
+    bv[0] = bv[1] = bv[2] = bv[3] = 0.f;
     if (a.bias && f < a.cf_dh) {
       const ushort4 bb = *reinterpret_cast<const ushort4*>(a.bias + row);
-      bv[i][0] = bf2f(bb.x); bv[i][1] = bf2f(bb.y); bv[i][2] = bf2f(bb.z); bv[i][3] = bf2f(bb.w);
-    } else {
-      bv[i][0] = bv[i][1] = bv[i][2] = bv[i][3] = 0.f;
+      bv[0] = bf2f(bb.x); bv[1] = bf2f(bb.y); bv[2] = bf2f(bb.z); bv[3] = bf2f(bb.w);
     }
+    sv[0] = sv[1] = sv[2] = sv[3] = 1.f;
+    if constexpr (F8) {
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (f < a.cf_dh) t = *reinterpret_cast<const float4*>(a.f8_sb + row);
+      const float sa = a.f8_sa[0];
+      sv[0] = sa * t.x; sv[1] = sa * t.y; sv[2] = sa * t.z; sv[3] = sa * t.w;
+    }
+  };
+  float qinv = 1.f, qamax = 0.f;
+  if (a.f8_cq) {
+    const float ap = *a.f8_q_amax_prev;
+    const float qs = ap > 0.f ? ap / 448.f : 1.f;
+    qinv = 1.f / qs;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.f8_q_scale_out = qs;
   }
   char* region = region_of(wr * 4 + wc);
 #pragma unroll
@@ -228,10 +244,12 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
       const int row = jj * 16 + c;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const unsigned lo = (unsigned)f2bf(acc[i][j][0] + bv[i][0]) |
-                            ((unsigned)f2bf(acc[i][j][1] + bv[i][1]) << 16);
-        const unsigned hi = (unsigned)f2bf(acc[i][j][2] + bv[i][2]) |
-                            ((unsigned)f2bf(acc[i][j][3] + bv[i][3]) << 16);
+        float bv[4], sv[4];
+        col_params(i, bv, sv);
+        const unsigned lo = (unsigned)f2bf(fmaf(acc[i][j][0], sv[0], bv[0])) |
+                            ((unsigned)f2bf(fmaf(acc[i][j][1], sv[1], bv[1])) << 16);
+        const unsigned hi = (unsigned)f2bf(fmaf(acc[i][j][2], sv[2], bv[2])) |
+                            ((unsigned)f2bf(fmaf(acc[i][j][3], sv[3], bv[3])) << 16);
         const int slot = i * 4 + g;
         *(LDS_AS v2u*)(region + bf_stage_off(row, slot)) = (v2u){lo, hi};
       }
@@ -252,14 +270,42 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
           const float4 x0 = xv[it][0], x1 = xv[it][1];
           const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
           float y[8];
+          if (maf) {   // shv = s_raw, tv = mu
+            const float ib = 1.f / a.cf_scale;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const unsigned us = sh[e >> 1], ut = tt[e >> 1];
-            const float shv = __uint_as_float((e & 1) ? (us & 0xffff0000u) : (us << 16));
-            const float tv = __uint_as_float((e & 1) ? (ut & 0xffff0000u) : (ut << 16));
-            const float sv = a.cf_scale * fast_tanhf(shv);
-            y[e] = fmaf(xs[e], __expf(sv), tv);
-            part += sv;
+            for (int e = 0; e < 8; ++e) {
+              const unsigned us = sh[e >> 1], ut = tt[e >> 1];
+              const float shv = __uint_as_float((e & 1) ? (us & 0xffff0000u) : (us << 16));
+              const float tv = __uint_as_float((e & 1) ? (ut & 0xffff0000u) : (ut << 16));
+              const float al = a.cf_scale * fast_tanhf(shv * ib);
+              y[e] = (xs[e] - tv) * __expf(-al);
+              part -= al;
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const unsigned us = sh[e >> 1], ut = tt[e >> 1];
+              const float shv = __uint_as_float((e & 1) ? (us & 0xffff0000u) : (us << 16));
+              const float tv = __uint_as_float((e & 1) ? (ut & 0xffff0000u) : (ut << 16));
+              const float sv = a.cf_scale * fast_tanhf(shv);
+              y[e] = fmaf(xs[e], __expf(sv), tv);
+              part += sv;
+            }
+          }
+          if (a.f8_cq) {   // e4m3 copy of y (the next fp8 product's operand), delayed scale
+            float f[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              qamax = fmaxf(qamax, fabsf(y[e]));
+              f[e] = fminf(fmaxf(y[e] * qinv, -448.f), 448.f);
+            }
+            int q0 = 0, q1 = 0;
+            q0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], q0, false);
+            q0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], q0, true);
+            q1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], q1, false);
+            q1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], q1, true);
+            *reinterpret_cast<uint2*>(a.f8_cq + (long)m * a.ld_f8_cq + jf) =
+                make_uint2((unsigned)q0, (unsigned)q1);
           }
           float* yr = a.cf_y + (long)m * a.ld_cf_y + jf;
           *reinterpret_cast<float4*>(yr) = make_float4(y[0], y[1], y[2], y[3]);
@@ -288,6 +334,11 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
         *lp = part + lold[it];
       }
     }
+  }
+  if (a.f8_cq) {   // one (mostly skipped) atomic per wave into the block's amax slot
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) qamax = fmaxf(qamax, __shfl_xor(qamax, off));
+    if (lane == 0) amax_slot_atomic(a.f8_q_amax_cur, qamax);
   }
 }
 
@@ -386,7 +437,7 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
       stage_half<A_KMAJOR, EB>(a.A, a.lda, m0, a.M, k0, ke, true, j == H_AHI, dst, wave, lane);
     else if constexpr (EPI == EPI_CPL_FWD)
       stage_half<B_KMAJOR, EB>(a.B, a.ldb, n0, a.cf_b_rows, k0, ke, false, j == H_BHI, dst, wave,
-                               lane, a.cf_dh);
+                               lane, a.cf_pair);
     else
       stage_half<B_KMAJOR, EB, BSPLIT>(a.B, a.ldb, n0, a.N, k0, ke, false, j == H_BHI, dst, wave,
                                        lane);
@@ -511,8 +562,10 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
   }
   if constexpr (EPI == EPI_CPL_FWD) {
     barrier();  // every wave is past its last operand read
-    epi_coupling_fwd<1>(a, acc, m0, n0, wr, wc,
-                        [&](int w) { return smem + w * 16384; }, lane);
+    // e4m3 operands: two 64-row passes (half the x rows in flight) - the F8 main loop leaves
+    // fewer registers, and one pass spilled (scratch 120 B/lane)
+    epi_coupling_fwd<F8 ? 2 : 1, F8>(a, acc, m0, n0, wr, wc,
+                                     [&](int w) { return smem + w * 16384; }, lane);
 #ifdef NF_G256_STAMPS
     NF_STAMP(3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -611,7 +664,7 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
       stage_half<A_KMAJOR>(a.A, a.lda, tm0, a.M, k0, a.K, true, j == H_AHI, dst, wave, lane);
     else if constexpr (EPI == EPI_CPL_FWD)
       stage_half<B_KMAJOR>(a.B, a.ldb, tn0, a.cf_b_rows, k0, a.K, false, j == H_BHI, dst, wave,
-                           lane, a.cf_dh);
+                           lane, a.cf_pair);
     else
       stage_half<B_KMAJOR>(a.B, a.ldb, tn0, a.N, k0, a.K, false, j == H_BHI, dst, wave, lane);
   };
@@ -938,6 +991,22 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
   NF_HIP_CHECK(hipGetLastError());
 }
 
+// e4m3 operands (both k-major) on the one-tile-per-block kernel, MADE column tiles paired as in
+// launch() (VINF_GEMM_PAIR read per call: 0 off, 1 auto, 2 always)
+template <int EPI>
+void launch_f8(GemmArgs a, hipStream_t stream) {
+  a.staged = EPI == EPI_CPL_FWD ? 0 : staged_ok(a, EPI);
+  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  const char* pe = getenv("VINF_GEMM_PAIR");
+  const int pv = pe ? atoi(pe) : 1;
+  a.pair_tiles = pv && a.krange && ntn % 2 == 0 &&
+                 (pv == 2 || (long)ntm * (ntn / 2) >= device_cus_256());
+  const int nblk = a.pair_tiles ? ntm * (ntn / 2) : ntm * ntn;
+  hipLaunchKernelGGL((gemm256_kernel<true, true, EPI, 4, false, true>), dim3(nblk), dim3(NTHR), 0,
+                     stream, a);
+  NF_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace g256
 }  // namespace gemm
 }  // namespace nf
@@ -1040,7 +1109,7 @@ void nf_launch_gemm256_nt_cpl(const void* h, long ldh, const void* W, long ldw, 
   a.cf_y = y; a.ld_cf_y = ld_y;
   a.cf_yb = (nf::bf16_t*)yb; a.ld_cf_yb = ld_yb; a.cf_yb_width = yb_width;
   a.cf_ldj = ldjp; a.ld_cf_ldj = ld_ldjp; a.cf_ldj_init = ldj_init;
-  a.cf_dh = Dh; a.cf_b_rows = w_rows; a.cf_scale = scale;
+  a.cf_dh = Dh; a.cf_b_rows = w_rows; a.cf_scale = scale; a.cf_pair = Dh;
   auto al16 = [](const void* p) { return ((unsigned long)p & 15) == 0; };
   if (Dh % 8 || w_rows < 2 * Dh || ld_x % 4 || ld_y % 4 || ld_st % 8 ||
       (yb && (ld_yb % 8 || !al16(yb) || yb_width < Dh || yb_width % 8)) || !al16(x) || !al16(y) ||
@@ -1052,6 +1121,80 @@ void nf_launch_gemm256_nt_cpl(const void* h, long ldh, const void* W, long ldw, 
   g256::launch<true, true, EPI_CPL_FWD>(a, 1, stream);
 }
 
+// Second MADE product of MAF layer l with the layer's transform fused (EPI_CPL_FWD, cf_mode 1):
+// o = h (W2 * M2)^T + b2 = [mu | s_raw] is never stored; each 256-column tile holds the s_raw
+// and mu columns of 128 features (W2 rows D + j and j), so the epilogue writes u = (x - mu)
+// e^-alpha (fp32 u, bf16 ubf, optional e4m3 uq under a delayed scale), s_raw (bf16 [M][D], the
+// backward's only use of o) and ldjp[tn][m] (-sum alpha over the tile's features, one owner per
+// entry). h / W2 are bf16, or e4m3 (f8 = 1: hs = h's per-tensor scale, ws = W2's per-row scales).
+// krange: [D / 128][2] K range of each paired tile (union of its mu and s_raw mask rows).
+void nf_launch_gemm256_maf_fwd(const void* h, long ldh, int f8, const float* hs, const void* W,
+                               long ldw, const float* ws, const void* bias, const int* krange,
+                               void* s_out, long ld_s, int M, int K, int D, const float* x,
+                               long ld_x, float* u, long ld_u, void* ubf, long ld_ub, float* ldjp,
+                               long ld_ldjp, int ldj_init, float bound, void* uq, long lduq,
+                               const float* q_amax_prev, float* q_scale_out, float* q_amax_cur,
+                               hipStream_t stream) {
+  if (M <= 0) return;
+  const int EB = f8 ? 1 : 2;
+  GemmArgs a{};
+  a.A = (const nf::bf16_t*)h; a.lda = ldh;
+  a.B = (const nf::bf16_t*)((const char*)W + (long)D * ldw * EB); a.ldb = ldw;   // s_raw rows
+  a.C = s_out; a.ldc = ld_s;
+  a.bias = bias ? (const nf::bf16_t*)bias + D : nullptr;
+  const int ntn = D / 128;
+  a.M = M; a.N = ntn * 256; a.K = K; a.k_per_split = f8 ? K : ((K + 63) / 64) * 64;
+  a.krange = krange; a.krange_segs = 1;
+  a.cf_x = x; a.ld_cf_x = ld_x;
+  a.cf_y = u; a.ld_cf_y = ld_u;
+  a.cf_yb = (nf::bf16_t*)ubf; a.ld_cf_yb = ld_ub; a.cf_yb_width = D;
+  a.cf_ldj = ldjp; a.ld_cf_ldj = ld_ldjp; a.cf_ldj_init = ldj_init;
+  a.cf_dh = D; a.cf_b_rows = D; a.cf_scale = bound; a.cf_pair = -D; a.cf_mode = 1;
+  a.f8_sa = hs; a.f8_sb = f8 ? ws + D : nullptr;
+  a.f8_cq = (unsigned char*)uq; a.ld_f8_cq = lduq;
+  a.f8_q_amax_prev = q_amax_prev; a.f8_q_scale_out = q_scale_out; a.f8_q_amax_cur = q_amax_cur;
+  auto al16 = [](const void* p) { return ((unsigned long)p & 15) == 0; };
+  if (D % 128 || ld_x % 4 || ld_u % 4 || ld_s % 8 || (ubf && (ld_ub % 8 || !al16(ubf))) ||
+      !al16(x) || !al16(u) || !al16(s_out) || !krange || (f8 && (K % 128 || !hs || !ws)) ||
+      (uq && (!f8 || lduq % 8 || !q_amax_prev || !q_scale_out || !q_amax_cur)) ||
+      (!f8 && K % 32)) {
+    fprintf(stderr, "vinf: fused MAF-forward GEMM needs D %% 128 == 0, 16-B aligned rows, K "
+                    "ranges, and (fp8) K %% 128 == 0 with both scales\n");
+    abort();
+  }
+  if (f8) g256::launch_f8<EPI_CPL_FWD>(a, stream);
+  else g256::launch<true, true, EPI_CPL_FWD>(a, 1, stream);
+}
+
+// Masked input gradient dx = relu'(h) * (dyq sa)(Wtq sb)^T on e4m3 operands (dyq [M][K] with a
+// per-tensor scale, Wtq = (W*M)^T [N][K] with per-row scales), bf16 dx plus optionally its e4m3
+// copy under a delayed scale (the next fp8 input-gradient product's operand).
+void nf_launch_gemm256_fp8_dgrad(const void* dyq, long lddy, const float* sa, const void* wtq,
+                                 long ldwt, const float* sb, const void* aux, long ld_aux,
+                                 int aux_bits, void* dx, long lddx, int M, int N, int K,
+                                 const int* krange, int krange_segs, void* dxq, long lddxq,
+                                 const float* q_amax_prev, float* q_scale_out, float* q_amax_cur,
+                                 hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  GemmArgs a{};
+  a.A = (const nf::bf16_t*)dyq; a.lda = lddy;
+  a.B = (const nf::bf16_t*)wtq; a.ldb = ldwt;
+  a.C = dx; a.ldc = lddx;
+  a.aux = (const nf::bf16_t*)aux; a.ld_aux = ld_aux; a.aux_bits = aux_bits;
+  a.M = M; a.N = N; a.K = K; a.k_per_split = K;
+  a.krange = krange; a.krange_segs = krange_segs;
+  a.f8_sa = sa; a.f8_sb = sb;
+  a.f8_cq = (unsigned char*)dxq; a.ld_f8_cq = lddxq;
+  a.f8_q_amax_prev = q_amax_prev; a.f8_q_scale_out = q_scale_out; a.f8_q_amax_cur = q_amax_cur;
+  if (K % 128 || lddy % 16 || ldwt % 16 || N % 8 || !aux || !staged_ok(a, EPI_BF16_RELUMASK) ||
+      (dxq && lddxq % 8)) {
+    fprintf(stderr, "vinf: fp8 masked input gradient needs K %% 128 == 0, 16-B rows, N %% 8 == 0, "
+                    "the ReLU operand and the staged epilogue\n");
+    abort();
+  }
+  g256::launch_f8<EPI_BF16_RELUMASK>(a, stream);
+}
+
 // Conditioner input gradient of coupling layer l fused with the backward of coupling layer l-1
 // (EPI_CPL_BWD, gemm_tile.h): gy = G[M][N] + dy[M][K] W[K][N] is consumed in the epilogue and
 // never stored; dst/gx of layer l-1 are written instead.
@@ -1059,9 +1202,20 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
                               long ldg, int M, int N, int K, const void* s_hat, long ld_s,
                               const float* x, long ld_x, void* dst, long ld_dst, int dst_pad,
                               float* gx, long ld_gx, int Dh, float scale, float c,
-                              hipStream_t stream, int w_kmajor) {
+                              hipStream_t stream, int w_kmajor, const int* krange,
+                              int krange_segs, int mode, const NfF8Operands* f8) {
   if (M <= 0 || N <= 0) return;
   GemmArgs a{};
+  if (f8) {   // e4m3 dy (per-tensor scale) and Wt (per-row scales); optional e4m3 copy of dst
+    a.f8_sa = f8->sa; a.f8_sb = f8->sb;
+    a.f8_cq = (unsigned char*)f8->q; a.ld_f8_cq = f8->ldq;
+    a.f8_q_amax_prev = f8->q_amax_prev; a.f8_q_scale_out = f8->q_scale_out;
+    a.f8_q_amax_cur = f8->q_amax_cur;
+  }
+  // MAF (mode 1): the first MADE product's input gradient of layer l with the MAF backward of
+  // layer l-1 (GemmArgs::cpl_mode), under the weight's per-tile K ranges
+  a.krange = krange; a.krange_segs = krange_segs;
+  a.cpl_mode = mode;
   a.A = (const nf::bf16_t*)dy; a.lda = lddy;
   a.B = (const nf::bf16_t*)W; a.ldb = ldw;
   a.C = (void*)G; a.ldc = ldg;
@@ -1077,6 +1231,15 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
     fprintf(stderr, "vinf: fused coupling-backward GEMM needs Dh <= N, 2 Dh <= pad <= Dh + N, "
                     "4-element aligned rows and the staged epilogue\n");
     abort();
+  }
+  if (f8) {
+    if (!w_kmajor || K % 128 || lddy % 16 || ldw % 16 || (f8->q && f8->ldq % 8)) {
+      fprintf(stderr, "vinf: fp8 fused backward needs Wt, K %% 128 == 0 and 16-B rows\n");
+      abort();
+    }
+    a.k_per_split = K;
+    g256::launch_f8<EPI_CPL_BWD>(a, stream);
+    return;
   }
   if (w_kmajor) g256::launch<true, true, EPI_CPL_BWD>(a, 1, stream);   // W given as Wt [N][K]
   else g256::launch<true, false, EPI_CPL_BWD>(a, 1, stream);

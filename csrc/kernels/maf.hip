@@ -9,7 +9,8 @@
 // with a delayed per-tensor scale (amax of this call folded into amax_cur, as fp8.hip's
 // quant_tensor) - the fp8 operand of the next layer's first GEMM, produced without another
 // pass over u.
-// maf_bwd: given g_u = dL/du, returns d_o = [dL/dmu | dL/ds_raw] (bf16, the masked GEMMs'
+// maf_bwd: given g_u = dL/du (reads only s_raw of o: mu drops out of the backward),
+// returns d_o = [dL/dmu | dL/ds_raw] (bf16, the masked GEMMs'
 // gradient operand) and g_x = g_u * exp(-alpha) (fp32, the direct path; the MADE path is
 // accumulated onto it by the input-gradient GEMM). c_ldj = dL/d(sum alpha) per row (e.g. 1/B
 // for a batch-mean NLL).
@@ -93,7 +94,7 @@ __global__ void __launch_bounds__(256) maf_fwd_kernel(const float* __restrict__ 
 
 __global__ void __launch_bounds__(256) maf_bwd_kernel(const float* __restrict__ gu, long ldg,
                                                       const float* __restrict__ u, long ldu,
-                                                      const bf16_t* __restrict__ o, long ldo,
+                                                      const bf16_t* __restrict__ s_raw, long lds,
                                                       int B, int D, float bound, float c_ldj,
                                                       const float* __restrict__ c_row,
                                                       bf16_t* __restrict__ dout, long lddo,
@@ -104,7 +105,7 @@ __global__ void __launch_bounds__(256) maf_bwd_kernel(const float* __restrict__ 
   if (c_row) c_ldj = c_row[row];   // per-row dL/d(sum alpha) (autograd callers)
   const float* gr = gu + (long)row * ldg;
   const float* ur = u + (long)row * ldu;
-  const bf16_t* sr = o + (long)row * ldo + D;
+  const bf16_t* sr = s_raw + (long)row * lds;
   bf16_t* dm = dout + (long)row * lddo;
   bf16_t* ds = dm + D;
   for (int c = lane * 4; c < D; c += 256) {
@@ -260,12 +261,13 @@ void nf_launch_maf_fwd(const float* x, long ldx, const void* o, long ldo, int B,
   NF_HIP_CHECK(hipGetLastError());
 }
 
-void nf_launch_maf_bwd(const float* gu, long ldg, const float* u, long ldu, const void* o, long ldo,
-                       int B, int D, float bound, float c_ldj, void* dout, long lddo, float* gx,
-                       long ldgx, hipStream_t stream, const float* c_row) {
+// s_raw: the s half of o = [mu | s_raw] (row stride lds), or the engine's own s buffer
+void nf_launch_maf_bwd(const float* gu, long ldg, const float* u, long ldu, const void* s_raw,
+                       long lds, int B, int D, float bound, float c_ldj, void* dout, long lddo,
+                       float* gx, long ldgx, hipStream_t stream, const float* c_row) {
   if (B <= 0) return;
   hipLaunchKernelGGL(maf_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, gu, ldg, u, ldu,
-                     (const bf16_t*)o, ldo, B, D, bound, c_ldj, c_row, (bf16_t*)dout, lddo, gx,
+                     (const bf16_t*)s_raw, lds, B, D, bound, c_ldj, c_row, (bf16_t*)dout, lddo, gx,
                      ldgx);
   NF_HIP_CHECK(hipGetLastError());
 }

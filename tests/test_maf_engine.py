@@ -138,6 +138,7 @@ def test_engine_masked_dgrad_nt_matches_nn(gpu, monkeypatch):
     from vi_normflows_amd.models.maf_engine import MAFEngine, MAFEngineConfig
 
     cfg = MAFEngineConfig(dim=256, hidden=512, n_layers=3, precision="bf16")
+    monkeypatch.setenv("VINF_MAF_FUSE", "0")      # both on the separate MAF kernels
     a = MAFEngine(cfg, batch=512, device=gpu, seed=4)
     monkeypatch.setenv("VINF_DGRAD_NT", "0")
     b = MAFEngine(cfg, batch=512, device=gpu, seed=4)
@@ -149,3 +150,94 @@ def test_engine_masked_dgrad_nt_matches_nn(gpu, monkeypatch):
     ga, gb = a.params.grad, b.params.grad
     assert torch.isfinite(ga).all()
     assert ((ga - gb).norm() / gb.norm()).item() < 1e-5
+
+
+def _fused_vs_separate(gpu, monkeypatch, cfg, batch, seed=4):
+    from vi_normflows_amd.models.maf_engine import MAFEngine
+
+    a = MAFEngine(cfg, batch=batch, device=gpu, seed=seed)
+    monkeypatch.setenv("VINF_MAF_FUSE", "0")
+    b = MAFEngine(cfg, batch=batch, device=gpu, seed=seed)
+    assert a.fuse and not b.fuse
+    x = torch.randn(batch, cfg.dim, generator=torch.Generator().manual_seed(seed + 1)).to(gpu)
+    for e in (a, b):
+        e.data_override = x
+        e._update_schedule()
+        e.forward()
+        e.backward()
+    torch.cuda.synchronize()
+    L = cfg.n_layers
+    rel = lambda p, q: ((p - q).norm() / q.norm()).item()
+    return a, b, rel, L
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["bf16", "fp8"])
+def test_engine_fused_maf_transforms_match_separate_kernels(gpu, monkeypatch, precision):
+    """The MAF transform in the second MADE product's epilogue and the MAF backward in the first
+    product's input-gradient epilogue (VINF_MAF_FUSE=1) == the separate maf_fwd / maf_bwd
+    kernels: u_L, log-det, loss and every gradient (the epilogues see the same bf16 [mu | s_raw]
+    the separate kernels read back; the difference is fast_tanhf vs tanhf, ~1e-6 relative)."""
+    cfg = MAFEngineConfig(dim=256, hidden=512, n_layers=3, precision=precision, init_out_std=0.3)
+    a, b, rel, L = _fused_vs_separate(gpu, monkeypatch, cfg, 512)
+    tol = 1e-3 if precision == "bf16" else 2e-2     # fp8: e4m3 rounding flips at ties
+    assert rel(a.X[L], b.X[L]) < tol
+    assert rel(a.ldj, b.ldj) < tol
+    assert abs(a.loss.item() - b.loss.item()) < tol * abs(b.loss.item())
+    assert rel(a.s_raw(L - 1).float(), b.s_raw(L - 1).float()) < tol
+    assert torch.isfinite(a.params.grad).all()
+    assert rel(a.params.grad, b.params.grad) < 5 * tol
+    for l in range(cfg.n_layers):
+        mk = a._mask(l)
+        assert (a.params.g(f"l{l}.W1")[mk["M1"] == 0] == 0).all()
+        assert (a.params.g(f"l{l}.W2")[mk["M2"] == 0] == 0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["bf16", "fp8"])
+def test_engine_fused_maf_paired_tiles_headline_width(gpu, monkeypatch, precision):
+    """Config-5 width (D = H = 1024) at a batch whose launches pair the column tiles (every
+    block takes a long and a short K range): fused == separate kernels."""
+    cfg = MAFEngineConfig(dim=1024, hidden=1024, n_layers=2, precision=precision,
+                          init_out_std=0.3)
+    a, b, rel, L = _fused_vs_separate(gpu, monkeypatch, cfg, 16384)
+    tol = 1e-3 if precision == "bf16" else 2e-2
+    assert rel(a.X[L], b.X[L]) < tol
+    assert abs(a.loss.item() - b.loss.item()) < tol * abs(b.loss.item())
+    assert rel(a.params.grad, b.params.grad) < 5 * tol
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim,hidden,batch", [(256, 512, 1024), (1024, 1024, 16384)],
+                         ids=["small", "config5_width"])
+def test_engine_fp8_input_gradients(gpu, monkeypatch, dim, hidden, batch):
+    """fp8 engine with e4m3 input-gradient products (after a bf16 bootstrap step seeds the
+    gradients' delayed scales) vs the same engine with bf16 input gradients, same weights and
+    data: the loss is the same forward, the gradient differs by the e4m3 rounding of dO / dH /
+    (W*M)^T only (3 mantissa bits: ~3 % per product, averaged over the reduction)."""
+    cfg = MAFEngineConfig(dim=dim, hidden=hidden, n_layers=4, precision="fp8", init_out_std=0.3)
+    a = MAFEngine(cfg, batch=batch, device=gpu, seed=4)
+    monkeypatch.setenv("VINF_FP8_DGRAD", "0")
+    b = MAFEngine(cfg, batch=batch, device=gpu, seed=4)
+    assert a.fp8_bwd and not b.fp8_bwd
+    x = torch.randn(batch, dim, generator=torch.Generator().manual_seed(9)).to(gpu)
+    for step in range(2):
+        for e in (a, b):
+            e.data_override = x
+            e._update_schedule()
+            e.forward()
+            e.backward()
+        torch.cuda.synchronize()
+        if step == 0:
+            assert a._gscale_ready
+            assert ((a.params.grad - b.params.grad).norm() / b.params.grad.norm()).item() < 1e-5
+    assert abs(a.loss.item() - b.loss.item()) < 1e-5 * abs(b.loss.item())
+    ga, gb = a.params.grad, b.params.grad
+    assert torch.isfinite(ga).all()
+    rel = ((ga - gb).norm() / gb.norm()).item()
+    print(f"fp8 input-gradient products: relative gradient difference {rel:.4f}")
+    assert rel < 0.1
+    for l in range(cfg.n_layers):
+        mk = a._mask(l)
+        assert (a.params.g(f"l{l}.W1")[mk["M1"] == 0] == 0).all()
+        assert (a.params.g(f"l{l}.W2")[mk["M2"] == 0] == 0).all()

@@ -105,7 +105,7 @@ class MAFEngine:
 
     # ------------------------------------------------------------------ setup
     def _build_masks(self):
-        from ..ops.masked import MaskPlan
+        from ..ops.masked import MaskPlan, tile_ranges
 
         cfg, dev = self.cfg, self.device
         D, H = cfg.dim, cfg.hidden
@@ -119,6 +119,13 @@ class MAFEngine:
                      "M2u": m2.to(torch.uint8).contiguous()}
             if dev.type == "cuda":
                 entry["P1"], entry["P2"] = MaskPlan(m1), MaskPlan(m2)
+                if D % 128 == 0:
+                    # K ranges of the fused forward's paired tiles: tile t = the s_raw rows
+                    # D + 128 t .. and the mu rows 128 t .. of the same 128 features
+                    m2c = m2.cpu()
+                    pair = torch.cat([torch.cat([m2c[D + t:D + t + 128], m2c[t:t + 128]])
+                                      for t in range(0, D, 128)])
+                    entry["P2pair"] = tile_ranges(pair, 256).to(dev).contiguous()
             self.masks.append(entry)
 
     def _mask(self, l):
@@ -139,7 +146,14 @@ class MAFEngine:
         self.X = torch.empty(L + 1, B, D, dtype=f32, device=dev)          # x_0 .. u_L
         self.Xbf = torch.empty(L + 1, B, D, dtype=self.cdt, device=dev)
         self.Hbf = torch.empty(L, B, H, dtype=self.cdt, device=dev)        # relu(h) per layer
-        self.O = torch.empty(L, B, 2 * D, dtype=self.cdt, device=dev)      # [mu | s_raw]
+        import os
+
+        # fused MAF transforms (GPU): the forward's second MADE product writes u / s_raw / the
+        # log-det shares from its epilogue (no [mu | s_raw] tensor, no maf_fwd pass) and each
+        # layer's first input-gradient product finishes the MAF backward of the layer below (no
+        # maf_bwd pass except at the top); VINF_MAF_FUSE=0 keeps the separate kernels
+        fuse_env = os.environ.get("VINF_MAF_FUSE", "1") != "0"
+
         self.ldj = torch.empty(B, dtype=f32, device=dev)
         self.nll_row = torch.empty(B, dtype=f32, device=dev)
         self.gU = torch.empty(B, D, dtype=f32, device=dev)
@@ -151,12 +165,17 @@ class MAFEngine:
         # weight gradients of several layers run as one launch of whole 256x256 tiles with the
         # full batch as K, entirely-masked tiles left out (ops.gemm.WgradPlan) - 13 GB at
         # B = 32768, nothing next to 288 GB of HBM
-        import os
-
         self.wgrad_defer = dev.type == "cuda" and os.environ.get("VINF_WGRAD_DEFER", "1") != "0"
         self._wplan = None
         # masked input gradients as NT products against a per-step (W*M)^T copy (ops.layout)
         self.wt_dgrad = self.wgrad_defer and os.environ.get("VINF_DGRAD_NT", "1") != "0"
+        # (the fused backward is an NT product against (W*M)^T)
+        self.fuse = dev.type == "cuda" and D % 128 == 0 and fuse_env and self.wt_dgrad
+        if self.fuse:
+            self.S = torch.empty(L, B, D, dtype=self.cdt, device=dev)      # s_raw per layer
+            self.ldjp = torch.empty(D // 128, B, dtype=f32, device=dev)    # per-tile ldj shares
+        else:
+            self.O = torch.empty(L, B, 2 * D, dtype=self.cdt, device=dev)  # [mu | s_raw]
         self.WT = None
         self._wt_plan = None
         if self.wgrad_defer:
@@ -176,12 +195,28 @@ class MAFEngine:
             # every delayed-scale state of a step in one pool, rolled by one launch per step
             from ..ops.fp8 import AMAX_SLOTS
 
-            self.amax_pool = torch.zeros(2 * L, 1 + AMAX_SLOTS, dtype=f32, device=dev)
+            # fp8 input-gradient products too (fused engine): e4m3 copies of each layer's
+            # [dmu | ds_raw] and hidden gradient come from the producing epilogues under delayed
+            # scales, against e4m3 (W*M)^T with per-row scales; VINF_FP8_DGRAD=0 keeps bf16
+            self.fp8_bwd = self.fuse and os.environ.get("VINF_FP8_DGRAD", "1") != "0"
+            self.amax_pool = torch.zeros(4 * L, 1 + AMAX_SLOTS, dtype=f32, device=dev)
             self.sx = [DelayedScale(dev, self.amax_pool[l]) for l in range(L)]      # input of l
             self.sh = [DelayedScale(dev, self.amax_pool[L + l]) for l in range(L)]  # hidden of l
-            for st in self.sx + self.sh:
+            self.sdo = [DelayedScale(dev, self.amax_pool[2 * L + l]) for l in range(L)]  # dO_l
+            self.sdh = [DelayedScale(dev, self.amax_pool[3 * L + l]) for l in range(L)]  # dH_l
+            for st in self.sx + self.sh + self.sdo + self.sdh:
                 st.external = True
             self._wq_fresh = False
+            self._gscale_ready = False
+            if self.fp8_bwd:
+                self.dOq = torch.empty(B, 2 * D, dtype=e4, device=dev)
+                self.dHq = torch.empty(B, H, dtype=e4, device=dev)
+                self.W1Tq = torch.empty(L * D, H, dtype=e4, device=dev)
+                self.W2Tq = torch.empty(L * H, 2 * D, dtype=e4, device=dev)
+                self.sW1T = torch.empty(L * D, dtype=f32, device=dev)
+                self.sW2T = torch.empty(L * H, dtype=f32, device=dev)
+        else:
+            self.fp8_bwd = False
 
     def init_params(self, seed: int = 0):
         cfg = self.cfg
@@ -259,6 +294,8 @@ class MAFEngine:
             torch.amax(self.amax_pool[:, 1:], 1, out=self.amax_pool[:, 0])
             self.amax_pool[:, 1:].zero_()
             _, sxs = self.sx[0].quantize(self.X[0], out=self.Xq)
+        if self.fuse:
+            return self._forward_fused(sxs if self.fp8 else None)
         for l in range(L):
             mk = self._mask(l)
             b1, b2 = P.c(f"l{l}.b1"), P.c(f"l{l}.b2")
@@ -288,12 +325,56 @@ class MAFEngine:
                           scale_state=nxt, ldj_init=(l == 0))
             if nxt is not None:
                 sxs = nxt.scale
-        # NLL per row and dL/du_L
+        self._nll()
+
+    def _nll(self):
+        """NLL per row, its batch mean and dL/du_L."""
+        D, L = self.cfg.dim, self.cfg.n_layers
         uL = self.X[L]
         torch.sum(uL * uL, 1, out=self.nll_row)
         self.nll_row.mul_(0.5).add_(0.5 * D * LOG2PI).sub_(self.ldj)
         torch.mean(self.nll_row, 0, out=self.loss)
         torch.mul(uL, 1.0 / self.B, out=self.gU)
+
+    def _forward_fused(self, sxs):
+        """Per layer: first MADE product (bias + ReLU, bf16 or e4m3 h), then the second product
+        with the MAF transform in its epilogue (ops native maf_gemm_fwd): u, its bf16 / e4m3
+        copies, s_raw and the per-tile log-det shares; ldj = the shares' sum at the end."""
+        from ..ops._ext import native
+
+        cfg, P = self.cfg, self.params
+        D, H, L = cfg.dim, cfg.hidden, cfg.n_layers
+        for l in range(L):
+            mk = self._mask(l)
+            b1, b2 = P.c(f"l{l}.b1"), P.c(f"l{l}.b2")
+            last = l == L - 1
+            if self.fp8:
+                from ..ops.fp8 import gemm_fp8
+
+                _, sh = gemm_fp8(self.Xq, sxs, self.W1q[l * H:(l + 1) * H],
+                                 self.s1[l * H:(l + 1) * H], b1, relu=True, krange=mk["P1"].fwd,
+                                 out=self.Hbf[l], out_q=self.Hq, out_scale=self.sh[l],
+                                 krange256=mk["P1"].fwd256)
+                nxt = None if last else self.sx[l + 1]
+                qargs = (self.Xq, nxt.amax[0:1], nxt.scale, nxt.cur) if nxt is not None else ()
+                native().maf_gemm_fwd(self.Hq, sh, self.W2q[l * 2 * D:(l + 1) * 2 * D],
+                                      self.s2[l * 2 * D:(l + 1) * 2 * D], b2, mk["P2pair"],
+                                      self.S[l], self.X[l], self.X[l + 1], self.Xbf[l + 1],
+                                      self.ldjp, l == 0, float(cfg.alpha_bound), *qargs)
+                if nxt is not None:
+                    sxs = nxt.scale
+            else:
+                native().masked_gemm_nt(self.Xbf[l], P.c(f"l{l}.W1"), b1, self.Hbf[l], 1,
+                                        mk["P1"].fwd, mk["P1"].fwd256)
+                native().maf_gemm_fwd(self.Hbf[l], None, P.c(f"l{l}.W2"), None, b2, mk["P2pair"],
+                                      self.S[l], self.X[l], self.X[l + 1], self.Xbf[l + 1],
+                                      self.ldjp, l == 0, float(cfg.alpha_bound))
+        torch.sum(self.ldjp, 0, out=self.ldj)
+        self._nll()
+
+    def s_raw(self, l: int) -> torch.Tensor:
+        """s_raw of layer l (the fused engine keeps only this half of [mu | s_raw])."""
+        return self.S[l] if self.fuse else self.O[l][:, self.cfg.dim:]
 
     # ------------------------------------------------------------------ backward
     def _wgrad_plan(self):
@@ -324,6 +405,7 @@ class MAFEngine:
             Ws = [[P.c(f"l{l}.W1"), P.c(f"l{l}.W2")] for l in range(self.cfg.n_layers)]
             buf = torch.empty(sum(W.numel() for row in Ws for W in row), dtype=torch.bfloat16,
                               device=self.device)
+            self._wt_buf = buf
             self.WT, pairs, off = [], [], 0
             for row in Ws:
                 out = []
@@ -350,6 +432,13 @@ class MAFEngine:
         sched = gemm.WgradScheduler(plan, plan.unit_ends, self._wchunk, self.unit_ready_hook)
         gu, gx = self.gU, self.gX
         WT = self._weights_t() if self.wt_dgrad else None
+        if self.fp8_bwd and self._gscale_ready:
+            return self._backward_fused_fp8(plan, sched, WT)
+        if self.fuse:
+            self._backward_fused(plan, sched, WT)
+            if self.fp8_bwd:
+                self._bootstrap_grad_scales()
+            return
         for k, l in enumerate(range(L - 1, -1, -1)):
             mk = self._mask(l)
             dO, dH = self.dOL[l], self.dHL[l]
@@ -361,6 +450,83 @@ class MAFEngine:
                                     mk["P1"].bwd256, None if WT is None else WT[l][0])
             sched.ready(plan.unit_ends[k][1], final=(l == 0))
             gu, gx = gx, gu
+
+    def _backward_fused(self, plan, sched, WT):
+        """maf_bwd of the top layer only; below it each layer's W1 input-gradient product
+        finishes the next layer down's MAF backward in its epilogue (native maf_gemm_bwd). The
+        data gradient dL/dx_0 is not needed, so layer 0 runs no W1 input-gradient product."""
+        from ..ops._ext import native
+
+        cfg, P = self.cfg, self.params
+        L = cfg.n_layers
+        gu, gx = self.gU, self.gX
+        fused.maf_bwd(gu, self.X[L], self.S[L - 1], self.dOL[L - 1], gx, bound=cfg.alpha_bound,
+                      c_ldj=1.0 / self.B)
+        for k, l in enumerate(range(L - 1, -1, -1)):
+            mk = self._mask(l)
+            native().masked_gemm_nn(self.dOL[l], P.c(f"l{l}.W2"), self.Hbf[l], self.dHL[l],
+                                    mk["P2"].bwd, False, mk["P2"].bwd256, WT[l][1])
+            if l > 0:
+                # gy_{l-1} = gx (direct path of layer l) + dH_l (W1 M1): layer l-1's backward
+                native().maf_gemm_bwd(self.dHL[l], WT[l][0], mk["P1"].bwd256, gx, self.S[l - 1],
+                                      self.X[l], self.dOL[l - 1], gu, float(cfg.alpha_bound),
+                                      1.0 / self.B)
+                gu, gx = gx, gu
+            sched.ready(plan.unit_ends[k][1], final=(l == 0))
+
+    def _bootstrap_grad_scales(self):
+        """First step of the fp8 backward: it ran in bf16; the exact amax of every kept [dmu |
+        ds_raw] / hidden gradient seeds the delayed scales the following fp8 steps use (a
+        scale of 1 would flush gradients of ~1/B to zero in e4m3)."""
+        L = self.cfg.n_layers
+        with torch.no_grad():
+            for l in range(L):
+                for buf, row in ((self.dOL[l], 2 * L + l), (self.dHL[l], 3 * L + l)):
+                    mn, mx = torch.aminmax(buf)
+                    self.amax_pool[row, 1] = torch.maximum(mx, -mn).float()
+        self._gscale_ready = True
+
+    def _quantize_weights_t(self):
+        """e4m3 (W*M)^T per layer with per-row scales, from the bf16 transposes (two strided
+        launches: every W1^T [D, H], every W2^T [H, 2D])."""
+        from ..ops._ext import native
+
+        D, H, L = self.cfg.dim, self.cfg.hidden, self.cfg.n_layers
+        buf = self._wt_buf
+        stride = D * H + H * 2 * D
+        native().fp8_quant_rows_strided(buf, stride, D, L, H, self.W1Tq, self.sW1T)
+        native().fp8_quant_rows_strided(buf[D * H:], stride, H, L, 2 * D, self.W2Tq, self.sW2T)
+
+    def _backward_fused_fp8(self, plan, sched, WT):
+        """The fused backward with both input-gradient products on e4m3 operands: dO_l (from
+        maf_bwd at the top, else from the layer above's fused epilogue) x (W2 M2)^T -> dH_l
+        (bf16 for the weight gradient + e4m3), dH_l x (W1 M1)^T -> layer l-1's MAF backward."""
+        from ..ops._ext import native
+
+        cfg = self.cfg
+        D, H, L = cfg.dim, cfg.hidden, cfg.n_layers
+        self._quantize_weights_t()
+        gu, gx = self.gU, self.gX
+        fused.maf_bwd(gu, self.X[L], self.S[L - 1], self.dOL[L - 1], gx, bound=cfg.alpha_bound,
+                      c_ldj=1.0 / self.B)
+        st = self.sdo[L - 1]
+        native().fp8_quant_tensor(self.dOL[L - 1], self.dOq, st.amax[0:1], st.scale, st.cur)
+        bound, c = float(cfg.alpha_bound), 1.0 / self.B
+        for k, l in enumerate(range(L - 1, -1, -1)):
+            mk = self._mask(l)
+            sdo, sdh = self.sdo[l], self.sdh[l]
+            qh = (self.dHq, sdh.amax[0:1], sdh.scale, sdh.cur) if l > 0 else ()
+            native().fp8_dgrad(self.dOq, sdo.scale, self.W2Tq[l * H:(l + 1) * H],
+                               self.sW2T[l * H:(l + 1) * H], self.Hbf[l], self.dHL[l],
+                               mk["P2"].bwd256, *qh)
+            if l > 0:
+                nx = self.sdo[l - 1]
+                native().maf_gemm_bwd(self.dHq, self.W1Tq[l * D:(l + 1) * D], mk["P1"].bwd256, gx,
+                                      self.S[l - 1], self.X[l], self.dOL[l - 1], gu, bound, c,
+                                      sdh.scale, self.sW1T[l * D:(l + 1) * D], self.dOq,
+                                      nx.amax[0:1], nx.scale, nx.cur)
+                gu, gx = gx, gu
+            sched.ready(plan.unit_ends[k][1], final=(l == 0))
 
     def backward(self):
         if self.wgrad_defer and self.cdt == torch.bfloat16:
