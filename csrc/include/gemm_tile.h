@@ -51,6 +51,8 @@ struct GemmArgs {
   const int* krange;           // [ntn][2] per output N-tile K range [lo, hi) (multiples of 64), or null
   int krange_segs;             // 2: krange is [ntn][4], two ranges per tile (gemm256 only)
   int pair_tiles;              // gemm256: each block computes two column tiles (set by launchers)
+  int pair_alt;                // gemm256 paired tiles: odd blocks take the short tile first, so
+                               // the CUs' epilogues (HBM-bound) do not all run at once
   const unsigned char* skip;   // [ntm*ntn] 1 -> tile entirely masked: write zeros, no MFMA, or null
   const unsigned char* cmask;  // [M][N] 0/1 applied to fp32 outputs (masked weight gradients), or null
   int staged;                  // 1 -> LDS-staged epilogue (set by the launchers, see staged_ok)

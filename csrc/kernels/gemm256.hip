@@ -858,6 +858,11 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_kernel(GemmArgs a) {
     if (rank == p) tn_a = c;
     if (rank == ntn - 1 - p) tn_b = c;
   }
+  if (a.pair_alt && (b & 1)) {   // short tile first on odd blocks
+    const int t = tn_a;
+    tn_a = tn_b;
+    tn_b = t;
+  }
   gemm256_body<A_KMAJOR, B_KMAJOR, EPI, D, DB, F8>(a, tm * ntn + tn_a, 0, smem);
   __syncthreads();  // the second tile's LDS-DMA reuses what the first tile's epilogue staged
   gemm256_body<A_KMAJOR, B_KMAJOR, EPI, D, DB, F8>(a, tm * ntn + tn_b, 0, smem);
@@ -942,6 +947,16 @@ int device_cus_256() {
   return n;
 }
 
+// VINF_PAIR_ALT (read per launch; default 1): odd blocks of a paired launch run their short tile
+// first, so half the CUs are in a main loop while the other half store their epilogue. The
+// fused MAF epilogues move ~420 KB per tile and run at the chip's HBM rate when every CU stores
+// at once; alternating took fwd2 172 -> 164 us (bf16) / 191 -> 178 (e4m3) and the fused
+// backward 183 -> 166 / 178 -> 167 per layer (profiles/r2_maf_kernels.json)
+inline int pair_alt_env() {
+  const char* e = getenv("VINF_PAIR_ALT");
+  return e ? atoi(e) : 1;
+}
+
 template <bool AK, bool BK_, int EPI, bool DB = false>
 void launch(GemmArgs a, int splits, hipStream_t stream) {
   a.staged = staged_ok(a, EPI);
@@ -958,6 +973,7 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
   }();
   a.pair_tiles = pair_env && a.krange && splits == 1 && ntn % 2 == 0 &&
                  (pair_env == 2 || (long)ntm * (ntn / 2) >= device_cus_256());
+  a.pair_alt = pair_alt_env();
   // plain products run persistent (one continuous LDS-DMA stream per block, see
   // gemm256_persistent_body); VINF_G256_PERSIST=0 restores one tile per block
   const int persist_env = g_persist;
@@ -1001,6 +1017,7 @@ void launch_f8(GemmArgs a, hipStream_t stream) {
   const int pv = pe ? atoi(pe) : 1;
   a.pair_tiles = pv && a.krange && ntn % 2 == 0 &&
                  (pv == 2 || (long)ntm * (ntn / 2) >= device_cus_256());
+  a.pair_alt = pair_alt_env();
   const int nblk = a.pair_tiles ? ntm * (ntn / 2) : ntm * ntn;
   hipLaunchKernelGGL((gemm256_kernel<true, true, EPI, 4, false, true>), dim3(nblk), dim3(NTHR), 0,
                      stream, a);
@@ -1294,6 +1311,7 @@ void nf_launch_gemm256_fp8_nt(const void* xq, long ldx, const float* sx, int sx_
   const int pv = pe ? atoi(pe) : 1;   // 0 off, 1 auto, 2 always (tests)
   a.pair_tiles = pv && krange && ntn % 2 == 0 &&
                  (pv == 2 || (long)ntm * (ntn / 2) >= g256::device_cus_256());
+  a.pair_alt = g256::pair_alt_env();
   const int nblk = a.pair_tiles ? ntm * (ntn / 2) : ntm * ntn;
   if (g256::g_depth == 6)
     hipLaunchKernelGGL((g256::gemm256_kernel<true, true, EPI_BF16, 6, false, true>),
