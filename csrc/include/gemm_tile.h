@@ -113,6 +113,7 @@ struct GemmArgs {
   int cf_mode;
   int desync;                  // persistent gemm256: s_sleep(127) rounds odd blocks wait up front
   int no_rot;                  // persistent gemm256: keep each block on one column (A/B knob)
+  int no_edge;                 // persistent EPI_CPL_FWD: run edge tiles as full tiles (A/B knob)
 };
 
 // LDS-staged epilogue switch (VINF_GEMM_STAGED_EPI=0 restores the fragment-layout stores) and

@@ -91,6 +91,15 @@ __device__ __forceinline__ int half_row(bool is_a, bool hi, int lr) {
     }                                                                                             \
   } while (0)
 
+// fragment column i = 0 of a quadrant only (bf16): the coupling forward's edge tile
+#define NF_G256_QUAD_I0(IO, JO, FB)                                                                \
+  do {                                                                                            \
+    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) if (ks == 0 || two)                          \
+      _Pragma("unroll") for (int j = 0; j < 4; ++j)                                               \
+        acc[IO][JO + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[0][ks], fa[j][ks],           \
+                                                                  acc[IO][JO + j], 0, 0, 0);      \
+  } while (0)
+
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef int v4i __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ v8i cat16(v8s lo, v8s hi) {
@@ -190,8 +199,14 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
   const int jf = j0 + f8 * 8;                                    // first of this thread's 8 features
   const bool fok = jf < a.cf_dh;
   const bool maf = a.cf_mode != 0;
-  // bias (and e4m3 dequantisation scale) of the 4 columns of fragment i: read where they are
-  // used (cached; 32 more live registers across the parking loop spilled the e4m3 build)
+  // bias (and e4m3 dequantisation scale) of the 4 columns of fragment i. AT_USE: read where
+  // they are used (cached; 32 more live registers across the parking loop spilled the e4m3 and
+  // one-pass builds); otherwise (the persistent bf16 form) read once up front.
+#ifdef NF_CPLF_AT_USE
+  constexpr bool AT_USE = true;
+#else
+  constexpr bool AT_USE = F8 || NP == 1;
+#endif
   auto col_params = [&](int i, float (&bv)[4], float (&sv)[4]) {
     const int tc = wc * 64 + i * 16 + g * 4;                     // tile column (4 consecutive)
     const int f = j0 + (tc & 127);                               // feature
@@ -209,6 +224,14 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
       sv[0] = sa * t.x; sv[1] = sa * t.y; sv[2] = sa * t.z; sv[3] = sa * t.w;
     }
   };
+  float bpre[4][4];
+  if constexpr (!AT_USE) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float sv[4];
+      col_params(i, bpre[i], sv);
+    }
+  }
   float qinv = 1.f, qamax = 0.f;
   if (a.f8_cq) {
     const float ap = *a.f8_q_amax_prev;
@@ -245,7 +268,15 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float bv[4], sv[4];
-        col_params(i, bv, sv);
+        if constexpr (AT_USE) {
+          col_params(i, bv, sv);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            bv[r] = bpre[i][r];
+            sv[r] = 1.f;
+          }
+        }
         const unsigned lo = (unsigned)f2bf(fmaf(acc[i][j][0], sv[0], bv[0])) |
                             ((unsigned)f2bf(fmaf(acc[i][j][1], sv[1], bv[1])) << 16);
         const unsigned hi = (unsigned)f2bf(fmaf(acc[i][j][2], sv[2], bv[2])) |
@@ -686,9 +717,16 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
   //   MODE 2: t = nkt - 1, no issues, vmcnt 2 / 0 / 0 / 0
   // FULL: the K-tile has both 32-deep k-steps (false only on a tile's last K-tile when
   //       K % 64 == 32, then `two` is the runtime answer).
-  auto ktile = [&](int T, int t, int m0, int n0, bool two_rt, auto mode_c, auto full_c) {
+  // EDGE (EPI_CPL_FWD tiles holding <= 16 features, e.g. the last 8 of Dh = 392): only the
+  // s / t columns 0..15 and 128..143 are real, i.e. fragment 0 of the B-lo half of waves wc = 0
+  // and 2; every other MFMA (and the B-hi fragment reads) of the tile is skipped. The DMA
+  // stream, barriers and waits are the full tile's, so the ring schedule is unchanged.
+  auto ktile = [&](int T, int t, int m0, int n0, bool two_rt, auto mode_c, auto full_c,
+                   auto edge_c) {
     constexpr int MODE = decltype(mode_c)::value;
+    constexpr bool E = decltype(edge_c)::value;
     const bool two = decltype(full_c)::value || two_rt;
+    const bool e_act = (wc & 1) == 0;
     constexpr bool F8 = false;
     auto slot = [&](int j) { return smem + ((4 * T + j) & (NSLOT - 1)) * HALF_BYTES; };
     auto issue_wait = [&](auto q_c) {   // q = 1..4
@@ -717,19 +755,25 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
-    NF_G256_QUAD(0, 0, fbl);
+    if constexpr (E) {
+      if (e_act) NF_G256_QUAD_I0(0, 0, fbl);
+    } else {
+      NF_G256_QUAD(0, 0, fbl);
+    }
     __builtin_amdgcn_s_setprio(0);
     barrier();
+    if constexpr (!E) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        fbh[i][ks] = read_frag<B_KMAJOR>(slot(H_BHI), wc * 32 + i * 16, ks, lane);
+        for (int ks = 0; ks < 2; ++ks)
+          fbh[i][ks] = read_frag<B_KMAJOR>(slot(H_BHI), wc * 32 + i * 16, ks, lane);
+    }
     issue_wait(std::integral_constant<int, 2>{});
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
-    NF_G256_QUAD(2, 0, fbh);
+    if constexpr (!E) NF_G256_QUAD(2, 0, fbh);
     __builtin_amdgcn_s_setprio(0);
     barrier();
 #pragma unroll
@@ -741,13 +785,17 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
-    NF_G256_QUAD(2, 4, fbh);
+    if constexpr (!E) NF_G256_QUAD(2, 4, fbh);
     __builtin_amdgcn_s_setprio(0);
     barrier();
     issue_wait(std::integral_constant<int, 4>{});
     barrier();
     __builtin_amdgcn_s_setprio(1);
-    NF_G256_QUAD(0, 4, fbl);
+    if constexpr (E) {
+      if (e_act) NF_G256_QUAD_I0(0, 4, fbl);
+    } else {
+      NF_G256_QUAD(0, 4, fbl);
+    }
     __builtin_amdgcn_s_setprio(0);
     barrier();
   };
@@ -767,12 +815,21 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
   for (int s = 0; s < ns; ++s) {
     const bool has_next = s + 1 < ns;
     if (wr == 1) barrier();
-    for (int t = 0; t < nkt - 2; ++t, ++T)
-      ktile(T, t, m0, n0, true, std::integral_constant<int, 0>{}, std::true_type{});
-    ktile(T, nkt - 2, m0, n0, true, std::integral_constant<int, 1>{}, std::true_type{});
-    ++T;
-    ktile(T, nkt - 1, m0, n0, !tail_half, std::integral_constant<int, 2>{}, std::false_type{});
-    ++T;
+    auto tile_loop = [&](auto edge_c) {
+      for (int t = 0; t < nkt - 2; ++t, ++T)
+        ktile(T, t, m0, n0, true, std::integral_constant<int, 0>{}, std::true_type{}, edge_c);
+      ktile(T, nkt - 2, m0, n0, true, std::integral_constant<int, 1>{}, std::true_type{}, edge_c);
+      ++T;
+      ktile(T, nkt - 1, m0, n0, !tail_half, std::integral_constant<int, 2>{}, std::false_type{},
+            edge_c);
+      ++T;
+    };
+    if constexpr (EPI == EPI_CPL_FWD) {
+      if (!a.no_edge && a.cf_dh - (n0 >> 1) <= 16) tile_loop(std::true_type{});
+      else tile_loop(std::false_type{});
+    } else {
+      tile_loop(std::false_type{});
+    }
     // the next tile's K-tile 0 and K-tile 1's A-lo / B-lo: stream halves 4T .. 4T+5, i.e. the
     // slots of K-tiles T-2 (all four, read long ago) and T-1's A-lo / B-lo (read in its phase
     // r1) - not the free pair the epilogue stages through
@@ -991,6 +1048,11 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
     }();
     a.desync = desync_env;
     a.no_rot = rot_env ? 0 : 1;
+    static const int edge_env = [] {
+      const char* e = getenv("VINF_G256_EDGE");
+      return e ? atoi(e) : 1;
+    }();
+    a.no_edge = edge_env ? 0 : 1;
     const int ntiles = ntm * ntn, cus = device_cus_256();
     const int G = ntiles < cus ? ntiles : cus;
     hipLaunchKernelGGL((gemm256_persistent_kernel<AK, BK_, EPI>), dim3(G), dim3(NTHR), 0, stream,
