@@ -92,6 +92,16 @@ def _self_launch(a) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def _json_stdout():
+    """Keep this process's stdout to the ONE JSON line: native libraries write to fd 1 (RCCL
+    prints a version banner when its communicator comes up), so fd 1 is pointed at stderr for
+    the rest of the run and the JSON line goes to a duplicate of the original stdout."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(fd, "w")
+
+
 def main() -> int:
     a = _args()
     env_world = os.environ.get("WORLD_SIZE")
@@ -100,6 +110,7 @@ def main() -> int:
     if env_world is not None and int(env_world) != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={env_world}; launch one rank "
                          f"per GPU (torch.distributed.run --nproc-per-node {a.gpus}) or drop --gpus")
+    out_f = _json_stdout()
 
     import torch
 
@@ -186,7 +197,8 @@ def main() -> int:
                                    "no published number for this metric)",
             },
         }
-        print(json.dumps(out), flush=True)
+        out_f.write(json.dumps(out) + "\n")
+        out_f.flush()
     vdist.shutdown()
     return 0
 

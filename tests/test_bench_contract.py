@@ -21,7 +21,11 @@ def _port():
 
 
 def _json_lines(out: str):
-    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    # stdout carries nothing but the JSON line (bench.py points fd 1 of its ranks at stderr, so
+    # native banners - RCCL prints one on communicator init - cannot land in the driver's parse)
+    lines = [l for l in out.splitlines() if l.strip()]
+    assert all(l.startswith("{") for l in lines), lines
+    return [json.loads(l) for l in lines]
 
 
 def _check(rec, n):

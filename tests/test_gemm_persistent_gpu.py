@@ -148,3 +148,33 @@ def test_persistent_switch_bitwise(gpu):
     finally:
         torch.ops.vinf.gemm_persist(prev)
     assert torch.equal(y0, y1)
+
+
+def test_engine_persistent_forward_only_bitwise(gpu):
+    """DP policy (parallel/runner.py): persistent grid in the forward only, one block per tile in
+    the backward. Same K order per tile -> loss and every gradient bitwise equal to the
+    all-persistent step, and the global switch is left off for the backward's collectives."""
+    from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI
+
+    cfg = RealNVPConfig(dim=784, n_layers=2, hidden=1024, anneal="none")
+    B = 16384                         # 64 x 4 = 256 tiles: the 256x256 kernel is selected
+    g = torch.Generator(device=gpu).manual_seed(3)
+    eps = torch.randn(B, cfg.dim, device=gpu, generator=g)
+    out = []
+    prev = torch.ops.vinf.gemm_persist(1)
+    try:
+        for fwd_only in (False, True):
+            torch.ops.vinf.gemm_persist(0 if fwd_only else 1)
+            eng = RealNVPVI(cfg, batch=B, device=gpu, seed=4, lr=1e-3)
+            eng.persist_forward_only = fwd_only
+            eng.eps_override = eps
+            eng.params.grad.zero_()
+            eng.train_step()
+            torch.cuda.synchronize()
+            out.append((eng.loss.clone(), eng.params.grad.clone(), eng.params.master.clone()))
+            if fwd_only:
+                assert torch.ops.vinf.gemm_persist(-1) == 0
+    finally:
+        torch.ops.vinf.gemm_persist(prev)
+    (l0, g0, p0), (l1, g1, p1) = out
+    assert torch.equal(l0, l1) and torch.equal(g0, g1) and torch.equal(p0, p1)

@@ -41,6 +41,12 @@ from ..utils.flat import FlatLayout, FlatParams
 from ..utils.profiling import trace_range
 
 
+def _ext_native():
+    from ..ops._ext import native
+
+    return native()
+
+
 @dataclass
 class RealNVPConfig:
     dim: int = 784
@@ -120,6 +126,8 @@ class RealNVPVI:
         self.grad_scale_host = 1.0
         self.unit_ready_hook = None   # callable(unit_idx) after a unit's grads are final
         self.eps_override = None      # fixed base noise [B, D] (tests); None -> Philox sampler
+        # DP runner: persistent GEMM grid in the forward only (parallel/runner.py)
+        self.persist_forward_only = False
 
         L = cfg.n_layers
         layout = FlatLayout()
@@ -573,8 +581,16 @@ class RealNVPVI:
     def train_step(self, reduce_fn=None):
         """One full ELBO step: sample, flow fwd, target, bwd, [grad all-reduce], optimizer."""
         self._update_schedule()
+        fwd_persist = self.persist_forward_only and self.device.type == "cuda"
+        if fwd_persist:
+            # DP: no collective is in flight during the forward (the optimizer waited for every
+            # bucket), so the one-block-per-CU persistent grid is safe there; the backward,
+            # where RCCL all-reduces hold CUs beside the GEMMs, launches one block per tile
+            _ext_native().gemm_persist(1)
         with trace_range("flow_forward+elbo"):
             self.forward()
+        if fwd_persist:
+            _ext_native().gemm_persist(0)
         with trace_range("flow_backward"):
             self.backward()
         if reduce_fn is not None:

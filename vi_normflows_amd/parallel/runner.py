@@ -54,13 +54,18 @@ class DataParallelRunner:
         force = force_reduce or os.environ.get("VINF_FORCE_REDUCE", "0") == "1"
         if force and info.world == 1 and not dist.is_initialized():
             _init_single_rank_group(info)
-        if info.world > 1 and engine.device.type == "cuda" and os.environ.get("VINF_DP_PERSIST", "0") != "1":
-            # multi-rank: RCCL kernels run on CUs beside the step's GEMMs; a persistent GEMM
+        persist = os.environ.get("VINF_DP_PERSIST", "fwd")   # "1" all | "0" none | "fwd"
+        if (info.world > 1 or force) and engine.device.type == "cuda" and persist != "1":
+            # multi-rank: RCCL kernels run on CUs beside the backward's GEMMs; a persistent GEMM
             # grid (one block per CU, each owning a fixed tile list) would wait for every CU an
-            # all-reduce holds, so the products launch one block per tile instead
+            # all-reduce holds, so those products launch one block per tile instead. The
+            # forward has no collective in flight: engines that support it keep the persistent
+            # grid there (``persist_forward_only``).
             from ..ops._ext import native
 
             native().gemm_persist(0)
+            if persist == "fwd" and hasattr(engine, "persist_forward_only"):
+                engine.persist_forward_only = True
         if info.world > 1 or (force and dist.is_initialized()):
             P = engine.params
             if info.world > 1:
