@@ -129,6 +129,18 @@ def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: b
         if dev.type == "cuda":
             run.capture(warmup=1)
         return run.step, B, dev, "bf16"
+    if cfg_id == 4 and impl == "engine" and dev.type == "cuda":
+        from ..models.iaf_engine import IAFEngine
+        from ..models.iaf_vae import IAFVAEConfig, synthetic_images
+        from ..parallel.runner import DataParallelRunner
+
+        B = batch or 8192
+        X = synthetic_images(B * 4, device=dev, seed=info.rank).reshape(B * 4, -1)
+        eng = IAFEngine(IAFVAEConfig(), B, X, device=dev, seed=0, rank=info.rank)
+        run = DataParallelRunner(eng, info)
+        if graph:
+            run.capture(warmup=2)
+        return run.step, B, dev, "bf16, IAF engine" + (", hipGraph" if run.graph else "")
     if cfg_id == 4:
         from ..models.iaf_vae import IAFVAE, IAFVAEConfig, synthetic_images
 
@@ -237,7 +249,7 @@ def main(argv=None):
     ap.add_argument("--graph", default="on", choices=["on", "off"])
     ap.add_argument("--cpu", action="store_true", help="config 0 on the CPU")
     ap.add_argument("--impl", default="engine", choices=["engine", "module"],
-                    help="config 5: explicit-backward MAF engine or the autograd MAFDensity module")
+                    help="configs 4 / 5: explicit-backward IAF / MAF engine or the autograd modules")
     a = ap.parse_args(argv)
     info = vdist.init(device_type="cpu" if a.config == 1 or (a.config == 0 and a.cpu) else None)
     step, B, dev, dtype = build(a.config, info, a.batch, a.precision, a.graph == "on", a.impl)
