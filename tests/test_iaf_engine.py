@@ -141,3 +141,15 @@ def test_iaf_engine_graph_replay_gpu(gpu):
     assert t0 == t2 == 3.0
     assert abs(l0 - l2) <= 1e-3 * max(1.0, abs(l0))
     assert d_graph <= 3 * 2 * 3e-4 + 1e-6
+
+
+@pytest.mark.gpu
+def test_train_cli_iaf_uses_engine(gpu, tmp_path):
+    """train.py's iaf_vae task on GPU runs the engine (hipGraph) and writes its checkpoint."""
+    from vi_normflows_amd.train import main
+
+    final = main(["--config", "config4_iaf10_vae", "iters=30", "log_every=10", "batch=1024",
+                  f"out_dir={tmp_path}", "name=iaf_eng", "extra.n_data=2048"])
+    assert final["engine"] == "iaf_engine"
+    assert math.isfinite(final["free_energy"])
+    assert (tmp_path / "iaf_eng" / "ckpt.pt").exists()

@@ -143,14 +143,17 @@ class IAFEngine:
             for i, lin in enumerate(lins):
                 P.p(f"dec.W{i}").copy_(lin.weight)
                 P.p(f"dec.b{i}").copy_(lin.bias)
-            self.masks = []
+            first = not hasattr(self, "masks")   # masks / plans are structural: built once
+            if first:                             # (a captured graph holds the plan tensors)
+                self.masks = []
             lo = self._flow_lo
             for k, f in enumerate(model.flows):
                 made = f.made
                 l0, l1 = made.layers
-                m0 = torch.cat([l0.mask, torch.ones_like(made.ctx.weight)], 1).to(self.device)
-                m1 = l1.mask.to(self.device)
-                self.masks.append((m0, m1))
+                if first:
+                    m0 = torch.cat([l0.mask, torch.ones_like(made.ctx.weight)], 1).to(self.device)
+                    self.masks.append((m0, l1.mask.to(self.device)))
+                m0, m1 = self.masks[k]
                 P.p(f"f{k}.W0")[:, :dz].copy_(l0.weight * l0.mask)
                 P.p(f"f{k}.W0")[:, dz:].copy_(made.ctx.weight)
                 P.p(f"f{k}.b0").copy_(l0.bias + made.ctx.bias)
@@ -164,11 +167,12 @@ class IAFEngine:
         P.v.zero_()
         self.step_t.zero_()
         self.rng_offset.zero_()
-        self._plans = None
-        if self.device.type == "cuda":
-            from ..ops.masked import plan_for
+        if not hasattr(self, "_plans"):
+            self._plans = None
+            if self.device.type == "cuda":
+                from ..ops.masked import plan_for
 
-            self._plans = [(plan_for(m0), plan_for(m1)) for m0, m1 in self.masks]
+                self._plans = [(plan_for(m0), plan_for(m1)) for m0, m1 in self.masks]
 
     # ------------------------------------------------------------------ masked products
     def _m_fwd(self, k, i, x, W, b, out, relu):
@@ -353,6 +357,15 @@ class IAFEngine:
             reduce_fn()
         with trace_range("optimizer"):
             self.optimizer_step()
+
+    def state_dict(self) -> dict:
+        return {"params": self.params.state_dict(), "step": self.step_t.detach().cpu(),
+                "rng_offset": self.rng_offset.detach().cpu(), "cfg": dict(self.cfg.__dict__)}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.params.load_state_dict(sd["params"])
+        self.step_t.copy_(sd["step"])
+        self.rng_offset.copy_(sd["rng_offset"])
 
     def flops_per_sample(self) -> float:
         """Dense-equivalent GEMM FLOPs per sample (forward + backward)."""

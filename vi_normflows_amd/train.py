@@ -181,8 +181,37 @@ def run_iaf_vae(cfg, out, info, logger):
     from .models.iaf_vae import IAFVAE, IAFVAEConfig, synthetic_images
 
     dev = _device(cfg, info)
-    model = IAFVAE(IAFVAEConfig(dim_z=cfg.dim_z, hidden=cfg.hidden, n_flows=cfg.K)).to(dev)
+    icfg = IAFVAEConfig(dim_z=cfg.dim_z, hidden=cfg.hidden, n_flows=cfg.K)
+    torch.manual_seed(cfg.seed)
+    model = IAFVAE(icfg).to(dev)
     X = synthetic_images(cfg.extra.get("n_data", 8192), seed=cfg.seed + info.rank, device=dev)
+    nb = X.shape[0] // cfg.batch
+    if (dev.type == "cuda" and cfg.optimizer == "adam" and cfg.schedule == "none" and nb > 0
+            and cfg.extra.get("engine", True)):
+        # models/iaf_engine.py: flat buffers, explicit backward, one hipGraph (DP: the runner's
+        # bucketed all-reduce; rank 0's parameters are broadcast)
+        from .models.iaf_engine import IAFEngine
+        from .parallel.runner import DataParallelRunner
+        from .utils.checkpoint import save_engine
+
+        eng = IAFEngine(icfg, cfg.batch, X[:nb * cfg.batch].reshape(nb * cfg.batch, -1),
+                        device=dev, seed=rank_seed(cfg.seed, info.rank), rank=info.rank,
+                        lr=cfg.lr, model=model)
+        run = DataParallelRunner(eng, info)
+        if cfg.extra.get("graph", True):
+            run.capture(warmup=1)
+            eng.load_module(model)     # the capture warm-up stepped Adam: start from the init
+        t0 = time.perf_counter()
+        for t in range(cfg.iters):
+            run.step()
+            if t % cfg.log_every == 0 or t == cfg.iters - 1:
+                F = float(eng.loss.item())
+                logger.log({"step": t, "F": F, "skipped": float(eng.n_skipped.item()),
+                            "samples_per_s": (t + 1) * cfg.batch * info.world
+                            / (time.perf_counter() - t0)})
+        save_engine(eng, out / "ckpt.pt", info.rank)
+        vdist.barrier()
+        return {"free_energy": float(eng.loss.item()), "engine": "iaf_engine"}
     gd = torch.Generator(device=dev).manual_seed(rank_seed(cfg.seed, info.rank))
 
     def loss_fn(t, beta):
