@@ -842,6 +842,8 @@ void gemm_fp8_nt(const at::Tensor& xq, const at::Tensor& sx, const at::Tensor& w
 }
 
 void gemm_set_mode(int64_t mode, int64_t depth) { nf_gemm_set_mode((int)mode, (int)depth); }
+int nf_gemm256_xcd_pack(int on);
+int64_t gemm_wgrad_xcd_pack(int64_t on) { return nf_gemm256_xcd_pack((int)on); }
 int64_t gemm_persist(int64_t on) {   // on < 0: query only; returns the previous setting
   const int prev = nf_gemm256_get_persist();
   if (on >= 0) nf_gemm256_set_persist((int)on);
@@ -859,6 +861,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
 #endif
   m.def("gemm_set_mode(int mode, int depth) -> ()", &gemm_set_mode);
   m.def("gemm_persist(int on) -> int", &gemm_persist);
+  m.def("gemm_wgrad_xcd_pack(int on) -> int", &gemm_wgrad_xcd_pack);
   m.def("fp8_quant_rows(Tensor x, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("fp8_quant_tensor(Tensor x, Tensor(a!) q, Tensor amax_prev, Tensor(b!) scale, Tensor(c!) amax_cur) -> ()");
   m.def("gemm_fp8_nt(Tensor xq, Tensor sx, Tensor wq, Tensor sw, Tensor? b, Tensor(a!) y, int relu, Tensor? krange, Tensor(b!)? yq=None, Tensor? q_amax_prev=None, Tensor(c!)? q_scale=None, Tensor(d!)? q_amax_cur=None, Tensor? krange256=None) -> ()");

@@ -955,15 +955,21 @@ struct TnDesc {
   int lda, ldb, ldc, M, N, K, start, staged;
 };
 constexpr int TN_MULTI_MAX = 40;   // 80-B descriptors: the table stays inside the 4 KiB kernarg
+constexpr int TN_PERM_MAX = 256;   // + 512 B: 3724 B of kernarg with 40 descriptors
 struct TnMulti {
   TnDesc d[TN_MULTI_MAX];
-  int n, tile0, ntiles;
+  int n, tile0, ntiles, use_perm;
+  // XCD packing (VINF_WGRAD_XCD_PACK): block position -> tile offset. Positions
+  // [x * ntiles/8, (x+1) * ntiles/8) run on XCD x (xcd_remap), so the permutation keeps each
+  // problem's tiles - which share A / B panels - inside one XCD's L2 where they fit
+  unsigned short perm[TN_PERM_MAX];
 };
 
 template <int D>
 __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
   __shared__ __attribute__((aligned(16))) char smem[smem_bytes(D)];
-  const int id = t.tile0 + xcd_remap(blockIdx.x, t.ntiles);
+  const int pos = xcd_remap(blockIdx.x, t.ntiles);
+  const int id = t.tile0 + (t.use_perm ? (int)t.perm[pos] : pos);
   int p = 0;
   for (int q = 1; q < t.n; ++q)
     if (id >= t.d[q].start) p = q;
@@ -986,6 +992,11 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
 // block per CU runs, and a persistent block that cannot start delays its whole tile list)
 static int g_persist = [] {
   const char* e = getenv("VINF_G256_PERSIST");
+  return e ? atoi(e) : 1;
+}();
+
+static int g_xcd_pack = [] {
+  const char* e = getenv("VINF_WGRAD_XCD_PACK");
   return e ? atoi(e) : 1;
 }();
 
@@ -1096,6 +1107,11 @@ using namespace nf::gemm;
 // earlier (VINF_G256_DEPTH at load, or set_mode's depth argument)
 void nf_gemm256_set_depth(int d) { g256::g_depth = d == 6 ? 6 : 4; }
 void nf_gemm256_set_persist(int on) { g256::g_persist = on ? 1 : 0; }
+int nf_gemm256_xcd_pack(int on) {   // on < 0: query; returns the previous setting
+  const int prev = g256::g_xcd_pack;
+  if (on >= 0) g256::g_xcd_pack = on ? 1 : 0;
+  return prev;
+}
 int nf_gemm256_get_persist() { return g256::g_persist; }
 
 // y[M][N] = act(x[M][K] W[N][K]^T + bias) -> bf16
@@ -1431,6 +1447,41 @@ void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int
   }
   t.tile0 = tile0;
   t.ntiles = ntiles;
+  if (g256::g_xcd_pack && ntiles % 8 == 0 && ntiles <= g256::TN_PERM_MAX) {
+    // first-fit-decreasing packing of this launch's problem segments into the 8 XCD bins
+    const int cap = ntiles / 8;
+    int seg_lo[g256::TN_MULTI_MAX], seg_n[g256::TN_MULTI_MAX], order[g256::TN_MULTI_MAX];
+    for (int i = 0; i < t.n; ++i) {
+      const int lo = t.d[i].start > tile0 ? t.d[i].start : tile0;
+      const int hi_p = i + 1 < t.n ? t.d[i + 1].start : base;
+      const int hi = hi_p < tile0 + ntiles ? hi_p : tile0 + ntiles;
+      seg_lo[i] = lo - tile0;
+      seg_n[i] = hi - lo;
+      order[i] = i;
+    }
+    for (int i = 1; i < t.n; ++i)   // stable insertion sort, largest segment first
+      for (int j = i; j > 0 && seg_n[order[j]] > seg_n[order[j - 1]]; --j) {
+        const int tmp = order[j]; order[j] = order[j - 1]; order[j - 1] = tmp;
+      }
+    int fill[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int oi = 0; oi < t.n; ++oi) {
+      int lo = seg_lo[order[oi]], n = seg_n[order[oi]];
+      while (n > 0) {
+        int b = -1;   // tightest bin that takes the whole segment, else the emptiest bin
+        for (int x = 0; x < 8; ++x)
+          if (cap - fill[x] >= n && (b < 0 || fill[x] > fill[b])) b = x;
+        if (b < 0)
+          for (int x = 0; x < 8; ++x)
+            if (b < 0 || fill[x] < fill[b]) b = x;
+        const int take = n < cap - fill[b] ? n : cap - fill[b];
+        for (int k = 0; k < take; ++k) t.perm[b * cap + fill[b] + k] = (unsigned short)(lo + k);
+        fill[b] += take;
+        lo += take;
+        n -= take;
+      }
+    }
+    t.use_perm = 1;
+  }
   if (g256::g_depth == 6)
     hipLaunchKernelGGL(g256::gemm256_multi_kernel<6>, dim3(ntiles), dim3(g256::NTHR), 0, stream, t);
   else

@@ -178,3 +178,33 @@ def test_engine_persistent_forward_only_bitwise(gpu):
         torch.ops.vinf.gemm_persist(prev)
     (l0, g0, p0), (l1, g1, p1) = out
     assert torch.equal(l0, l1) and torch.equal(g0, g1) and torch.equal(p0, p1)
+
+
+def test_wgrad_xcd_packing_bitwise(gpu):
+    """The weight-gradient launches pack each problem's tiles into one XCD's block range
+    (gemm256.hip, VINF_WGRAD_XCD_PACK): a permutation of which block computes which tile, so
+    every gradient is bitwise equal to the unpacked order. RealNVP-8 at B = 16384: 320 tiles
+    in launches of one tile per CU, problems of 16 / 16 / 8 tiles straddling the bins."""
+    from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI
+
+    cfg = RealNVPConfig(dim=784, n_layers=8, hidden=1024, anneal="none")
+    B = 16384
+    g = torch.Generator(device=gpu).manual_seed(9)
+    eps = torch.randn(B, cfg.dim, device=gpu, generator=g)
+    out = []
+    prev = torch.ops.vinf.gemm_wgrad_xcd_pack(-1)
+    try:
+        for pack in (0, 1):
+            torch.ops.vinf.gemm_wgrad_xcd_pack(pack)
+            eng = RealNVPVI(cfg, batch=B, device=gpu, seed=2, lr=1e-3)
+            assert eng.wgrad_defer
+            eng.eps_override = eps
+            eng.params.grad.zero_()
+            eng.forward()
+            eng.backward()
+            torch.cuda.synchronize()
+            out.append(eng.params.grad.clone())
+    finally:
+        torch.ops.vinf.gemm_wgrad_xcd_pack(prev)
+    assert torch.equal(out[0], out[1])
+    assert out[0].abs().sum() > 0
