@@ -612,7 +612,7 @@ void maf_bwd(const at::Tensor& gu, const at::Tensor& u, const at::Tensor& o, dou
 
 // gated IAF update: y = m + sigmoid(s + gb) (z - m), ldj = sum log sigmoid(s + gb)
 void iaf_gate_fwd(const at::Tensor& o, const at::Tensor& z, double gate_bias, const at::Tensor& y,
-                  const at::Tensor& ldj) {
+                  const at::Tensor& ldj, const c10::optional<at::Tensor>& ybf) {
   chk_mat(o, "o", at::kBFloat16);
   chk_mat(z, "z", at::kFloat);
   chk_mat(y, "y", at::kFloat);
@@ -621,8 +621,19 @@ void iaf_gate_fwd(const at::Tensor& o, const at::Tensor& z, double gate_bias, co
                   y.size(1) == D, "iaf_gate_fwd shapes");
   TORCH_CHECK(ldj.is_cuda() && ldj.scalar_type() == at::kFloat && ldj.is_contiguous() &&
                   ldj.numel() == B, "ldj: fp32 [B]");
+  void* yb = nullptr;
+  long ldyb = 0;
+  if (ybf && ybf->defined()) {   // optional bf16 copy of y (e.g. the next MADE's operand columns)
+    chk_mat(*ybf, "ybf", at::kBFloat16);
+    TORCH_CHECK(ybf->size(0) == B && ybf->size(1) == D && ld2(*ybf) % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(ybf->data_ptr()) % 8 == 0,
+                "ybf: bf16 [B, D], 8-B aligned rows");
+    yb = ybf->data_ptr();
+    ldyb = ld2(*ybf);
+  }
   nf_launch_iaf_gate_fwd(o.data_ptr(), ld2(o), z.data_ptr<float>(), ld2(z), B, D, (float)gate_bias,
-                         y.data_ptr<float>(), ld2(y), ldj.data_ptr<float>(), cur_stream());
+                         y.data_ptr<float>(), ld2(y), ldj.data_ptr<float>(), cur_stream(), yb,
+                         ldyb);
 }
 
 void iaf_gate_bwd(const at::Tensor& gy, const c10::optional<at::Tensor>& gl, const at::Tensor& z,
@@ -881,7 +892,8 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("fp8_dgrad(Tensor dyq, Tensor sa, Tensor Wtq, Tensor sb, Tensor h, Tensor(a!) dx, Tensor krange256, Tensor(b!)? dxq=None, Tensor? q_amax_prev=None, Tensor(c!)? q_scale=None, Tensor(d!)? q_amax_cur=None) -> ()");
   m.def("fp8_quant_rows_strided(Tensor x, int layer_stride, int rows_per, int layers, int C, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("maf_fwd(Tensor x, Tensor o, float bound, Tensor(a!) u, Tensor(b!)? ubf, Tensor(c!)? uq, Tensor? amax_prev, Tensor(d!)? scale, Tensor(e!)? amax_cur, Tensor(f!) ldj, bool ldj_init) -> ()");
-  m.def("iaf_gate_fwd(Tensor o, Tensor z, float gate_bias, Tensor(a!) y, Tensor(b!) ldj) -> ()");
+  m.def("iaf_gate_fwd(Tensor o, Tensor z, float gate_bias, Tensor(a!) y, Tensor(b!) ldj, "
+        "Tensor(c!)? ybf=None) -> ()");
   m.def("iaf_gate_bwd(Tensor gy, Tensor? gl, Tensor z, Tensor o, float gate_bias, Tensor(a!) dout, Tensor(b!) gz) -> ()");
   m.def("maf_bwd(Tensor gu, Tensor u, Tensor o, float bound, float c_ldj, Tensor(a!) dout, Tensor(b!) gx, Tensor? c_row=None) -> ()");
 }

@@ -219,7 +219,8 @@ void nf_launch_maf_bwd(const float* gu, long ldg, const float* u, long ldu, cons
                        float* gx, long ldgx, hipStream_t stream, const float* c_row = nullptr);
 // maf.hip: gated IAF update (o = [m | s] bf16 from the MADE GEMM)
 void nf_launch_iaf_gate_fwd(const void* o, long ldo, const float* z, long ldz, int B, int D,
-                            float gate_bias, float* y, long ldy, float* ldj, hipStream_t stream);
+                            float gate_bias, float* y, long ldy, float* ldj, hipStream_t stream,
+                            void* ybf = nullptr, long ldyb = 0);
 void nf_launch_iaf_gate_bwd(const float* gy, long ldg, const float* gl, const float* z, long ldz,
                             const void* o, long ldo, int B, int D, float gate_bias, void* dout,
                             long lddo, float* gz, long ldgz, hipStream_t stream);

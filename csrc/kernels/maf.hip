@@ -152,7 +152,8 @@ __global__ void __launch_bounds__(256) iaf_gate_fwd_kernel(const bf16_t* __restr
                                                            const float* __restrict__ z, long ldz,
                                                            int B, int D, float gb,
                                                            float* __restrict__ y, long ldy,
-                                                           float* __restrict__ ldj) {
+                                                           float* __restrict__ ldj,
+                                                           bf16_t* __restrict__ ybf, long ldyb) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
@@ -160,6 +161,7 @@ __global__ void __launch_bounds__(256) iaf_gate_fwd_kernel(const bf16_t* __restr
   const bf16_t* sr = mr + D;
   const float* zr = z + (long)row * ldz;
   float* yr = y + (long)row * ldy;
+  bf16_t* ybr = ybf ? ybf + (long)row * ldyb : nullptr;   // the next MADE's bf16 operand
   float acc = 0.f;
   for (int c = lane * 4; c < D; c += 256) {
     const ushort4 mv = *reinterpret_cast<const ushort4*>(mr + c);
@@ -176,6 +178,11 @@ __global__ void __launch_bounds__(256) iaf_gate_fwd_kernel(const bf16_t* __restr
       acc += log_sigmoidf_(t);
     }
     *reinterpret_cast<float4*>(yr + c) = make_float4(ys[0], ys[1], ys[2], ys[3]);
+    if (ybr) {
+      ushort4 b;
+      b.x = f2bf(ys[0]); b.y = f2bf(ys[1]); b.z = f2bf(ys[2]); b.w = f2bf(ys[3]);
+      *reinterpret_cast<ushort4*>(ybr + c) = b;
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
@@ -230,10 +237,12 @@ __global__ void __launch_bounds__(256) iaf_gate_bwd_kernel(const float* __restri
 using namespace nf;
 
 void nf_launch_iaf_gate_fwd(const void* o, long ldo, const float* z, long ldz, int B, int D,
-                            float gate_bias, float* y, long ldy, float* ldj, hipStream_t stream) {
+                            float gate_bias, float* y, long ldy, float* ldj, hipStream_t stream,
+                            void* ybf, long ldyb) {
   if (B <= 0) return;
   hipLaunchKernelGGL(iaf_gate_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream,
-                     (const bf16_t*)o, ldo, z, ldz, B, D, gate_bias, y, ldy, ldj);
+                     (const bf16_t*)o, ldo, z, ldz, B, D, gate_bias, y, ldy, ldj, (bf16_t*)ybf,
+                     ldyb);
   NF_HIP_CHECK(hipGetLastError());
 }
 

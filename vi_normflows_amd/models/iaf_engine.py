@@ -119,7 +119,7 @@ class IAFEngine:
         # backward
         self.dlogits = e(B, X)
         self.dD = [e(B, H), e(B, H)]
-        self.DX = [e(B, dz + C, dt=f32), e(B, dz + C, dt=f32)]   # [dz_k | running d(context)]
+        self.DX = e(B, dz + C, dt=f32)            # [dz_k | running d(context)]
         self.dOm = e(B, 2 * dz)
         self.dAm = e(B, Hm)
         self.dOenc = e(B, 2 * dz + C)
@@ -205,17 +205,18 @@ class IAFEngine:
         torch.mm(dy.t(), x, out=dW)
         torch.sum(dy, 0, out=db)
 
-    def _gate_fwd(self, o, z, gb, y, ldj):
+    def _gate_fwd(self, o, z, gb, y, ldj, ybf):
         if self._plans is not None:
             from ..ops._ext import native
 
-            native().iaf_gate_fwd(o, z, gb, y, ldj)
+            native().iaf_gate_fwd(o, z, gb, y, ldj, ybf)   # + the next operand's bf16 columns
             return
         dz = z.shape[1]
         m, s = o[:, :dz].float(), o[:, dz:].float() + gb
         sg = torch.sigmoid(s)
         y.copy_(m + sg * (z - m))
         ldj.copy_(torch.nn.functional.logsigmoid(s).sum(1))
+        ybf.copy_(y)
 
     def _gate_bwd(self, gy, gl, z, o, gb, dout, gz):
         if self._plans is not None:
@@ -226,10 +227,10 @@ class IAFEngine:
         dz = z.shape[1]
         m, s = o[:, :dz].float(), o[:, dz:].float() + gb
         sg = torch.sigmoid(s)
-        gz.copy_(gy * sg)
         dout[:, :dz].copy_(gy * (1 - sg))
         # y = m + sg (z - m): dy/ds = sg (1 - sg)(z - m); ldj = sum log sg: d/ds = 1 - sg
         dout[:, dz:].copy_(gy * sg * (1 - sg) * (z - m) + gl[:, None] * (1 - sg))
+        gz.copy_(gy * sg)          # last: gz may alias gy (the engine updates dz_k in place)
 
     # ------------------------------------------------------------------ step
     def _load_batch(self):
@@ -262,17 +263,21 @@ class IAFEngine:
         self._sig = torch.exp(0.5 * lv)
         torch.addcmul(mu, self._sig, eps, out=self.Z[0])
         self.lq.copy_(-0.5 * dz * LOG2PI - 0.5 * lv.sum(1) - 0.5 * (eps * eps).sum(1))
-        # IAF layers: [z_k | h] -> MADE -> gated update
+        # IAF layers: [z_k | h] -> MADE -> gated update. The context columns of every layer's
+        # operand are filled in one copy; the z columns of layer k+1 (and the decoder input)
+        # come from layer k's gate kernel as its bf16 side output
+        C = cfg.context
+        self.Xin[:, :, dz:].copy_(self.Oenc[:, 2 * dz:].unsqueeze(0).expand(K, B, C))
+        self.Xin[0][:, :dz].copy_(self.Z[0])
         for k in range(K):
             xin = self.Xin[k]
-            xin[:, :dz].copy_(self.Z[k])
-            xin[:, dz:].copy_(self.Oenc[:, 2 * dz:])
             self._m_fwd(k, 0, xin, P.c(f"f{k}.W0"), P.c(f"f{k}.b0"), self.Am[k], True)
             self._m_fwd(k, 1, self.Am[k], P.c(f"f{k}.W1"), P.c(f"f{k}.b1"), self.Om[k], False)
-            self._gate_fwd(self.Om[k], self.Z[k], self.gate_bias[k], self.Z[k + 1], self.ldjk[k])
+            nxt = self.Xin[k + 1][:, :dz] if k + 1 < K else self.zKb
+            self._gate_fwd(self.Om[k], self.Z[k], self.gate_bias[k], self.Z[k + 1], self.ldjk[k],
+                           nxt)
         # decoder + likelihood
         zK = self.Z[K]
-        self.zKb.copy_(zK)
         h = self.zKb
         for i in range(3):
             out = self.D[i] if i < 2 else self.logits
@@ -300,23 +305,23 @@ class IAFEngine:
         gemm.linear_wgrad_group([
             (self.dD[1], self.D[0], P.g("dec.W1"), P.g("dec.b1")),
             (self.dD[0], self.zKb, P.g("dec.W0"), P.g("dec.b0"))])
-        cur = self.DX[0]
+        cur = self.DX
         # dF/dz_K: prior term (beta/B) z_K plus the decoder path; context-gradient sum = 0
         torch.mul(self.Z[K], self.beta / B, out=cur[:, :dz])
         cur[:, dz:].zero_()
         gemm.linear_dgrad(self.dD[0], P.c("dec.W0"), cur[:, :dz], accumulate=True)
         self._hook(K + 1)
-        # IAF layers, top down: DX holds [dz_k | sum of the context gradients so far]
+        # IAF layers, top down: DX holds [dz_k | sum of the context gradients so far]; the gate
+        # backward turns dz_{k+1} into its direct-path dz_k in place (each element is read
+        # before it is written, by the same lane) and the MADE input gradient accumulates onto
+        # both parts
         for k in range(K - 1, -1, -1):
-            nxt = self.DX[(K - k) % 2]
             self._gate_bwd(cur[:, :dz], self.gl, self.Z[k], self.Om[k], self.gate_bias[k],
-                           self.dOm, nxt[:, :dz])
-            nxt[:, dz:].copy_(cur[:, dz:])
+                           self.dOm, cur[:, :dz])
             self._m_wgrad(k, 1, self.dOm, self.Am[k], P.g(f"f{k}.W1"), P.g(f"f{k}.b1"))
             self._m_dgrad(k, 1, self.dOm, P.c(f"f{k}.W1"), self.Am[k], self.dAm, False)
             self._m_wgrad(k, 0, self.dAm, self.Xin[k], P.g(f"f{k}.W0"), P.g(f"f{k}.b0"))
-            self._m_dgrad(k, 0, self.dAm, P.c(f"f{k}.W0"), None, nxt, True)
-            cur = nxt
+            self._m_dgrad(k, 0, self.dAm, P.c(f"f{k}.W0"), None, cur, True)
             # masked weight entries get a zero gradient (keeps them at zero under Adam)
             a, b = self.layout.unit_ranges[k + 1]
             P.grad[a:b].mul_(self.flow_mask[a - self._flow_lo:b - self._flow_lo])
