@@ -213,3 +213,58 @@ def test_iaf_engine_dp_gradient_equals_single_process(tmp_path):
     single.backward()
     err = (r0["grad"] / world - single.params.grad).abs().max()
     assert err <= 1e-5 * (1 + single.params.grad.abs().max()), float(err)
+
+
+@pytest.mark.gpu
+def test_iaf_engine_bf16_vs_fp32_oracle(gpu):
+    """bf16 fidelity at config-4 widths (3072 -> 1024 -> 1024 encoder, 10 IAF layers with
+    1024-wide MADEs, 256-d latent, 256-d context): the GPU engine (bf16 operands, fp32
+    accumulation, fp32 z chain / log-dets / likelihood) against fp32 autograd through
+    ``IAFVAE.loss`` on the CPU, same weights and base noise, B = 256. Every product rounds its
+    operands to bf16 (u = 2^-8): the loss is a batch mean of sums of 3072 Bernoulli terms
+    (~2800 nats) whose per-logit rounding errors are independent, so it lands far inside 1e-4
+    relative (measured 2e-6); each parameter's gradient is a product of two bf16 operands over
+    K = batch plus the backward chain's own rounding: 4e-2 relative L2 (measured worst 1.8e-2,
+    the 3072-wide first encoder layer)."""
+    cfg = IAFVAEConfig()
+    B = 256
+    torch.manual_seed(21)
+    model = IAFVAE(cfg)
+    with torch.no_grad():
+        model.enc_out.weight.normal_(0, 0.02)
+        model.enc_out.bias.normal_(0, 0.1)
+        for f in model.flows:
+            f.made.layers[-1].weight.normal_(0, 0.05)
+            f.made.layers[-1].weight.mul_(f.made.layers[-1].mask)
+            f.made.layers[-1].bias.normal_(0, 0.1)
+    data = synthetic_images(B, cfg.image_shape, seed=3).reshape(B, -1)
+    eps = torch.randn(B, cfg.dim_z, generator=torch.Generator().manual_seed(4))
+    eng = IAFEngine(cfg, B, data.to(gpu), device=gpu, model=model.to(gpu))
+    eng.eps_override = eps.to(gpu)
+    eng.forward()
+    eng.backward()
+    torch.cuda.synchronize()
+    ref = model.cpu()
+    F = _module_grads(ref, data, eps)
+    rel_loss = abs(float(eng.loss) - float(F)) / abs(float(F))
+    P = eng.params
+    dz = cfg.dim_z
+    pairs = []
+    lins = [m for m in ref.encoder if isinstance(m, torch.nn.Linear)] + [ref.enc_out]
+    for i, lin in enumerate(lins):
+        pairs += [(f"enc.W{i}", lin.weight.grad), (f"enc.b{i}", lin.bias.grad)]
+    for i, lin in enumerate([m for m in ref.decoder if isinstance(m, torch.nn.Linear)]):
+        pairs += [(f"dec.W{i}", lin.weight.grad), (f"dec.b{i}", lin.bias.grad)]
+    for k, f in enumerate(ref.flows):
+        l0, l1 = f.made.layers
+        pairs += [(f"f{k}.W1", l1.weight.grad * l1.mask), (f"f{k}.b1", l1.bias.grad),
+                  (f"f{k}.b0", l0.bias.grad)]
+    worst, which = 0.0, None
+    for name, g in pairs:
+        ga = P.g(name).float().cpu()
+        rel = float((ga - g).norm() / g.norm().clamp_min(1e-12))
+        if rel > worst:
+            worst, which = rel, name
+    print(f"[iaf engine] bf16 vs fp32 oracle: loss rel {rel_loss:.2e}, worst grad rel {worst:.2e} ({which})")
+    assert rel_loss <= 1e-4
+    assert worst <= 4e-2, (which, worst)
