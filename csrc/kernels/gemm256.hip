@@ -28,6 +28,7 @@
 // The two wave row-groups run one barrier apart (wr == 1 takes an extra barrier up front), so
 // on each SIMD one wave issues its LDS reads / DMA while the other runs MFMAs.
 #include "gemm_tile.h"
+#include "wgrad_pack.h"
 
 // Diagnostic build only (csrc/build.py --variant stamps -D NF_G256_STAMPS): every block records
 // s_memrealtime (100 MHz, chip-global) at body entry, after the prologue wait, after the main
@@ -1447,40 +1448,16 @@ void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int
   }
   t.tile0 = tile0;
   t.ntiles = ntiles;
-  if (g256::g_xcd_pack && ntiles % 8 == 0 && ntiles <= g256::TN_PERM_MAX) {
-    // first-fit-decreasing packing of this launch's problem segments into the 8 XCD bins
-    const int cap = ntiles / 8;
-    int seg_lo[g256::TN_MULTI_MAX], seg_n[g256::TN_MULTI_MAX], order[g256::TN_MULTI_MAX];
+  if (g256::g_xcd_pack && ntiles <= g256::TN_PERM_MAX) {
+    int seg_lo[g256::TN_MULTI_MAX], seg_n[g256::TN_MULTI_MAX];
     for (int i = 0; i < t.n; ++i) {
       const int lo = t.d[i].start > tile0 ? t.d[i].start : tile0;
       const int hi_p = i + 1 < t.n ? t.d[i + 1].start : base;
       const int hi = hi_p < tile0 + ntiles ? hi_p : tile0 + ntiles;
       seg_lo[i] = lo - tile0;
       seg_n[i] = hi - lo;
-      order[i] = i;
     }
-    for (int i = 1; i < t.n; ++i)   // stable insertion sort, largest segment first
-      for (int j = i; j > 0 && seg_n[order[j]] > seg_n[order[j - 1]]; --j) {
-        const int tmp = order[j]; order[j] = order[j - 1]; order[j - 1] = tmp;
-      }
-    int fill[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int oi = 0; oi < t.n; ++oi) {
-      int lo = seg_lo[order[oi]], n = seg_n[order[oi]];
-      while (n > 0) {
-        int b = -1;   // tightest bin that takes the whole segment, else the emptiest bin
-        for (int x = 0; x < 8; ++x)
-          if (cap - fill[x] >= n && (b < 0 || fill[x] > fill[b])) b = x;
-        if (b < 0)
-          for (int x = 0; x < 8; ++x)
-            if (b < 0 || fill[x] < fill[b]) b = x;
-        const int take = n < cap - fill[b] ? n : cap - fill[b];
-        for (int k = 0; k < take; ++k) t.perm[b * cap + fill[b] + k] = (unsigned short)(lo + k);
-        fill[b] += take;
-        lo += take;
-        n -= take;
-      }
-    }
-    t.use_perm = 1;
+    t.use_perm = nf::wgrad_xcd_perm(t.n, seg_lo, seg_n, ntiles, t.perm) ? 1 : 0;
   }
   if (g256::g_depth == 6)
     hipLaunchKernelGGL(g256::gemm256_multi_kernel<6>, dim3(ntiles), dim3(g256::NTHR), 0, stream, t);
