@@ -39,7 +39,9 @@ LOG2PI = math.log(2 * math.pi)
 
 class IAFEngine:
     """Explicit-backward IAF VAE step on flat buffers. ``data``: fp32 [n_batches * B, dim_x]
-    binary images held on the device; step t trains on batch t mod n_batches."""
+    binary images held on the device; step t trains on batch t mod n_batches. The objective
+    uses a fixed ``beta`` (config 4's ELBO); the annealed schedules run on the module path
+    (``train.py`` picks the engine only for ``schedule=none`` with Adam)."""
 
     def __init__(self, cfg: IAFVAEConfig, batch: int, data: torch.Tensor, device="cuda",
                  seed: int = 0, rank: int = 0, lr: float = 3e-4, betas=(0.9, 0.999),
