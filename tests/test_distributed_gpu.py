@@ -122,3 +122,55 @@ def test_rccl_reducer_eager_and_captured_bitwise(tmp_path):
     assert torch.equal(r["plain"], r["rccl_eager"])
     assert torch.equal(r["plain"], r["rccl_graph"])
     assert r["plain_loss"] == r["rccl_graph_loss"]
+
+
+def _rccl_iaf_worker(rank, port, out_dir):
+    """Config 4 on the DP path: the IAF engine with the forced bucketed all-reduce on a 1-rank
+    RCCL communicator, eager and captured into the step hipGraph, against the no-reduce
+    engine (3 steps each)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0")
+    from vi_normflows_amd.models.iaf_engine import IAFEngine
+    from vi_normflows_amd.models.iaf_vae import IAFVAEConfig, synthetic_images
+    from vi_normflows_amd.parallel import dist as vdist
+    from vi_normflows_amd.parallel.runner import DataParallelRunner
+
+    info = vdist.init()
+    dev = info.device
+    cfg = IAFVAEConfig()
+    B = 1024
+    data = synthetic_images(2 * B, cfg.image_shape, seed=2, device=dev).reshape(2 * B, -1)
+    out = {}
+    for name in ("plain", "rccl_eager", "rccl_graph"):
+        eng = IAFEngine(cfg, B, data, device=dev, seed=3)
+        run = DataParallelRunner(eng, info, bucket_cap_mb=8.0, force_reduce=(name != "plain"))
+        if name != "plain":
+            assert run.reducer is not None and len(run.reducer.buckets) > 2
+        if name == "rccl_graph":
+            assert run.capture(warmup=1), "hipGraph capture with RCCL collectives failed"
+            run.step()
+            run.step()
+        else:
+            for _ in range(3):
+                run.step()
+        torch.cuda.synchronize()
+        out[name] = eng.params.master.cpu()
+        out[name + "_loss"] = float(eng.loss.item())
+        out[name + "_step"] = float(eng.step_t.item())
+    torch.save(out, os.path.join(out_dir, "rccl_iaf.pt"))
+    dist.destroy_process_group()
+
+
+def test_rccl_reducer_iaf_engine(tmp_path):
+    mp.spawn(_rccl_iaf_worker, args=(_port(), str(tmp_path)), nprocs=1, join=True)
+    r = torch.load(tmp_path / "rccl_iaf.pt", weights_only=True)
+    for k in ("plain", "rccl_eager", "rccl_graph"):
+        assert r[k + "_step"] == 3.0
+    d_e = float((r["plain"] - r["rccl_eager"]).abs().max())
+    d_g = float((r["plain"] - r["rccl_graph"]).abs().max())
+    print(f"[iaf rccl] max |dp| eager {d_e:.3e} graph {d_g:.3e}; losses {r['plain_loss']:.4f} "
+          f"{r['rccl_eager_loss']:.4f} {r['rccl_graph_loss']:.4f}")
+    # a 1-rank SUM all-reduce is the identity; Adam's sign-flip scale bounds any
+    # rounding-level difference between separately constructed engines (2 lr per step)
+    assert d_e <= 3 * 2 * 3e-4 + 1e-6 and d_g <= 3 * 2 * 3e-4 + 1e-6
+    assert abs(r["plain_loss"] - r["rccl_graph_loss"]) <= 1e-3 * max(1.0, abs(r["plain_loss"]))
