@@ -63,7 +63,6 @@ def _args(argv=None):
     ap.add_argument("--anneal", choices=["none", "reference"], default="none",
                     help="beta_t schedule: none (beta = 1) or the reference's min(1, 0.001 + t/T)")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto")
-    ap.add_argument("--gemm", choices=["mfma", "blas"], default=os.environ.get("VINF_GEMM", "mfma"))
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--force-reduce", action="store_true",
                     help="run the bucketed all-reduce path even at world size 1 (RCCL check)")
@@ -115,11 +114,9 @@ def main() -> int:
     import torch
 
     from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI
-    from vi_normflows_amd.ops import gemm
     from vi_normflows_amd.parallel import dist as vdist
     from vi_normflows_amd.parallel.runner import DataParallelRunner
 
-    gemm.set_backend(a.gemm)
     info = vdist.init(device_type="cpu" if a.cpu else None)
     world = info.world
     cfg = RealNVPConfig(dim=a.dim, n_layers=a.layers, hidden=a.hidden, anneal=a.anneal,
@@ -183,7 +180,7 @@ def main() -> int:
             "notes": {
                 "per_gpu_batch": a.batch,
                 "hipgraph": captured,
-                "gemm_backend": a.gemm,
+                "gemm_backend": "mfma",
                 "model_tflops": round(tflops, 1),
                 "optimizer": f"adam lr {a.lr:g}, linear warm-up {a.lr_warmup:g} steps, "
                              f"clip {a.max_grad_norm:g}, anneal {a.anneal}",

@@ -111,7 +111,8 @@ struct GemmArgs {
   // ldj share is -sum alpha, C = s_raw; with f8_cq also the e4m3 copy of u (delayed scale)
   int cf_pair;
   int cf_mode;
-  int desync;                  // persistent gemm256: s_sleep(127) rounds odd blocks wait up front
+  int desync;                  // persistent gemm256: s_sleep(127) rounds the delayed blocks wait up front
+  int desync_bit;              // block b is delayed iff (b >> desync_bit) & 1 (0: parity = XCD parity)
   int no_rot;                  // persistent gemm256: keep each block on one column (A/B knob)
   int no_edge;                 // persistent EPI_CPL_FWD: run edge tiles as full tiles (A/B knob)
 };

@@ -802,7 +802,7 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
   };
 
   if (ns <= 0) return;
-  if (a.desync && (b & 1))
+  if (a.desync && ((b >> a.desync_bit) & 1))
     for (int i = 0; i < a.desync; ++i) __builtin_amdgcn_s_sleep(127);
   int m0, n0;
   tile_org(0, m0, n0);
@@ -1058,7 +1058,12 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
       const char* e = getenv("VINF_G256_ROT");
       return e ? atoi(e) : 1;
     }();
+    static const int desync_bit_env = [] {
+      const char* e = getenv("VINF_G256_DESYNC_BIT");
+      return e ? atoi(e) : 0;
+    }();
     a.desync = desync_env;
+    a.desync_bit = desync_bit_env;
     a.no_rot = rot_env ? 0 : 1;
     static const int edge_env = [] {
       const char* e = getenv("VINF_G256_EDGE");

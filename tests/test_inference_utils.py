@@ -190,6 +190,31 @@ def test_train_cli_tasks(tmp_path):
     assert math.isfinite(out["nll"]) and out["precision"] == "fp32"
 
 
+def test_realnvp_preset_trains_the_bench_model(tmp_path):
+    """config3 (the DP headline preset) runs the bench's hyper-parameters (lr 1e-3, 100-step
+    warm-up, beta = 1, split pairing) through the CLI: F decreases, no step is skipped."""
+    from vi_normflows_amd.train import main
+
+    c = load("config3_realnvp32_dp8")
+    assert (c.lr, c.lr_warmup, c.schedule, c.pairing) == (1e-3, 100.0, "none", "split")
+    out = main(["--config", "config3_realnvp32_dp8", "device=cpu", "dim=64", "K=4", "hidden=64",
+                "batch=256", "iters=60", "log_every=10", "extra.graph=false",
+                f"out_dir={tmp_path}"])
+    rec = [json.loads(l) for l in
+           (tmp_path / "config3_realnvp32_dp8" / "metrics.jsonl").read_text().splitlines()]
+    F = [r["F"] for r in rec]
+    assert all(math.isfinite(f) for f in F)
+    assert F[-1] < F[0] - 1.0, F
+    assert out["skipped_steps"] == 0.0 and rec[-1]["skipped"] == 0.0
+
+
+def test_unknown_schedule_is_an_error():
+    with pytest.raises(ValueError, match="unknown schedule"):
+        load("config3_realnvp32_dp8", ["schedule=refrence"])
+    with pytest.raises(ValueError, match="pairing"):
+        load("config3_realnvp32_dp8", ["pairing=zigzag"])
+
+
 def test_get_data_cli(capsys):
     from vi_normflows_amd.get_data import main
 

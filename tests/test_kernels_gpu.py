@@ -216,10 +216,13 @@ def test_engine_gpu_fp32_matches_autograd(gpu):
 
     cfg = RealNVPConfig(dim=10, n_layers=3, hidden=16, target="banana", anneal="none",
                         init_out_std=0.3)
+    from vi_normflows_amd.ops import gemm
+
     eng = RealNVPVI(cfg, batch=9, device=gpu, compute_dtype=torch.float32, seed=5)
-    eng._update_schedule()
-    eng.forward()
-    eng.backward()
+    with gemm.oracle():   # fp32 conditioner products: the explicit torch reference path
+        eng._update_schedule()
+        eng.forward()
+        eng.backward()
     params = {n: v.detach().cpu().clone().requires_grad_(True)
               for n, v in eng.params.named_views().items()}
     F, _ = autograd_free_energy(eng, params, eng.eps0.cpu().clone(), 1.0)

@@ -30,4 +30,6 @@ SCHEDULES = {"reference": reference_schedule, "theano": theano_schedule,
 
 
 def get_schedule(name: str):
+    if name not in SCHEDULES:
+        raise ValueError(f"unknown beta schedule {name!r}; expected one of {sorted(SCHEDULES)}")
     return SCHEDULES[name]

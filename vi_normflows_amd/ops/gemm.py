@@ -7,37 +7,56 @@ nn.Linear convention):
 * ``linear_dgrad`` dx = (dy W) [* 1(h > 0)]              (fused ReLU-mask; fp32 accumulate option)
 * ``linear_wgrad`` dW = dy^T x (fp32), db = colsum(dy)   (fp32 outputs into the flat grad buffer)
 
-Backends (selected per call by :func:`set_backend` / ``VINF_GEMM``):
-``"mfma"`` - the hand-written gfx950 MFMA kernels in ``csrc/kernels/gemm.hip``
-(bf16 in, fp32 accumulate, fused epilogues); ``"blas"`` - hipBLASLt through
-``torch.mm`` for plain library GEMMs (used to A/B the MFMA kernels). CPU tensors
-always use torch in their own dtype.
+Routing (no silent fallback on the GPU):
+
+* GPU tensors run the hand-written gfx950 MFMA kernels (``csrc/kernels/gemm*.hip``, bf16 in,
+  fp32 accumulate, fused epilogues). A GPU operand that is not bf16 raises ``TypeError``.
+* CPU tensors (the CPU plumbing / test path) use torch in their own dtype.
+* ``with gemm.oracle():`` explicitly routes GPU calls to the torch composites, in any dtype
+  - the test oracle for the kernels and the hipBLASLt baseline of
+  ``vi_normflows_amd.bench.blas_baseline``. Nothing enters it implicitly.
 """
 from __future__ import annotations
 
-import os
+import contextlib
+import threading
 
 import torch
 
-_BACKEND = os.environ.get("VINF_GEMM", "mfma")
+_state = threading.local()
 
 
-def set_backend(name: str) -> None:
-    global _BACKEND
-    if name not in ("mfma", "blas"):
-        raise ValueError(name)
-    _BACKEND = name
+@contextlib.contextmanager
+def oracle():
+    """Run every GEMM entry point of this module through its torch composite (GPU included)
+    for the duration of the block: an explicit reference / baseline, never a fallback."""
+    prev = getattr(_state, "oracle", False)
+    _state.oracle = True
+    try:
+        yield
+    finally:
+        _state.oracle = prev
 
 
 def backend() -> str:
-    return _BACKEND
+    """``"oracle"`` inside :func:`oracle`, else ``"mfma"`` (GPU) - engines pick their fused
+    MFMA-only paths (coupling epilogues, deferred weight gradients) on ``"mfma"``."""
+    return "oracle" if getattr(_state, "oracle", False) else "mfma"
 
 
 def _mfma_ok(*ts) -> bool:
-    """The hand-written MFMA kernels take bf16 GPU operands; fp32 compute (tests, CPU) takes
-    the torch path."""
-    return _BACKEND == "mfma" and all(t is None or (t.is_cuda and t.dtype == torch.bfloat16)
-                                      for t in ts)
+    """True -> the MFMA kernels; False -> torch (CPU tensors, or inside :func:`oracle`).
+    A GPU operand outside the oracle must be bf16: anything else is a caller error."""
+    if getattr(_state, "oracle", False):
+        return False
+    cuda = [t for t in ts if t is not None and t.is_cuda]
+    if not cuda:
+        return False
+    bad = [t.dtype for t in cuda if t.dtype != torch.bfloat16]
+    if bad:
+        raise TypeError(f"GPU GEMM operands must be bf16 for the MFMA kernels (got {bad[0]}); "
+                        "use `with ops.gemm.oracle():` for an explicit torch reference")
+    return True
 
 
 def linear_fwd(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, out: torch.Tensor,
@@ -45,7 +64,7 @@ def linear_fwd(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, out: to
     """``mask_out`` (MFMA path, ReLU layers): also write the bitmask 1(out > 0) as uint8
     [M, N/8] (bit e of byte j <-> column 8j+e) for :func:`linear_dgrad`'s ``relu_bits`` -
     1/16 of the bytes of re-reading the bf16 activation in the backward. Ignored elsewhere."""
-    if _mfma_ok(x) and x.is_cuda:
+    if _mfma_ok(x, W):
         from ._ext import native
 
         native().gemm_nt(x, W, b, out, 1 if relu else 0, mask_out if relu else None)
@@ -67,7 +86,7 @@ def linear_dgrad(dy: torch.Tensor, W: torch.Tensor, out: torch.Tensor,
     ``relu_bits`` (MFMA path): the bitmask :func:`linear_fwd` wrote for ``relu_of``, read
     instead of the bf16 activation; the other paths use ``relu_of``. ``Wt`` (MFMA path, bf16
     output): a current copy of W^T, which runs the product as NT (both operands k-major)."""
-    if _mfma_ok(dy) and dy.is_cuda:
+    if _mfma_ok(dy, W):
         from ._ext import native
 
         if relu_bits is not None:
@@ -102,7 +121,7 @@ def linear_fwd_coupling(h: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None
     ``ldjp`` [ceil(Dh/128), B]: per-column-tile partial log-dets (the caller sums them; no
     atomics, bitwise reproducible). Elsewhere: torch, with the whole sum in ``ldjp[0]``."""
     Dh = x.shape[1]
-    if _mfma_ok(h) and h.is_cuda:
+    if _mfma_ok(h, W):
         from ._ext import native
 
         native().gemm_nt_cpl(h, W, b, st, x, y, ybf, ldjp, bool(ldj_init), float(scale))
@@ -138,7 +157,7 @@ def linear_dgrad_coupling(dy: torch.Tensor, W: torch.Tensor, G: torch.Tensor, s_
         gx = gy e^s
 
     Elsewhere: the two steps through torch (same math as ``ops.fused.coupling_bwd``)."""
-    if _mfma_ok(dy) and dy.is_cuda:
+    if _mfma_ok(dy, W):
         from ._ext import native
 
         native().gemm_nn_cpl(dy, W, G, s_hat, x, dst, gx, float(scale), float(c), Wt)
@@ -163,7 +182,7 @@ def linear_wgrad_group(items) -> None:
     :func:`linear_wgrad`.
     """
     items = list(items)
-    if items and all(_mfma_ok(dy) and dy.is_cuda for dy, _, _, _ in items):
+    if items and all(_mfma_ok(dy, x) for dy, x, _, _ in items):
         from ._ext import native
 
         for c in range(0, len(items), 4):
@@ -178,7 +197,7 @@ def linear_wgrad_group(items) -> None:
 def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dW: torch.Tensor,
                  db: torch.Tensor | None) -> None:
     """dW = dy^T x and db = sum_rows(dy), both written in dW/db's dtype (fp32)."""
-    if _mfma_ok(dy) and dy.is_cuda:
+    if _mfma_ok(dy, x):
         from ._ext import native
 
         native().gemm_tn(dy, x, dW, db)
@@ -206,7 +225,7 @@ class WgradPlan:
     launch). The caller picks ranges that are multiples of the CU count, so a RealNVP-32 step's
     1280 weight-gradient tiles run as 5 launches of exactly one tile per CU.
 
-    Off the MFMA path (CPU, fp32, blas backend) a problem is computed by :func:`linear_wgrad`
+    Off the MFMA path (CPU tensors, or inside :func:`oracle`) a problem is computed by :func:`linear_wgrad`
     when the range covering its LAST tile is run, so every problem is done exactly once.
     """
 
@@ -237,7 +256,7 @@ class WgradPlan:
         assert 0 <= tile0 and end <= self.total, (tile0, ntiles, self.total)
         first = bisect.bisect_right(self.starts, tile0) - 1
         last = bisect.bisect_left(self.starts, end) - 1        # problem holding tile end-1
-        if not all(_mfma_ok(it[0]) and it[0].is_cuda for it in self.items[first:last + 1]):
+        if not all(_mfma_ok(it[0], it[1]) for it in self.items[first:last + 1]):
             for p in range(first, last + 1):
                 if tile0 < self.starts[p + 1] <= end:
                     dy, x, dW, db, _, cm = self.items[p]

@@ -57,11 +57,15 @@ def run_realnvp(cfg, out, info, logger):
     from .utils.checkpoint import load_engine, save_engine
 
     dev = _device(cfg, info)
+    if cfg.schedule not in ("reference", "none"):
+        raise ValueError(f"realnvp_vi: schedule must be 'reference' or 'none', got {cfg.schedule!r}")
+    if cfg.pairing not in ("split", "interleaved"):
+        raise ValueError(f"realnvp_vi: pairing must be 'split' or 'interleaved', got {cfg.pairing!r}")
     rc = RealNVPConfig(dim=cfg.dim, n_layers=cfg.K, hidden=cfg.hidden, n_hidden=cfg.n_hidden,
-                       target=cfg.extra.get("target", "banana"), anneal=cfg.schedule
-                       if cfg.schedule in ("reference", "none") else "reference",
-                       anneal_iters=cfg.iters)
-    eng = RealNVPVI(rc, batch=cfg.batch, device=dev, seed=cfg.seed, rank=info.rank, lr=cfg.lr)
+                       target=cfg.extra.get("target", "banana"), anneal=cfg.schedule,
+                       anneal_iters=cfg.iters, banana_pairing=cfg.pairing)
+    eng = RealNVPVI(rc, batch=cfg.batch, device=dev, seed=cfg.seed, rank=info.rank, lr=cfg.lr,
+                    lr_warmup=cfg.lr_warmup, max_grad_norm=cfg.max_grad_norm)
     ckpt = out / "ckpt.pt"
     if cfg.extra.get("resume"):
         load_engine(eng, cfg.extra["resume"], info.rank)

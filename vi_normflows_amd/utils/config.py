@@ -41,6 +41,11 @@ class RunConfig:
     hidden: int = 64
     n_hidden: int = 2
     dim_z: int = 40
+    # optimizer / estimator knobs of the explicit-backward engines (realnvp_vi): linear lr ramp
+    # over the first steps, global-norm clip (0 = off), twisted-Gaussian target pairing
+    lr_warmup: float = 0.0
+    max_grad_norm: float = 0.0
+    pairing: str = "split"         # split: (z_i, z_{D/2+i}) | interleaved: (z_2i, z_2i+1)
     extra: dict = field(default_factory=dict)
 
     def override(self, items: list[str]) -> "RunConfig":
@@ -64,6 +69,18 @@ class RunConfig:
                 raise KeyError(f"unknown config key {k}")
         return c
 
+    def validate(self) -> "RunConfig":
+        """Reject values no task understands (a typo must not silently select a default)."""
+        from ..inference.annealing import SCHEDULES
+
+        if self.schedule not in SCHEDULES:
+            raise ValueError(f"unknown schedule {self.schedule!r}; expected one of {sorted(SCHEDULES)}")
+        if self.pairing not in ("split", "interleaved"):
+            raise ValueError(f"unknown pairing {self.pairing!r}; expected 'split' or 'interleaved'")
+        if self.lr_warmup < 0 or self.max_grad_norm < 0:
+            raise ValueError("lr_warmup and max_grad_norm must be >= 0")
+        return self
+
     def to_dict(self) -> dict:
         return asdict(self)
 
@@ -76,12 +93,17 @@ PRESETS: dict[str, RunConfig] = {
     "config1_two_moons_cpu": RunConfig(name="config1_two_moons_cpu", task="flow_vi", device="cpu",
                                        target="U1", flow="planar", K=16, dim=2, iters=10000,
                                        lr=1e-2, batch=256, optimizer="adam"),
+    # the RealNVP presets train exactly the model bench.py times: Adam lr 1e-3 with a 100-step
+    # linear warm-up (the first bias-corrected Adam step is a sign step on every parameter),
+    # beta = 1, target pairs straddling the coupling split. The reference annealing schedule
+    # with lr 1e-4 and no ramp diverged at step 1 on this model.
     "config2_realnvp8": RunConfig(name="config2_realnvp8", task="realnvp_vi", device="cuda",
-                                  K=8, dim=784, hidden=1024, batch=16384, iters=200, lr=1e-4,
-                                  schedule="reference"),
+                                  K=8, dim=784, hidden=1024, batch=65536, iters=200, lr=1e-3,
+                                  lr_warmup=100.0, schedule="none", pairing="split"),
     "config3_realnvp32_dp8": RunConfig(name="config3_realnvp32_dp8", task="realnvp_vi",
-                                       device="cuda", K=32, dim=784, hidden=1024, batch=32768,
-                                       iters=200, lr=1e-4, schedule="reference"),
+                                       device="cuda", K=32, dim=784, hidden=1024, batch=65536,
+                                       iters=200, lr=1e-3, lr_warmup=100.0, schedule="none",
+                                       pairing="split"),
     "config4_iaf10_vae": RunConfig(name="config4_iaf10_vae", task="iaf_vae", device="cuda", K=10,
                                    dim=3072, hidden=1024, dim_z=256, batch=1024, iters=200,
                                    lr=3e-4),
@@ -114,7 +136,7 @@ def load(spec: str | None, overrides: list[str] | None = None) -> RunConfig:
         cfg = base.override([f"{k}={json.dumps(v)}" for k, v in data.items()
                              if k != "extra"])
         cfg.extra.update(data.get("extra", {}))
-    return cfg.override(overrides or [])
+    return cfg.override(overrides or []).validate()
 
 
 def rank_seed(seed: int, rank: int) -> int:
