@@ -148,6 +148,12 @@ def main() -> int:
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     dt = vdist.all_reduce_max(dt)
+    # replica check (outside the timed region): every rank's fp32 master weights against rank
+    # 0's after the timed steps. A mis-ordered or dropped collective (e.g. in a captured graph)
+    # leaves diverged replicas, whose step time must not be reported as a result.
+    max_diff = _replica_max_diff(eng.params.master, world)
+    identical = max_diff == 0.0
+    buckets = runner.reducer.describe() if runner.reducer is not None else []
     loss = float(eng.loss.item())
     steps_done = int(eng.step_t.item())
     ms = 1000.0 * dt / a.steps
@@ -192,12 +198,33 @@ def main() -> int:
                 "cpu_anchor_note": "BASELINE.md measured-here reference NumPy planar VAE "
                                    "forward-only 17.8k samples/s (different workload; "
                                    "no published number for this metric)",
+                "replicas_identical": identical,
+                "max_replica_diff": max_diff,
+                "allreduce_buckets": {"count": len(buckets),
+                                      "mb": [round(b["mb"], 2) for b in buckets]},
             },
         }
         out_f.write(json.dumps(out) + "\n")
         out_f.flush()
     vdist.shutdown()
+    if not identical:
+        sys.stderr.write(f"bench.py: replicas diverged (max |master - master_rank0| = {max_diff})\n")
+        return 3
     return 0
+
+
+def _replica_max_diff(master, world: int) -> float:
+    """max over ranks of max |master - rank 0's master| (0.0 at world size 1)."""
+    if world == 1:
+        return 0.0
+    import torch
+    import torch.distributed as dist
+
+    ref = master.clone()
+    dist.broadcast(ref, 0)
+    d = (master - ref).abs().max().reshape(1).double()
+    dist.all_reduce(d, op=dist.ReduceOp.MAX)
+    return float(d.item())
 
 
 if __name__ == "__main__":

@@ -8,6 +8,14 @@
 namespace {
 
 constexpr int kH = 64;
+constexpr long kMaxLds = 163840;   // what nf_launch_vae_step grants the rows kernel
+
+// LDS bytes the rows kernel needs for (Din, dz, K): the engine gate (train.py, PlanarVAEEngine)
+// and vae_step's own check use the same number
+int64_t vae_rows_lds_bytes(int64_t Din, int64_t dz, int64_t K) {
+  const long De = 2 * dz + 2 * dz * K + K;
+  return (int64_t)nf_vae_rows_lds_bytes((int)Din, (int)dz, (int)K, (int)De);
+}
 
 void f32(const at::Tensor& t, const char* n) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), n,
@@ -31,6 +39,10 @@ void vae_step(const at::Tensor& master, const at::Tensor& grad, at::IntArrayRef 
   TORCH_CHECK((long)offs.size() == 4 * L + 4, "vae_step: 4 L + 4 parameter offsets");
   TORCH_CHECK(master.numel() == grad.numel(), "master / grad layouts differ");
   const long De = 2 * dz + 2 * dz * K + K;
+  const long ldg = (De + 3) & ~3L;   // gphi rows padded to 16 B (float4 loads of the wgrad phase)
+  TORCH_CHECK(nf_vae_rows_lds_bytes((int)Din, (int)dz, (int)K, (int)De) <= kMaxLds,
+              "vae_step: Din / dz / K need more than 160 KiB of LDS per row block "
+              "(vinf::vae_rows_lds_bytes); use the module path");
   TORCH_CHECK(x.dim() == 2 && x.size(0) == B && x.size(1) == Din, "x must be [B, Din]");
   // parameter extents (out x in + out) for a bounds check of every offset
   std::vector<long> numel;
@@ -43,7 +55,7 @@ void vae_step(const at::Tensor& master, const at::Tensor& grad, at::IntArrayRef 
   for (size_t i = 0; i < numel.size(); ++i)
     TORCH_CHECK(offs[i] >= 0 && offs[i] % 4 == 0 && offs[i] + numel[i] <= master.numel(),
                 "vae_step: parameter offset out of range / not 16-B aligned");
-  const long need = 4L * L * B * kH + B * De + B * dz + B * Din;
+  const long need = 4L * L * B * kH + B * ldg + B * dz + B * Din;
   TORCH_CHECK(ws.numel() >= need, "vae_step: workspace too small");
   TORCH_CHECK(frow.numel() >= B && loss.numel() >= 1, "frow / loss");
   const float* eps_p = nullptr;
@@ -83,7 +95,7 @@ void vae_step(const at::Tensor& master, const at::Tensor& grad, at::IntArrayRef 
   float* egrad = w;           w += L * BH;
   float* dact = w;            w += L * BH;
   float* dgrad = w;           w += L * BH;
-  float* gphi = w;            w += B * De;
+  float* gphi = w;            w += B * ldg;
   float* zk = w;              w += B * dz;
   float* dl = w;
   nf_launch_vae_step(prm, x.data_ptr<float>(), eps_p, (unsigned)seed, offset.data_ptr<int64_t>(),
@@ -96,6 +108,7 @@ void vae_step(const at::Tensor& master, const at::Tensor& grad, at::IntArrayRef 
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(vinf, m) {
+  m.def("vae_rows_lds_bytes(int Din, int dz, int K) -> int", &vae_rows_lds_bytes);
   m.def("vae_step(Tensor master, Tensor(a!) grad, int[] offs, Tensor x, Tensor? eps, int seed, "
         "Tensor offset, Tensor beta, int B, int Din, int dz, int K, int L, Tensor(b!) ws, "
         "Tensor(c!) frow, Tensor(d!) loss, Tensor(e!)? zk_out, Tensor(f!)? ldj_out) -> ()");

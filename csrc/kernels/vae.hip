@@ -210,11 +210,13 @@ __device__ __forceinline__ void store_rows(const float* src, int ld, int n, floa
   }
 }
 // transposed [n][R] LDS block -> global rows [row0 + r][n]
+// src [n][R] (LDS, transposed) -> rows row0.. of dst with row pitch ld (>= n)
 __device__ __forceinline__ void store_rows_t(const float* src, int n, float* dst, long row0,
-                                             int nrows) {
+                                             int nrows, int ld = 0) {
+  if (ld <= 0) ld = n;
   for (int t = threadIdx.x; t < R * n; t += NT) {
     const int r = t / n, c = t % n;
-    if (r < nrows) dst[(row0 + r) * n + c] = src[c * R + r];
+    if (r < nrows) dst[(row0 + r) * ld + c] = src[c * R + r];
   }
 }
 
@@ -400,7 +402,7 @@ __global__ void __launch_bounds__(NT, 1) vae_rows_kernel(RowsArgs a) {
     for (int j = lane; j < De; j += 64) gph[j * R + r] = 0.f;
   }
   __syncthreads();
-  store_rows_t(gph, De, a.gphi, row0, nrows);
+  store_rows_t(gph, De, a.gphi, row0, nrows, (De + 3) & ~3);   // 16-B aligned rows
   for (int l = 0; l < L; ++l) store_rows(ea + l * R * H, H, H, a.eact + (long)l * a.B * H, row0, nrows);
   // ---- encoder input-gradient chain (down to the first hidden layer's pre-activation)
   gin = gph;
@@ -417,11 +419,11 @@ __global__ void __launch_bounds__(NT, 1) vae_rows_kernel(RowsArgs a) {
 // ------------------------------------------------------------------ phase 2: weight gradients
 constexpr int MAXP = 12;
 struct WgProb {
-  const float* dY;   // [B][O]
+  const float* dY;   // [B][ldy], ldy = O rounded up to a multiple of 4 (16-B aligned float4 rows)
   const float* X;    // [B][I]
   float* dW;         // [O][I]
   float* db;         // [O]
-  int O, I, tiles_i, tile0;
+  int O, I, tiles_i, tile0, ldy;
 };
 struct WgArgs {
   WgProb p[MAXP];
@@ -455,7 +457,7 @@ __global__ void __launch_bounds__(256) vae_wgrad_kernel(WgArgs a) {
     for (int t = tid; t < WB * 16; t += 256) {
       const int bb = t / 16, c4 = (t % 16) * 4, bi = b0 + bb;
       float4 y = make_float4(0.f, 0.f, 0.f, 0.f), xv = y;
-      if (bi < a.B && o0 + c4 < pb.O) y = *reinterpret_cast<const float4*>(pb.dY + (long)bi * pb.O + o0 + c4);
+      if (bi < a.B && o0 + c4 < pb.O) y = *reinterpret_cast<const float4*>(pb.dY + (long)bi * pb.ldy + o0 + c4);
       if (bi < a.B && i0 + c4 < pb.I) xv = *reinterpret_cast<const float4*>(pb.X + (long)bi * pb.I + i0 + c4);
       *reinterpret_cast<float4*>(sy + bb * 68 + c4) = y;
       *reinterpret_cast<float4*>(sx + bb * 68 + c4) = xv;
@@ -552,7 +554,7 @@ void nf_launch_vae_step(const NfVaeParams& prm, const float* x, const float* eps
   int tiles = 0;
   auto add = [&](const float* dY, const float* X, float* dW, float* db, int O, int I) {
     WgProb& q = w.p[w.np++];
-    q.dY = dY; q.X = X; q.dW = dW; q.db = db; q.O = O; q.I = I;
+    q.dY = dY; q.X = X; q.dW = dW; q.db = db; q.O = O; q.I = I; q.ldy = (O + 3) & ~3;
     q.tiles_i = (I + 63) / 64;
     q.tile0 = tiles;
     tiles += ((O + 63) / 64) * q.tiles_i;

@@ -66,6 +66,9 @@ def test_bench_torchrun_two_ranks_cpu():
     recs = _json_lines(r.stdout)
     assert len(recs) == 1, r.stdout      # rank 0 only
     _check(recs[0], 2)
+    notes = recs[0]["notes"]
+    assert notes["replicas_identical"] is True and notes["max_replica_diff"] == 0.0
+    assert notes["allreduce_buckets"]["count"] >= 1
 
 
 def test_bench_self_launch_two_ranks_cpu():
@@ -76,6 +79,7 @@ def test_bench_self_launch_two_ranks_cpu():
     recs = _json_lines(r.stdout)
     assert len(recs) == 1, r.stdout
     _check(recs[0], 2)
+    assert recs[0]["notes"]["replicas_identical"] is True
 
 
 def test_bench_gpus_world_mismatch_is_an_error():
@@ -91,4 +95,7 @@ def test_bench_force_reduce_cpu():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--force-reduce", *SMALL],
                        cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
-    _check(_json_lines(r.stdout)[0], 1)
+    rec = _json_lines(r.stdout)[0]
+    _check(rec, 1)
+    assert rec["notes"]["replicas_identical"] is True
+    assert rec["notes"]["allreduce_buckets"]["count"] >= 1

@@ -191,3 +191,51 @@ def test_trainer_dp_broadcast_hooks_equal_single_process(tmp_path, nan_rank):
     tr.fit(3)
     for a, b in zip(r[0]["params"], model.parameters()):
         assert torch.allclose(a, b.detach(), atol=1e-6, rtol=1e-5)
+
+
+def _mixed_worker(rank, world, port, X, Y, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from vi_normflows_amd.inference.elbo import FreeEnergy
+    from vi_normflows_amd.inference.trainer import TrainConfig, Trainer
+
+    model = _mlp(1000 + rank)
+    scale = torch.nn.Parameter(torch.ones(3, dtype=torch.float64))   # mixed dtypes: no flat buffer
+    n = X.shape[0] // world
+    xs, ys = X[rank * n:(rank + 1) * n], Y[rank * n:(rank + 1) * n]
+
+    def loss_fn(t, beta):
+        return FreeEnergy(((model(xs) * scale.float() - ys) ** 2).mean(), {})
+
+    tr = Trainer(list(model.parameters()) + [scale], loss_fn,
+                 TrainConfig(iters=3, lr=0.05, optimizer="sgd", log_every=1))
+    assert tr.flat is None          # the legacy path under test
+    tr.fit(3)
+    torch.save({"params": [p.detach().clone() for p in model.parameters()] + [scale.detach().clone()]},
+               os.path.join(out_dir, f"m{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_trainer_dp_mixed_dtypes_averages_gradients(tmp_path):
+    """the per-tensor (mixed dtype) path all-reduces and averages the gradients, so
+    replicas stay identical and match one process on the concatenated batch."""
+    from vi_normflows_amd.inference.elbo import FreeEnergy
+    from vi_normflows_amd.inference.trainer import TrainConfig, Trainer
+
+    world = 2
+    torch.manual_seed(4)
+    X, Y = torch.randn(8, 5), torch.randn(8, 3)
+    mp.spawn(_mixed_worker, args=(world, _free_port(), X, Y, str(tmp_path)), nprocs=world, join=True)
+    r = [torch.load(tmp_path / f"m{k}.pt", weights_only=True) for k in range(world)]
+    for a, b in zip(r[0]["params"], r[1]["params"]):
+        assert torch.equal(a, b)
+    model = _mlp(1000)
+    scale = torch.nn.Parameter(torch.ones(3, dtype=torch.float64))
+
+    def loss_fn(t, beta):
+        return FreeEnergy(((model(X) * scale.float() - Y) ** 2).mean(), {})
+
+    Trainer(list(model.parameters()) + [scale], loss_fn,
+            TrainConfig(iters=3, lr=0.05, optimizer="sgd")).fit(3)
+    for a, b in zip(r[0]["params"], list(model.parameters()) + [scale]):
+        assert torch.allclose(a, b.detach().to(a.dtype), atol=1e-6, rtol=1e-5)

@@ -155,6 +155,24 @@ def test_train_cli_iaf_uses_engine(gpu, tmp_path):
     assert (tmp_path / "iaf_eng" / "ckpt.pt").exists()
 
 
+@pytest.mark.gpu
+def test_train_cli_annealed_iaf_uses_engine(gpu, tmp_path):
+    """An annealed config-4 run (reference beta_t) takes the engine path, and the logged beta
+    follows optimization.py:71-72 from t = 0 (the capture warm-up is rolled back)."""
+    import json
+
+    from vi_normflows_amd.inference.annealing import reference_schedule
+    from vi_normflows_amd.train import main
+
+    final = main(["--config", "config4_iaf10_vae", "iters=40", "log_every=10", "batch=1024",
+                  "schedule=reference", f"out_dir={tmp_path}", "name=iaf_ann",
+                  "extra.n_data=2048"])
+    assert final["engine"] == "iaf_engine" and math.isfinite(final["free_energy"])
+    rec = [json.loads(l) for l in (tmp_path / "iaf_ann" / "metrics.jsonl").read_text().splitlines()]
+    for r in rec:
+        assert abs(r["beta"] - reference_schedule(r["step"], 40)) < 1e-5, r
+
+
 def _dp_worker(rank, world, port, data, eps_all, out_dir, B):
     import os
 
@@ -268,3 +286,24 @@ def test_iaf_engine_bf16_vs_fp32_oracle(gpu):
     print(f"[iaf engine] bf16 vs fp32 oracle: loss rel {rel_loss:.2e}, worst grad rel {worst:.2e} ({which})")
     assert rel_loss <= 1e-4
     assert worst <= 4e-2, (which, worst)
+
+
+@pytest.mark.parametrize("anneal", ["reference", "theano"])
+def test_engine_device_beta_schedule_matches_reference_formulas(anneal):
+    """beta_t of the IAF engine follows optimization.py:71-72 / theano_implement.py:169-175
+    step by step (device scalars), and the objective it reports uses it."""
+    from vi_normflows_amd.inference.annealing import reference_schedule, theano_schedule
+    from vi_normflows_amd.models.iaf_engine import IAFEngine
+    from vi_normflows_amd.models.iaf_vae import IAFVAEConfig, synthetic_images
+
+    cfg = IAFVAEConfig(image_shape=(1, 8, 8), dim_z=8, hidden=32, n_flows=2, made_hidden=32,
+                       context=16)
+    B, iters = 16, 40
+    data = synthetic_images(2 * B, cfg.image_shape, seed=0).reshape(2 * B, -1)
+    eng = IAFEngine(cfg, B, data, device="cpu", seed=0, anneal=anneal, anneal_iters=iters)
+    f = (lambda t: reference_schedule(t, iters)) if anneal == "reference" else theano_schedule
+    for t in range(6):
+        eng.train_step()
+        assert abs(eng.beta_t.item() - f(t)) < 1e-6, (t, eng.beta_t.item(), f(t))
+        assert abs(eng._lik_coef.item() + f(t) / B) < 1e-7
+    assert math.isfinite(eng.loss.item())

@@ -38,19 +38,36 @@ def test_engine_trains_cpu():
     assert losses[-1] < losses[0] - 10.0, losses
 
 
+def _largest_k(dz):
+    """Largest K the HIP step accepts at dz (the rows kernel's LDS image <= 160 KiB)."""
+    for K in range(8, -1, -1):
+        if PlanarVAEEngine.supported(VAEConfig(dim_x=784, dim_z=dz, K=K, width=64, hidden_layers=3)):
+            return K
+    return None
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("B", [128, 100])
-def test_vae_step_matches_autograd(gpu, B):
+@pytest.mark.parametrize("B,dz,K", [(128, 40, 4), (100, 40, 4),
+                                    # K = 3: De = 2 dz (K + 1) + K = 323 is not a multiple of 4
+                                    # (the gphi rows are padded to 16 B for the float4 loads)
+                                    (96, 40, 3),
+                                    # the largest dz with the largest K its LDS image allows
+                                    (64, 64, None)])
+def test_vae_step_matches_autograd(gpu, B, dz, K):
     """fp32 HIP step vs autograd on the same device: same eps, same parameters."""
-    cfg = _cfg()
+    if K is None:
+        K = _largest_k(dz)
+        assert K is not None and K >= 1
+    cfg = VAEConfig(dim_x=784, dim_z=dz, K=K, width=64, hidden_layers=3)
+    assert PlanarVAEEngine.supported(cfg)
     eng = PlanarVAEEngine(cfg, batch=B, device=gpu, seed=1)
     g = torch.Generator().manual_seed(2)
     with torch.no_grad():   # larger weights than the 0.05 init so every path is exercised
         eng.params.master.mul_(4.0)
     eng.set_batch(synthetic_binary_images(B, 784, seed=1).to(gpu))
-    eng.eps_override = torch.randn(B, 40, generator=g).to(gpu)
+    eng.eps_override = torch.randn(B, dz, generator=g).to(gpu)
     eng.beta.fill_(0.7)
-    eng.zk_out = torch.zeros(B, 40, device=gpu)
+    eng.zk_out = torch.zeros(B, dz, device=gpu)
     eng.ldj_out = torch.zeros(B, device=gpu)
     eng.forward_backward()
     torch.cuda.synchronize()
@@ -68,6 +85,67 @@ def test_vae_step_matches_autograd(gpu, B):
         a, r = eng.layout.view(got["grad"], name), eng.layout.view(ref["grad"], name)
         err = (a - r).abs().max().item()
         assert err <= 2e-4 * r.abs().max().item() + 1e-6, (name, err, r.abs().max().item())
+
+
+def test_engine_gate_rejects_oversized_lds():
+    """dz = 64, K = 8 needs ~184 KB of LDS per row block: not supported (module path), and
+    vinf::vae_step itself refuses it instead of failing to launch."""
+    try:
+        from vi_normflows_amd.ops._ext import native
+
+        lds = int(native().vae_rows_lds_bytes(784, 64, 8))
+    except Exception:
+        pytest.skip("native library not loadable here")
+    assert lds > 163840
+    assert not PlanarVAEEngine.supported(VAEConfig(dim_x=784, dim_z=64, K=8, width=64,
+                                                   hidden_layers=3))
+    assert PlanarVAEEngine.supported(_cfg())
+
+
+@pytest.mark.gpu
+def test_vae_step_refuses_oversized_lds(gpu):
+    cfg = VAEConfig(dim_x=784, dim_z=64, K=8, width=64, hidden_layers=3)
+    eng = PlanarVAEEngine(cfg, batch=16, device=gpu, seed=0)
+    eng.set_batch(synthetic_binary_images(16, 784, seed=0).to(gpu))
+    with pytest.raises(RuntimeError, match="LDS"):
+        eng.forward_backward()
+
+
+def _dp_worker(rank, world, port, out_dir):
+    import json
+    import os
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from vi_normflows_amd.train import main
+
+    final = main(["--config", "mnist_planar_vae", "device=cpu", "iters=8", "log_every=4",
+                  "batch=16", "dim_z=4", "K=2", "extra.n_data=64", 'extra.engine="force"',
+                  "extra.recon_every=0", f"out_dir={out_dir}", "name=dp"])
+    with open(os.path.join(out_dir, f"final{rank}.json"), "w") as f:
+        json.dump(final, f)
+
+
+def test_planar_vae_engine_data_parallel_gloo(tmp_path):
+    """Config 0 (the reference's main workload) on the ENGINE path with 2 gloo ranks: rank 0's
+    weights are broadcast, the step's gradients go through the runner's bucketed all-reduce,
+    and both replicas end bitwise identical."""
+    import json
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_dp_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    f = [json.loads((tmp_path / f"final{r}.json").read_text()) for r in range(2)]
+    assert f[0]["engine"] == f[1]["engine"] == "vae_engine"
+    assert f[0]["param_checksum"] == f[1]["param_checksum"]
+    assert f[0]["skipped_steps"] == 0.0 and math.isfinite(f[0]["free_energy_per_sample"])
+    rec = [json.loads(l) for l in (tmp_path / "dp" / "metrics.jsonl").read_text().splitlines()]
+    assert rec and "grad_norm" in rec[-1] and "skipped" in rec[-1]
 
 
 @pytest.mark.gpu

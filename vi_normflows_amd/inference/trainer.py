@@ -145,7 +145,28 @@ class Trainer:
         self.flat.mul_(self._gscale.to(self.flat.dtype))
         return True
 
+    def _allreduce_grads_legacy(self) -> None:
+        """Mixed dtypes / devices (no flat buffer): one coalesced all-reduce per dtype/device
+        group of the gradients, then the 1/world average - every rank steps on the same mean
+        gradient (without it the replicas would drift apart)."""
+        groups: dict = {}
+        for p in self.params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)   # a parameter without a gradient contributes 0
+            groups.setdefault((p.grad.dtype, p.grad.device), []).append(p.grad)
+        for grads in groups.values():
+            flat = torch.cat([g.reshape(-1) for g in grads])
+            dist.all_reduce(flat)
+            flat.mul_(1.0 / self.world)
+            off = 0
+            for g in grads:
+                n = g.numel()
+                g.copy_(flat[off:off + n].view_as(g))
+                off += n
+
     def _grads_finite_legacy(self, loss) -> bool:
+        if self.world > 1:
+            self._allreduce_grads_legacy()
         tot = torch.zeros((), dtype=torch.float64, device=loss.device)
         tot = tot + loss.detach().double() * 0.0
         for p in self.params:

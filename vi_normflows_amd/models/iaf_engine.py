@@ -39,19 +39,26 @@ LOG2PI = math.log(2 * math.pi)
 
 class IAFEngine:
     """Explicit-backward IAF VAE step on flat buffers. ``data``: fp32 [n_batches * B, dim_x]
-    binary images held on the device; step t trains on batch t mod n_batches. The objective
-    uses a fixed ``beta`` (config 4's ELBO); the annealed schedules run on the module path
-    (``train.py`` picks the engine only for ``schedule=none`` with Adam)."""
+    binary images held on the device; step t trains on batch t mod n_batches.
+
+    ``anneal``: ``"none"`` (fixed ``beta``, config 4's ELBO), ``"reference"``
+    (beta_t = min(1, 0.001 + t / min(max_iter / 4, 1e4)), normflows/optimization.py:71-72) or
+    ``"theano"`` (beta_t = min(1, 0.01 + t / 1e4), theano_implement.py:169-175). beta_t and the
+    two coefficients it scales (likelihood-logit gradient, prior gradient) are device scalars
+    updated inside the captured step, so an annealed run replays one hipGraph."""
 
     def __init__(self, cfg: IAFVAEConfig, batch: int, data: torch.Tensor, device="cuda",
                  seed: int = 0, rank: int = 0, lr: float = 3e-4, betas=(0.9, 0.999),
                  eps: float = 1e-8, beta: float = 1.0, max_grad_norm: float = 0.0,
-                 model: IAFVAE | None = None):
+                 model: IAFVAE | None = None, anneal: str = "none", anneal_iters: int = 10000):
         self.cfg, self.B = cfg, int(batch)
         self.device = torch.device(device)
         self.cdt = torch.bfloat16 if self.device.type == "cuda" else torch.float32
         self.seed, self.rank = int(seed), int(rank)
         self.lr, self.betas, self.eps, self.beta = lr, betas, eps, float(beta)
+        if anneal not in ("none", "reference", "theano"):
+            raise ValueError(f"IAFEngine anneal must be none | reference | theano, got {anneal!r}")
+        self.anneal, self.anneal_iters = anneal, int(anneal_iters)
         self.max_grad_norm = float(max_grad_norm)
         self.grad_scale_host = 1.0
         self.unit_ready_hook = None
@@ -96,6 +103,11 @@ class IAFEngine:
         e = lambda *s, dt=cdt: torch.empty(*s, dtype=dt, device=dev)  # noqa: E731
         self.step_t = torch.zeros((), dtype=f32, device=dev)
         self.rng_offset = torch.zeros((), dtype=torch.int64, device=dev)
+        # beta_t and the coefficients it scales: dF/dlogits = lik_coef (x - sigmoid) with
+        # lik_coef = -beta_t / B, the prior term's dF/dz_K = prior_coef z_K with beta_t / B
+        self.beta_t = torch.full((), self.beta, dtype=f32, device=dev)
+        self._lik_coef = torch.full((), -self.beta / self.B, dtype=f32, device=dev)
+        self._prior_coef = torch.full((), self.beta / self.B, dtype=f32, device=dev)
         self.loss = torch.zeros((), dtype=f32, device=dev)
         self.gnorm2 = torch.zeros((), dtype=f32, device=dev)
         self.skip = torch.zeros((), dtype=f32, device=dev)
@@ -287,9 +299,9 @@ class IAFEngine:
             h = out
         # log p(x|z) and its logit gradient in one pass: dF/dlogits = -(beta/B)(x - sigmoid)
         fused.bernoulli_logits(self.logits, self.xf, dlogits=self.dlogits,
-                               coef_host=-self.beta / B, logpx=self.logpx)
+                               coef=self._lik_coef, logpx=self.logpx)
         lp = self.logpx - 0.5 * dz * LOG2PI - 0.5 * (zK * zK).sum(1)
-        F = self.lq - self.ldjk.sum(0) - self.beta * lp
+        F = self.lq - self.ldjk.sum(0) - self.beta_t * lp
         torch.mean(F, 0, out=self.loss)
 
     def _hook(self, unit):
@@ -309,7 +321,7 @@ class IAFEngine:
             (self.dD[0], self.zKb, P.g("dec.W0"), P.g("dec.b0"))])
         cur = self.DX
         # dF/dz_K: prior term (beta/B) z_K plus the decoder path; context-gradient sum = 0
-        torch.mul(self.Z[K], self.beta / B, out=cur[:, :dz])
+        torch.mul(self.Z[K], self._prior_coef, out=cur[:, :dz])
         cur[:, dz:].zero_()
         gemm.linear_dgrad(self.dD[0], P.c("dec.W0"), cur[:, :dz], accumulate=True)
         self._hook(K + 1)
@@ -353,11 +365,33 @@ class IAFEngine:
                              gscale=self.gscale, skip=self.skip)
         self.n_skipped.add_(self.skip)
 
-    def train_step(self, reduce_fn=None):
+    def _update_schedule(self):
+        """Device-side step / beta_t update (captured into the step graph)."""
         self.step_t.add_(1.0)      # Adam's bias correction reads the 1-based step
         self.rng_offset.add_(1)
+        if self.anneal == "none":
+            return
+        if self.anneal == "reference":   # optimization.py:71-72, t = step - 1
+            cool, start = min(self.anneal_iters / 4.0, 1e4), 0.001
+        else:                            # theano_implement.py:169-175
+            cool, start = 1e4, 0.01
+        torch.clamp((self.step_t - 1.0) * (1.0 / cool) + start, max=1.0, out=self.beta_t)
+        torch.mul(self.beta_t, -1.0 / self.B, out=self._lik_coef)
+        torch.mul(self.beta_t, 1.0 / self.B, out=self._prior_coef)
+
+    def train_step(self, reduce_fn=None):
+        self._update_schedule()
+        fwd_persist = self.persist_forward_only and self.device.type == "cuda"
+        if fwd_persist:
+            # DP runner policy (parallel/runner.py): the persistent GEMM grid in the forward
+            # only - no collective is in flight there; the previous setting is restored
+            from ..ops._ext import native
+
+            prev = native().gemm_persist(1)
         with trace_range("iaf_forward"):
             self.forward()
+        if fwd_persist:
+            native().gemm_persist(prev)
         with trace_range("iaf_backward"):
             self.backward()
         if reduce_fn is not None:

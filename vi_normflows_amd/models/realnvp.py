@@ -586,11 +586,11 @@ class RealNVPVI:
             # DP: no collective is in flight during the forward (the optimizer waited for every
             # bucket), so the one-block-per-CU persistent grid is safe there; the backward,
             # where RCCL all-reduces hold CUs beside the GEMMs, launches one block per tile
-            _ext_native().gemm_persist(1)
+            prev = _ext_native().gemm_persist(1)
         with trace_range("flow_forward+elbo"):
             self.forward()
         if fwd_persist:
-            _ext_native().gemm_persist(0)
+            _ext_native().gemm_persist(prev)
         with trace_range("flow_backward"):
             self.backward()
         if reduce_fn is not None:

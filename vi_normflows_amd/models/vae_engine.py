@@ -81,7 +81,14 @@ class PlanarVAEEngine:
         self.skip = torch.zeros((), device=dev)
         self.gscale = torch.ones((), device=dev)
         self._partials = torch.zeros(512, device=dev)
-        self.ws = torch.zeros(4 * L * self.B * _H + self.B * (self.De + dz + Din), device=dev)
+        self.n_skipped = torch.zeros((), device=dev)
+        # DP runner contract (parallel/runner.py): the step's gradients are final after the one
+        # vae_step launch pair, so every unit is handed to the bucketed all-reduce at once;
+        # grad_scale_host folds the 1/world average into the optimizer's gradient multiplier
+        self.unit_ready_hook = None
+        self.grad_scale_host = 1.0
+        ldg = (self.De + 3) // 4 * 4   # gphi rows padded to 16 B (vae.hip wgrad float4 loads)
+        self.ws = torch.zeros(4 * L * self.B * _H + self.B * (ldg + dz + Din), device=dev)
         self.eps_override = None
         self.zk_out = self.ldj_out = None
         g = torch.Generator().manual_seed(int(seed))
@@ -168,18 +175,43 @@ class PlanarVAEEngine:
             for n, t in self._module_pairs(model):
                 self.params.g(n).copy_(t.grad)
 
+    @staticmethod
+    def supported(cfg: VAEConfig) -> bool:
+        """Whether the HIP step takes this configuration (the same limits ``vinf::vae_step``
+        checks): width 64, 1-4 hidden layers, dz <= 64 (multiple of 4), K <= 8, Din <= 1024
+        (multiple of 4), paper flow / encoder layout, and the rows kernel's LDS image within
+        160 KiB (vinf::vae_rows_lds_bytes)."""
+        if cfg.flow_variant != "paper" or cfg.encode_layout != "paper" or cfg.width != _H:
+            return False
+        dz, K, L, Din = cfg.dim_z, cfg.K, cfg.hidden_layers, cfg.dim_x
+        if not (1 <= L <= 4 and 1 <= dz <= 64 and dz % 4 == 0 and 0 <= K <= 8
+                and Din % 4 == 0 and 4 <= Din <= 1024):
+            return False
+        try:
+            from ..ops._ext import native
+
+            return int(native().vae_rows_lds_bytes(Din, dz, K)) <= 163840
+        except Exception:   # no native library on this machine: the engine cannot run anyway
+            return False
+
     def optimizer_step(self):
         P = self.params
         fused.sumsq_guard(P.grad, self._partials, out_sumsq=self.gnorm2, skip=self.skip,
-                          scale=self.gscale, max_norm=0.0, base_scale=1.0)
+                          scale=self.gscale, max_norm=0.0, base_scale=self.grad_scale_host)
         b1, b2 = self.betas
         fused.flat_optimizer(fused.OPT_ADAM, P.master, P.grad, P.m, P.v, pbf=None, lr=self.lr,
                              b1=b1, b2=b2, eps=self.eps, wd=0.0, step=self.step_t,
                              gscale=self.gscale, skip=self.skip)
+        self.n_skipped.add_(self.skip)
 
-    def train_step(self):
+    def train_step(self, reduce_fn=None):
         self._update_schedule()
         self.forward_backward()
+        if self.unit_ready_hook is not None:
+            for u in range(len(self.layout.unit_ranges) - 1, -1, -1):
+                self.unit_ready_hook(u)
+        if reduce_fn is not None:
+            reduce_fn()
         self.optimizer_step()
 
     def capture(self, warmup: int = 2):

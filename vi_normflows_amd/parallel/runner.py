@@ -55,6 +55,7 @@ class DataParallelRunner:
         if force and info.world == 1 and not dist.is_initialized():
             _init_single_rank_group(info)
         persist = os.environ.get("VINF_DP_PERSIST", "fwd")   # "1" all | "0" none | "fwd"
+        self._persist_prev = None     # process-global GEMM switch, restored by close()
         if (info.world > 1 or force) and engine.device.type == "cuda" and persist != "1":
             # multi-rank: RCCL kernels run on CUs beside the backward's GEMMs; a persistent GEMM
             # grid (one block per CU, each owning a fixed tile list) would wait for every CU an
@@ -63,7 +64,7 @@ class DataParallelRunner:
             # grid there (``persist_forward_only``).
             from ..ops._ext import native
 
-            native().gemm_persist(0)
+            self._persist_prev = int(native().gemm_persist(0))
             if persist == "fwd" and hasattr(engine, "persist_forward_only"):
                 engine.persist_forward_only = True
         if info.world > 1 or (force and dist.is_initialized()):
@@ -105,14 +106,42 @@ class DataParallelRunner:
             fn = (lambda: faults.maybe_inject(self._t - 1, self.info.rank, grad)) if poison else None
             self.engine.train_step(reduce_fn=fn)
 
+    def close(self) -> None:
+        """Restore the process-global persistent-GEMM switch this runner changed."""
+        if self._persist_prev is not None:
+            from ..ops._ext import native
+
+            native().gemm_persist(self._persist_prev)
+            self._persist_prev = None
+        if hasattr(self.engine, "persist_forward_only"):
+            self.engine.persist_forward_only = False
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
     def capture(self, warmup: int = 2) -> bool:
-        """Capture one training step into a hipGraph. Returns False if capture is unsupported."""
+        """Capture one training step into a hipGraph. Returns False if capture is unsupported
+        or not enabled for this job.
+
+        Collectives inside the graph: a 1-rank RCCL communicator (``force_reduce``) is captured
+        by default (tested: tests/test_distributed_gpu.py). A multi-rank job replays eager steps
+        unless ``VINF_GRAPH_COLLECTIVES=1`` opts in (eager costs ~0.1 ms of a ~37 ms step,
+        profiles/r2_graph_vs_eager_rccl_ab.jsonl); with the opt-in, whether to use the graph is
+        decided collectively, so no rank replays a graph while another steps eagerly."""
         if self.engine.device.type != "cuda":
             return False
-        if self.reducer is not None and os.environ.get("VINF_GRAPH_COLLECTIVES", "1") != "1":
-            # RCCL all-reduces are captured into the step graph by default (tested on a 1-rank
-            # RCCL communicator: tests/test_distributed_gpu.py); VINF_GRAPH_COLLECTIVES=0 keeps
-            # DP steps eager
+        multi = self.reducer is not None and self.info.world > 1
+        env = os.environ.get("VINF_GRAPH_COLLECTIVES")
+        if self.reducer is not None and (env == "0" or (multi and env != "1")):
             return False
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -123,15 +152,19 @@ class DataParallelRunner:
         torch.cuda.synchronize()
         # the warmup advanced the schedule; keep the step count honest for replay
         g = torch.cuda.CUDAGraph()
+        ok = True
         try:
             with torch.cuda.graph(g):
                 self._eager_step()
         except Exception:
-            self.graph = None
+            ok = False
             torch.cuda.synchronize()
-            return False
-        self.graph = g
-        return True
+        if multi:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.engine.device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            ok = bool(flag.item())
+        self.graph = g if ok else None
+        return ok
 
     def step(self):
         if self.graph is not None:

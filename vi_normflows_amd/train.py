@@ -128,14 +128,20 @@ def run_planar_vae(cfg, out, info, logger):
     vae.init_reference(generator=torch.Generator().manual_seed(cfg.seed))
     vae.to(dev)
     it = make_batch_iter(X, cfg.batch, cfg.iters, generator=g, rank=info.rank, world=info.world)
-    engine_ok = (dev.type == "cuda" and info.world == 1 and cfg.optimizer == "adam"
-                 and cfg.schedule in ("none", "reference") and cfg.hidden == 64
-                 and 1 <= cfg.n_hidden <= 4 and cfg.dim_z % 4 == 0 and cfg.dim_z <= 64
-                 and cfg.K <= 8 and cfg.dim % 4 == 0 and cfg.dim <= 1024
-                 and cfg.extra.get("engine", True))
+    from .models.vae_engine import PlanarVAEEngine
+
+    # GPU: the HIP engine whenever it takes the configuration (extra.engine=false opts out);
+    # CPU: only on request (extra.engine="force": the engine's autograd reference step, e.g.
+    # the gloo DP tests of the engine's runner contract)
+    want = cfg.extra.get("engine", True)
+    engine_ok = (cfg.optimizer == "adam" and cfg.schedule in ("none", "reference")
+                 and ((dev.type == "cuda" and want is not False and PlanarVAEEngine.supported(vcfg))
+                      or (dev.type != "cuda" and want == "force" and cfg.hidden == 64)))
     if engine_ok:
-        # models/vae_engine.py: the whole step in two HIP launches + flat Adam, one hipGraph
-        from .models.vae_engine import PlanarVAEEngine
+        # models/vae_engine.py: the whole step in two HIP launches + flat Adam, one hipGraph; DP
+        # through the runner (rank 0's weights broadcast, bucketed RCCL all-reduce, 1/world in
+        # the optimizer); rank-distinct noise streams come from the rank seed
+        from .parallel.runner import DataParallelRunner
 
         eng = PlanarVAEEngine(vcfg, batch=cfg.batch, device=dev, seed=rank_seed(cfg.seed, info.rank),
                               lr=cfg.lr, anneal=cfg.schedule, anneal_iters=cfg.iters)
@@ -146,24 +152,48 @@ def run_planar_vae(cfg, out, info, logger):
             return xb if n == cfg.batch else xb[torch.arange(cfg.batch) % n]
 
         eng.set_batch(full(it(0)).to(dev))
-        graph = eng.capture(warmup=1)
+        run = DataParallelRunner(eng, info)
+        if dev.type == "cuda" and cfg.extra.get("graph", True):
+            run.capture(warmup=1)
         eng.params.m.zero_()           # the capture warm-up stepped Adam: start from the init
         eng.params.v.zero_()
         eng.load_module(vae)
         eng.step_t.zero_()
+        eng.n_skipped.zero_()
+        recon_every = int(cfg.extra.get("recon_every", 200))
+        x_probe = X[min(101, X.shape[0] - 1)]          # the reference plots X[101] (utils.py:33)
         F = float("nan")
         for t in range(cfg.iters):
             eng.set_batch(full(it(t)).to(dev))
-            graph.replay()
-            if (t + 1) % max(cfg.log_every, 1) == 0 or t + 1 == cfg.iters:
+            run.step()
+            last = t + 1 == cfg.iters
+            if (t + 1) % max(cfg.log_every, 1) == 0 or last:
+                # optimization.py:97-102: objective + gradient magnitude every log_every steps
+                # (read from the step itself, no extra passes: SURVEY Q10), plus skipped steps
                 F = eng.loss.item()
                 if logger is not None:
-                    logger.log({"step": t + 1, "F": F, "beta": eng.beta.item()})
+                    logger.log({"step": t + 1, "F": F, "beta": eng.beta.item(),
+                                "grad_norm": math.sqrt(max(float(eng.gnorm2.item()), 0.0)),
+                                "skipped": float(eng.n_skipped.item())})
+            if info.is_main and recon_every > 0 and ((t + 1) % recon_every == 0 or last):
+                # optimization.py:103-111: a true-vs-reconstruction figure every 200 steps
+                from .viz.plots import compare_reconstruction
+
+                try:
+                    compare_reconstruction(eng.to_module(PlanarVAE(vcfg)), x_probe, K=cfg.K,
+                                           t=t + 1, figname=str(out / "{}_flows_iter_{}.png"),
+                                           generator=torch.Generator().manual_seed(t))
+                except ImportError:   # matplotlib absent: figures are optional
+                    recon_every = 0
         if info.is_main:
             vae = eng.to_module(vae)
             vae.cpu().save_reference(out / f"weights_phi_{cfg.K}.npy", out / f"weights_theta_{cfg.K}.npy")
             append_free_energy(out / "free_energy.txt", cfg.K, F * cfg.batch)
-        return {"free_energy_per_sample": F, "engine": "vae_engine"}
+        vdist.barrier()
+        return {"free_energy_per_sample": F, "engine": "vae_engine",
+                "skipped_steps": float(eng.n_skipped.item()),
+                # replica check: identical on every rank after broadcast + all-reduced steps
+                "param_checksum": float(eng.params.master.double().sum().item())}
     gd = torch.Generator(device=dev).manual_seed(rank_seed(cfg.seed, info.rank))
 
     def loss_fn(t, beta):
@@ -190,8 +220,8 @@ def run_iaf_vae(cfg, out, info, logger):
     model = IAFVAE(icfg).to(dev)
     X = synthetic_images(cfg.extra.get("n_data", 8192), seed=cfg.seed + info.rank, device=dev)
     nb = X.shape[0] // cfg.batch
-    if (dev.type == "cuda" and cfg.optimizer == "adam" and cfg.schedule == "none" and nb > 0
-            and cfg.extra.get("engine", True)):
+    if (dev.type == "cuda" and cfg.optimizer == "adam" and nb > 0
+            and cfg.schedule in ("none", "reference", "theano") and cfg.extra.get("engine", True)):
         # models/iaf_engine.py: flat buffers, explicit backward, one hipGraph (DP: the runner's
         # bucketed all-reduce; rank 0's parameters are broadcast)
         from .models.iaf_engine import IAFEngine
@@ -200,17 +230,23 @@ def run_iaf_vae(cfg, out, info, logger):
 
         eng = IAFEngine(icfg, cfg.batch, X[:nb * cfg.batch].reshape(nb * cfg.batch, -1),
                         device=dev, seed=rank_seed(cfg.seed, info.rank), rank=info.rank,
-                        lr=cfg.lr, model=model)
+                        lr=cfg.lr, model=model, anneal=cfg.schedule, anneal_iters=cfg.iters)
         run = DataParallelRunner(eng, info)
         if cfg.extra.get("graph", True):
             run.capture(warmup=1)
             eng.load_module(model)     # the capture warm-up stepped Adam: start from the init
+            eng.params.m.zero_()
+            eng.params.v.zero_()
+            eng.step_t.zero_()         # ... and advanced the schedule: beta_t restarts at t = 0
+            eng.n_skipped.zero_()
         t0 = time.perf_counter()
         for t in range(cfg.iters):
             run.step()
             if t % cfg.log_every == 0 or t == cfg.iters - 1:
                 F = float(eng.loss.item())
-                logger.log({"step": t, "F": F, "skipped": float(eng.n_skipped.item()),
+                logger.log({"step": t, "F": F, "beta": float(eng.beta_t.item()),
+                            "grad_norm": math.sqrt(max(float(eng.gnorm2.item()), 0.0)),
+                            "skipped": float(eng.n_skipped.item()),
                             "samples_per_s": (t + 1) * cfg.batch * info.world
                             / (time.perf_counter() - t0)})
         save_engine(eng, out / "ckpt.pt", info.rank)
