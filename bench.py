@@ -16,7 +16,7 @@ warm-up over the first 100 steps (the first bias-corrected Adam step is a sign
 step on all 72 M parameters; without the ramp the flow's log-det collapses to
 -1500 in one step). The target's pairs (z_i, z_{D/2+i}) straddle the coupling
 split. ``final_free_energy`` in the record is the F of the last timed step;
-``profiles/r2_headline_convergence.jsonl`` holds a 2000-step trajectory of this
+``profiles/r2_headline_convergence_split_lr1e-3_b65536.jsonl`` holds a 2000-step trajectory of this
 exact configuration.
 
     python bench.py --gpus N --steps K --warmup W

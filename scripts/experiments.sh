@@ -1,0 +1,33 @@
+# Named GPU experiments (round 3 and later), one parameterised runner instead of one-off files.
+#   gpurun -- 'bash scripts/experiments.sh <name> [args]'
+# Every GPU step runs under its own time limit and the chain stops at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+name=$1; shift
+O=gpurun_out/exp_$name; mkdir -p $O
+
+case $name in
+  mem_issue)      # per-CU / per-XCD global load & store issue rates (tools/mem_issue_bench.hip)
+    /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/mem_issue_bench.hip -o $O/mem_issue_bench &&
+    timeout -k 10 120 $O/mem_issue_bench full > $O/mem.jsonl ;;
+  desync)         # persistent GEMMs with a start offset on half the blocks: bit 0 = XCD parity,
+                  # bit 5 = half the CUs of every XCD; args: batch
+    b=${1:-262144}
+    for cfg in "0 0" "4 0" "4 5" "6 5" "4 3"; do set -- $cfg
+      VINF_G256_DESYNC=$1 VINF_G256_DESYNC_BIT=$2 VINF_BENCH_TAG=b${b}_d$1_bit$2 \
+        timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --batch $b --iters 10 \
+        --only fwd_l1,fwd_l2,cpl_fwd,dgrad_l2,cpl_bwd >> $O/sg.jsonl || exit 1
+    done ;;
+  wgrad_ab)       # the deferred weight-gradient launch: baseline, deeper ring, XCD packing off
+    for r in 1 2; do
+      VINF_BENCH_TAG=base timeout -k 10 180 python -m vi_normflows_amd.bench.wgrad_bench --layers 13 >> $O/wg.jsonl || exit 1
+      VINF_BENCH_TAG=depth6 VINF_G256_DEPTH=6 timeout -k 10 180 python -m vi_normflows_amd.bench.wgrad_bench --layers 13 >> $O/wg.jsonl || exit 1
+      VINF_BENCH_TAG=xcdpack0 VINF_WGRAD_XCD_PACK=0 timeout -k 10 180 python -m vi_normflows_amd.bench.wgrad_bench --layers 13 >> $O/wg.jsonl || exit 1
+    done ;;
+  mask_ab)        # forward product with / without the ReLU bitmask output, bitmask vs bf16 read
+    for r in 1 2; do
+      timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 \
+        --only fwd_l2,fwd_l2_nomask,dgrad_l2,dgrad_l2_bf16aux >> $O/sg.jsonl || exit 1
+    done ;;
+  *) echo "unknown experiment $name"; exit 2 ;;
+esac

@@ -31,6 +31,8 @@
 struct Shape {
   int width, rows, gap, load, ni;
   long pitch;
+  int pair = 0;   // gap 2 only: odd instructions fill the other 16-B slots of the previous one's
+                  // lines (the coupling-forward epilogue's two float4 stores per 8 features)
   int nx = 8;     // XCDs that work: blocks with (b % 8) < nx (blocks b and b + 8 share an XCD)
   int cu_div = 1; // of those, only blocks with ((b >> 3) % cu_div) == 0 work
 };
@@ -79,7 +81,8 @@ __global__ void __launch_bounds__(512, 1) mem_kernel(char* buf, long region, Sha
   } else {
 #pragma unroll 8
     for (int i = 0; i < s.ni; ++i) {
-      const long r0 = (long)((i * 8 + w) * s.rows) * s.pitch;
+      const int ii = s.pair ? (i >> 1) : i;
+      const long r0 = (long)((ii * 8 + w) * s.rows) * s.pitch + (s.pair ? (i & 1) * W : 0);
       *(T*)(base + r0 + roff) = mk<W>(i ^ lane);
     }
   }
@@ -120,6 +123,12 @@ int main(int argc, char** argv) {
         t.cu_div = cd;
         cases.push_back(t);
       }
+  for (int pr = 0; pr < 2; ++pr) {   // gap-2 stores alone vs filled by the next instruction
+    Shape t{16, 4, 2, 0, 256, 2048};
+    t.pair = pr;
+    cases.push_back(t);
+  }
+  cases.push_back(Shape{16, 4, 1, 0, 256, 2048});   // contiguous reference
   const int grids[] = {dev_cus};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -154,9 +163,9 @@ int main(int argc, char** argv) {
       const double bytes = instr * 64 * s.width;  // per block
       // cycles per wave-instruction per CU at an assumed 2.0 GHz (relative measure only)
       printf("{\"op\": \"%s\", \"width\": %d, \"rows\": %d, \"gap\": %d, \"pitch\": %ld, "
-             "\"blocks\": %d, \"xcds\": %d, \"working\": %d, \"us\": %.2f, \"GBps_per_cu\": %.1f, "
+             "\"pair\": %d, \"blocks\": %d, \"xcds\": %d, \"working\": %d, \"us\": %.2f, \"GBps_per_cu\": %.1f, "
              "\"TBps_total\": %.2f, \"ns_per_instr\": %.2f}\n",
-             s.load ? "load" : "store", s.width, s.rows, s.gap, s.pitch, g, s.nx, working, us,
+             s.load ? "load" : "store", s.width, s.rows, s.gap, s.pitch, s.pair, g, s.nx, working, us,
              bytes / us / 1e3, bytes * working / us / 1e6, us * 1e3 / instr);
       fflush(stdout);
     }

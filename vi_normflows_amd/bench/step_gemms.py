@@ -40,6 +40,10 @@ def build(B: int, dev):
     m2 = torch.empty(B, H // 8, device=dev, dtype=torch.uint8)
     fns["fwd_l2"] = (lambda: gemm.linear_fwd(h1, W2, b1, h2, relu=True, mask_out=m2),
                      2.0 * B * H * H)
+    # A/B probes of the epilogue's side outputs: the ReLU bitmask store (forward) and the
+    # bitmask vs bf16-activation read (input gradient)
+    fns["fwd_l2_nomask"] = (lambda: gemm.linear_fwd(h1, W2, b1, h2, relu=True, mask_out=None),
+                            2.0 * B * H * H)
     W3 = torch.zeros(Np, H, device=dev)
     W3[:2 * Dh] = torch.randn(2 * Dh, H, device=dev, generator=g) * 0.03
     W3 = W3.to(bf)
@@ -61,6 +65,8 @@ def build(B: int, dev):
     dh1 = torch.empty(B, H, device=dev, dtype=bf)
     fns["dgrad_l2"] = (lambda: gemm.linear_dgrad(dh2, W2, dh1, relu_of=h1, relu_bits=m1, Wt=W2t),
                        2.0 * B * H * H)
+    fns["dgrad_l2_bf16aux"] = (lambda: gemm.linear_dgrad(dh2, W2, dh1, relu_of=h1, Wt=W2t),
+                               2.0 * B * H * H)
     W1t = W1.t().contiguous()
     G = torch.randn(B, Dp, device=dev, generator=g)
     dst0 = torch.empty(B, Np, device=dev, dtype=bf)

@@ -1,0 +1,73 @@
+"""Weight-gradient launches of the RealNVP-32 headline step in isolation.
+
+Builds the deferred weight-gradient plan of ``--layers`` conditioner layers (392-1024-1024-784,
+per-layer problems dW3 [800 x 1024], dW2 [1024 x 1024], dW1 [1024 x 416], K = batch) on random
+bf16 operands and times the launches the engine issues (``ops.gemm.WgradScheduler``: chunks of
+CU-count whole 256x256 tiles), interleaving ``--iters`` repetitions in one process.
+
+    python -m vi_normflows_amd.bench.wgrad_bench [--batch 65536] [--layers 8] [--iters 5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+
+import torch
+
+
+def build(B: int, layers: int, dev):
+    from ..ops import gemm
+
+    bf = torch.bfloat16
+    H, Dp, Np = 1024, 416, 800
+    g = torch.Generator(device=dev).manual_seed(0)
+
+    def rnd(*s):
+        return torch.randn(*s, device=dev, generator=g).to(bf)
+
+    items = []
+    grads = []
+    for _ in range(layers):
+        dst, a2, dh2, a1, dh1, x = rnd(B, Np), rnd(B, H), rnd(B, H), rnd(B, H), rnd(B, H), rnd(B, Dp)
+        for dy, inp, (o, i) in ((dst, a2, (Np, H)), (dh2, a1, (H, H)), (dh1, x, (H, Dp))):
+            dW = torch.empty(o, i, device=dev)
+            db = torch.empty(o, device=dev)
+            grads.append((dW, db))
+            items.append((dy, inp, dW, db))
+    return gemm.WgradPlan(items), grads
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--layers", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--tag", default=os.environ.get("VINF_BENCH_TAG", ""))
+    a = ap.parse_args(argv)
+    dev = torch.device("cuda")
+    plan, _ = build(a.batch, a.layers, dev)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    nl = plan.total // cus          # whole launches of one tile per CU
+    flops = 2.0 * a.batch * cus * 256 * 256
+    for _ in range(2):
+        plan.run(0, cus)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(a.iters):
+        for c in range(nl):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            plan.run(c * cus, cus)
+            e.record()
+            e.synchronize()
+            ts.append(s.elapsed_time(e) * 1e3)
+    ts.sort()
+    med = ts[len(ts) // 2]
+    print(json.dumps({"tag": a.tag, "launches": nl, "tiles_per_launch": cus,
+                      "us_min": round(ts[0], 1), "us_med": round(med, 1),
+                      "tflops_padded": round(flops / med / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
