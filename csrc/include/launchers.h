@@ -96,6 +96,8 @@ void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, co
 void nf_gemm256_set_depth(int d);
 void nf_gemm256_set_persist(int on);
 int nf_gemm256_get_persist();
+void nf_gemm256_set_cpl_edge(int on);
+int nf_gemm256_get_cpl_edge();
 // input gradient with W given transposed (Wt [N][K]): NT instantiation, bf16 (ReLU-mask) epilogue
 void nf_launch_gemm256_nt_dgrad(const void* dy, long lddy, const void* Wt, long ldwt,
                                 const void* aux, long ld_aux, int aux_is_bits, void* dx,

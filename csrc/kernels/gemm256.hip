@@ -436,24 +436,36 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
   // bias gradient db[m] = sum_k Aop(m,k) (weight-gradient launches, tn == 0 blocks: the DODB
-  // instantiation): an MFMA of a ones fragment against A fragment j == wc of each A half, read
-  // once more from LDS with a wave-uniform offset (2 / 4 extra reads and 4 extra MFMAs per
-  // K-tile per wave; selecting fa[wc] from registers compiled to a branch ladder per MFMA)
+  // instantiation). Wave wc sums A fragment j == wc of each A half - already in registers for
+  // the MFMAs, 8 consecutive k of row (lane & 15) per k-step - with v_dot2_f32_bf16 against a
+  // (1, 1) literal: 4 VALU per k-step in the MFMA shadow, no extra registers, LDS reads or
+  // MFMAs (the former ones-fragment MFMA held 20 VGPRs, which spilled the 10-slot ring build).
+  // The wave-uniform switch picks the fragment once per half (indexing fa[wc] per instruction
+  // compiled to a branch ladder). dbs[h]: partial over this lane's k chunks; lanes are reduced
+  // over (lane >> 4) in the epilogue.
   constexpr bool do_db = DODB;
-  v4f accb[2] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
-  v8s ones;
+  v8s fa[4][2], fbl[2][2], fbh[2][2];
+  float dbs[2] = {0.f, 0.f};
+  auto db_sum = [&](float& sacc, bool two_) {
+    typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
+    const v2bf one = {(__bf16)1.0f, (__bf16)1.0f};
+    auto add = [&](const v8s (&f)[2]) {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;
-  v8s fdb[2];
-  auto db_read = [&](const char* half) {
+      for (int ks = 0; ks < 2; ++ks) {
+        if (ks == 1 && !two_) break;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) fdb[ks] = read_frag<A_KMAJOR>(half, wr * 64 + wc * 16, ks, lane);
-  };
-  auto db_mfma = [&](v4f& acc_b, bool two_) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      if (ks == 1 && !two_) break;
-      acc_b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fdb[ks], acc_b, 0, 0, 0);
+        for (int e = 0; e < 4; ++e) {
+          const unsigned w = (unsigned)(unsigned short)f[ks][2 * e] |
+                             ((unsigned)(unsigned short)f[ks][2 * e + 1] << 16);
+          sacc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf, w), one, sacc, false);
+        }
+      }
+    };
+    switch (wc) {
+      case 0: add(fa[0]); break;
+      case 1: add(fa[1]); break;
+      case 2: add(fa[2]); break;
+      default: add(fa[3]); break;
     }
   };
 
@@ -492,7 +504,6 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
     NF_STAMP(1);
     if (wr == 1) barrier();
 
-    v8s fa[4][2], fbl[2][2], fbh[2][2];
     // One K-tile (4 phases). STEADY: every half this K-tile issues exists (t + 2 < nkt) and
     // the K-tile is a whole 64-deep step, so the issue bound checks, the runtime vmcnt ladder
     // and the tail branch inside the MFMA cluster all fold away (straight-line phases with a
@@ -523,13 +534,12 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
           fa[j][ks] = read_frag<A_KMAJOR>(slot(t, H_ALO), wr * 64 + j * 16, ks, lane);
-      if constexpr (do_db) db_read(slot(t, H_ALO));
       issue_wait(4 * t + 6 + X, P + 1);
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
       NF_G256_QUAD(0, 0, fbl);
-      if constexpr (do_db) db_mfma(accb[0], two);
+      if constexpr (do_db) db_sum(dbs[0], two);
       __builtin_amdgcn_s_setprio(0);
       barrier();
       // ---- r2: M0-3 x N2-3
@@ -551,13 +561,12 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
           fa[j][ks] = read_frag<A_KMAJOR>(slot(t, H_AHI), wr * 64 + j * 16, ks, lane);
-      if constexpr (do_db) db_read(slot(t, H_AHI));
       issue_wait(4 * t + 8 + X, P + 3);
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
       NF_G256_QUAD(2, 4, fbh);
-      if constexpr (do_db) db_mfma(accb[1], two);
+      if constexpr (do_db) db_sum(dbs[1], two);
       __builtin_amdgcn_s_setprio(0);
       barrier();
       // ---- r4: M4-7 x N0-1 (no LDS reads)
@@ -585,11 +594,14 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
   // ---------------------------------------------------------------- epilogue
   // acc[i][j]: n = n0 + wc*64 + i*16 + (lane>>4)*4 + r, m = m0 + wr*128 + j*16 + (lane&15)
   const int g = lane >> 4, c = lane & 15;
-  if (do_db && a.dbias != nullptr && g == 0) {  // accb[h]: m = wr*128 + h*64 + wc*16 + (lane & 15), any of the 4 rows
+  if (do_db && a.dbias != nullptr) {   // dbs[h]: m = wr*128 + h*64 + wc*16 + (lane & 15)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+      float v = dbs[h];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
       const int m = m0 + wr * 128 + h * 64 + wc * 16 + c;
-      if (m < a.M) a.dbias[(long)split * a.M + m] = accb[h][0];
+      if (g == 0 && m < a.M) a.dbias[(long)split * a.M + m] = v;
     }
   }
   if constexpr (EPI == EPI_CPL_FWD) {
@@ -1103,11 +1115,112 @@ void launch_f8(GemmArgs a, hipStream_t stream) {
   NF_HIP_CHECK(hipGetLastError());
 }
 
+// Coupling forward of the last r = Dh % 128 (<= 8) features of a layer, for the launches whose
+// 256-column GEMM tiles cover only the first Dh - r features. Fused, those 8 features were a
+// whole extra column tile (n0 = 3 * 256 at Dh = 392): a full 256 x 256 main loop, 97% of it on
+// zero weight rows, plus an epilogue pass - ~40 us of a 195 us launch at the headline shape
+// (bench/step_gemms.py cpl_fwd vs cpl_fwd_384). Here one wave owns 16 rows: the 16 x 16 MFMA
+// output holds the r s-columns (weight rows j0 + f, MFMA rows 0..7) and r t-columns (rows
+// Dh + j0 + f, MFMA rows 8..15) over the same v_mfma_f32_16x16x32_bf16 k-sequence the tile
+// kernel runs, so s_hat / t are bitwise the fused path's; the lanes holding t hand them to the
+// s lanes with one shuffle, the upper half of the wave zeroes the next operand's pad columns.
+// ldjp row Dh / 128 gets this slice's sum of s (written, or added under !ldj_init).
+struct CplEdgeArgs {
+  const bf16_t* h; long ldh;
+  const bf16_t* W; long ldw;
+  const bf16_t* bias;
+  int M, K, Dh, j0, r;
+  const float* x; long ldx;
+  float* y; long ldy;
+  bf16_t* yb; long ldyb; int yb_width;
+  bf16_t* st; long ldst;
+  float* ldjp; int ldj_init;
+  float scale;
+};
+
+__global__ void __launch_bounds__(256) cpl_edge_fwd_kernel(CplEdgeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int m0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  if (m0 >= a.M) return;
+  const int e = lane & 15, g = lane >> 4, f = e & 7;
+  const bool wok = f < a.r;
+  const long wrow = (e < 8 ? 0 : a.Dh) + a.j0 + (wok ? f : 0);
+  const bf16_t* wp = a.W + wrow * a.ldw + 8 * g;
+  const int mr = min(m0 + e, a.M - 1);
+  const bf16_t* hp = a.h + (long)mr * a.ldh + 8 * g;
+  v4f acc = {0.f, 0.f, 0.f, 0.f};
+  const v8s zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int k0 = 0; k0 < a.K; k0 += 256) {   // K % 256 == 0 (launcher): 8 k-steps per chunk,
+    v8s wv[8], hv[8];                          // all 16 loads issued before the first MFMA
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      wv[s] = wok ? *reinterpret_cast<const v8s*>(wp + k0 + 32 * s) : zero;
+      hv[s] = *reinterpret_cast<const v8s*>(hp + k0 + 32 * s);
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[s], hv[s], acc, 0, 0, 0);
+  }
+  // acc[i] of lane l: MFMA row 4 (l >> 4) + i, sample m0 + (l & 15). Lanes 0..31 hold s_hat of
+  // features 4 (l >> 4) + i, lanes 32..63 the matching t rows.
+  float tv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) tv[i] = __shfl(acc[i], (lane + 32) & 63);
+  const int m = m0 + e;
+  if (lane < 32) {
+    float part = 0.f, lold = 0.f;
+    const int jf = a.j0 + 4 * g;
+    if (m < a.M && 4 * g < a.r) {
+      if (!a.ldj_init && g == 0) lold = a.ldjp[m];
+      const float4 xv = *reinterpret_cast<const float4*>(a.x + (long)m * a.ldx + jf);
+      const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+      float yv[4];
+      unsigned short sh[4], ybv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float bs = a.bias ? bf2f(a.bias[jf + i]) : 0.f;
+        const float bt = a.bias ? bf2f(a.bias[a.Dh + jf + i]) : 0.f;
+        sh[i] = f2bf(fmaf(acc[i], 1.f, bs));
+        const float tt = bf2f(f2bf(fmaf(tv[i], 1.f, bt)));
+        const float sv = a.scale * fast_tanhf(bf2f(sh[i]));
+        yv[i] = fmaf(xs[i], __expf(sv), tt);
+        ybv[i] = f2bf(yv[i]);
+        part += sv;
+      }
+      *reinterpret_cast<float4*>(a.y + (long)m * a.ldy + jf) = make_float4(yv[0], yv[1], yv[2], yv[3]);
+      if (a.yb)
+        *reinterpret_cast<ushort4*>(a.yb + (long)m * a.ldyb + jf) =
+            make_ushort4(ybv[0], ybv[1], ybv[2], ybv[3]);
+      *reinterpret_cast<ushort4*>(a.st + (long)m * a.ldst + jf) =
+          make_ushort4(sh[0], sh[1], sh[2], sh[3]);
+    }
+    part += __shfl_xor(part, 16);
+    if (g == 0 && m < a.M) a.ldjp[m] = part + lold;
+  } else if (a.yb && m < a.M) {   // zero the next operand's pad columns [Dh, yb_width)
+    bf16_t* yr = a.yb + (long)m * a.ldyb;
+    for (int c = a.Dh + 8 * (g - 2); c < a.yb_width; c += 16)
+      *reinterpret_cast<uint4*>(yr + c) = make_uint4(0, 0, 0, 0);
+  }
+}
+
+// VINF_CPL_EDGE (read at load; default 0): 1 routes a layer's last Dh % 128 <= 8 features
+// through cpl_edge_fwd_kernel instead of the fused edge column tile. Measured SLOWER at the
+// headline shape (cpl_fwd 208.7 vs 190.4 us, profiles/r3/cpl_edge_ab.jsonl): its 16-row x 64-B
+// operand loads re-read the 134 MB activation at ~2.4 TB/s, while the fused edge tile only adds
+// its DMA stream (~37 us). Kept as an A/B switch with its bitwise test.
+static int g_cpl_edge = [] {
+  const char* e = getenv("VINF_CPL_EDGE");
+  return e ? atoi(e) : 0;
+}();
+
 }  // namespace g256
 }  // namespace gemm
 }  // namespace nf
 
 using namespace nf::gemm;
+
+void nf_gemm256_set_cpl_edge(int on) { g256::g_cpl_edge = on ? 1 : 0; }
+int nf_gemm256_get_cpl_edge() { return g256::g_cpl_edge; }
 
 // 4 (default): 8-slot LDS ring, 128 KiB; 6: 10-slot ring, 160 KiB, half-tiles issued 2 phases
 // earlier (VINF_G256_DEPTH at load, or set_mode's depth argument)
@@ -1204,7 +1317,14 @@ void nf_launch_gemm256_nt_cpl(const void* h, long ldh, const void* W, long ldw, 
   a.B = (const nf::bf16_t*)W; a.ldb = ldw;
   a.C = st; a.ldc = ld_st;
   a.bias = (const nf::bf16_t*)bias;
-  const int ntn = (Dh + 127) / 128;
+  // the last r = Dh % 128 <= 8 features go to cpl_edge_fwd_kernel (bf16 operands, K % 256 == 0):
+  // the GEMM covers Dh - r features and never reaches the pad columns, which the edge kernel zeroes
+  const int r = Dh % 128;
+  const bool edge = g256::g_cpl_edge && r > 0 && r <= 8 && Dh > 128 && K % 256 == 0 &&
+                    ldh % 8 == 0 && ldw % 8 == 0 && ((unsigned long)h & 15) == 0 &&
+                    ((unsigned long)W & 15) == 0;
+  const int dmain = edge ? Dh - r : Dh;
+  const int ntn = (dmain + 127) / 128;
   a.M = M; a.N = ntn * 256; a.K = K; a.k_per_split = ((K + 63) / 64) * 64;
   a.cf_x = x; a.ld_cf_x = ld_x;
   a.cf_y = y; a.ld_cf_y = ld_y;
@@ -1220,6 +1340,20 @@ void nf_launch_gemm256_nt_cpl(const void* h, long ldh, const void* W, long ldw, 
     abort();
   }
   g256::launch<true, true, EPI_CPL_FWD>(a, 1, stream);
+  if (edge) {
+    g256::CplEdgeArgs e{};
+    e.h = (const nf::bf16_t*)h; e.ldh = ldh;
+    e.W = (const nf::bf16_t*)W; e.ldw = ldw;
+    e.bias = (const nf::bf16_t*)bias;
+    e.M = M; e.K = K; e.Dh = Dh; e.j0 = dmain; e.r = r;
+    e.x = x; e.ldx = ld_x; e.y = y; e.ldy = ld_y;
+    e.yb = (nf::bf16_t*)yb; e.ldyb = ld_yb; e.yb_width = yb_width;
+    e.st = (nf::bf16_t*)st; e.ldst = ld_st;
+    e.ldjp = ldjp + (long)ntn * ld_ldjp; e.ldj_init = ldj_init;
+    e.scale = scale;
+    hipLaunchKernelGGL(g256::cpl_edge_fwd_kernel, dim3((M + 63) / 64), dim3(256), 0, stream, e);
+    NF_HIP_CHECK(hipGetLastError());
+  }
 }
 
 // Second MADE product of MAF layer l with the layer's transform fused (EPI_CPL_FWD, cf_mode 1):

@@ -10,6 +10,9 @@ case $name in
   mem_issue)      # per-CU / per-XCD global load & store issue rates (tools/mem_issue_bench.hip)
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/mem_issue_bench.hip -o $O/mem_issue_bench &&
     timeout -k 10 120 $O/mem_issue_bench full > $O/mem.jsonl ;;
+  dma)            # LDS-DMA operand stream: segment size x footprint x DMA depth per wave
+    /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/mem_issue_bench.hip -o $O/mem_issue_bench &&
+    timeout -k 10 120 $O/mem_issue_bench dma > $O/dma.jsonl ;;
   desync)         # persistent GEMMs with a start offset on half the blocks: bit 0 = XCD parity,
                   # bit 5 = half the CUs of every XCD; args: batch
     b=${1:-262144}
@@ -24,6 +27,13 @@ case $name in
       VINF_BENCH_TAG=depth6 VINF_G256_DEPTH=6 timeout -k 10 180 python -m vi_normflows_amd.bench.wgrad_bench --layers 13 >> $O/wg.jsonl || exit 1
       VINF_BENCH_TAG=xcdpack0 VINF_WGRAD_XCD_PACK=0 timeout -k 10 180 python -m vi_normflows_amd.bench.wgrad_bench --layers 13 >> $O/wg.jsonl || exit 1
     done ;;
+  wgrad_probe)    # TN weight-gradient loop: real vs cache-resident operands vs the NT kernel
+    VINF_BENCH_TAG=d4 timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 > $O/probe.jsonl &&
+    VINF_BENCH_TAG=d6 VINF_G256_DEPTH=6 timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 >> $O/probe.jsonl ;;
+  wgrad_quick)    # weight-gradient correctness + the real deferred launch + the TN/NT probe
+    timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 &&
+    VINF_BENCH_TAG=${1:-cur} timeout -k 10 180 python -m vi_normflows_amd.bench.wgrad_bench --layers 13 >> $O/wg.jsonl &&
+    VINF_BENCH_TAG=${1:-cur} timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 >> $O/probe.jsonl ;;
   mask_ab)        # forward product with / without the ReLU bitmask output, bitmask vs bf16 read
     for r in 1 2; do
       timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 \

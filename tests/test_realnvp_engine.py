@@ -252,6 +252,46 @@ def test_gemm_nt_cpl_matches_torch(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M,K,init", [(700, 1024, True), (65, 512, False), (4096, 256, True)])
+def test_cpl_edge_kernel_matches_fused_edge_tile(gpu, M, K, init):
+    """The last Dh % 128 = 8 features through cpl_edge_fwd_kernel (gemm_cpl_edge(1), default)
+    vs the fused edge column tile (gemm_cpl_edge(0)): the same MFMA k-sequence, so s_hat, y and
+    its bf16 copy are bitwise equal; the pad columns are zeroed; the log-det partial row only
+    differs in summation order (also under ldj accumulate)."""
+    from vi_normflows_amd.ops import gemm
+
+    torch.manual_seed(11)
+    Dh = 392
+    h = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = torch.zeros(800, K, device=gpu)
+    W[:2 * Dh] = torch.randn(2 * Dh, K, device=gpu) * 0.03
+    W = W.to(torch.bfloat16)
+    b = (torch.randn(800, device=gpu) * 0.1).to(torch.bfloat16)
+    x = torch.randn(M, Dh, device=gpu)
+    ldj0 = torch.randn(4, M, device=gpu)
+    outs = []
+    prev = torch.ops.vinf.gemm_cpl_edge(1)
+    try:
+        for on in (1, 0):
+            torch.ops.vinf.gemm_cpl_edge(on)
+            st = torch.full((M, 800), 5.0, device=gpu).to(torch.bfloat16)
+            y = torch.full((M, Dh), 7.0, device=gpu)
+            yb = torch.full((M, 416), 3.0, device=gpu).to(torch.bfloat16)
+            ldjp = ldj0.clone()
+            gemm.linear_fwd_coupling(h, W, b, st, x, y, yb, ldjp, init, 0.5)
+            outs.append((st[:, :Dh].clone(), y, yb, ldjp))
+    finally:
+        torch.ops.vinf.gemm_cpl_edge(prev)
+    torch.cuda.synchronize()
+    (s1, y1, b1, l1), (s2, y2, b2, l2) = outs
+    assert torch.equal(s1, s2)
+    assert torch.equal(y1, y2)
+    assert torch.equal(b1, b2)
+    assert (b1[:, Dh:] == 0).all()
+    assert torch.allclose(l1, l2, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
 def test_transpose_plan_matches_torch(gpu):
     """Batched bf16 transpose (csrc/kernels/layout.hip): ragged shapes, row strides != cols."""
     from vi_normflows_amd.ops.layout import TransposePlan

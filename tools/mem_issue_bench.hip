@@ -17,6 +17,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                     \
@@ -88,6 +89,166 @@ __global__ void __launch_bounds__(512, 1) mem_kernel(char* buf, long region, Sha
   }
 }
 
+// LDS-DMA (global_load_lds, 16 B per lane) issue cost: the GEMM ring's operand stream. Wave w
+// of block b issues NI DMA instructions; instruction i covers `rows` rows x (1024 / rows) B of
+// its block's region (row pitch `pitch`, rows wrapping inside `foot` bytes, so a small footprint
+// is L2-resident after the first pass) into a 16-KiB LDS ring, keeping INF in flight
+// (s_waitcnt vmcnt(INF - 1) after each issue).
+template <int INF>
+__global__ void __launch_bounds__(512, 1) dma_kernel(const char* buf, long region, long foot, int rows,
+                                                     long pitch, int ni, unsigned* sink) {
+  __shared__ __attribute__((aligned(16))) char ring[8][16 * 1024];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lpr = 64 / rows;
+  const char* base = buf + (long)blockIdx.x * region;
+  const long roff = (long)(lane / lpr) * pitch + (long)(lane % lpr) * 16;
+  const long nrows_foot = foot / pitch;
+  for (int i = 0; i < ni; ++i) {
+    const long r0 = ((long)(i * 8 + w) * rows) % nrows_foot;
+    __builtin_amdgcn_global_load_lds((const void*)(base + r0 * pitch + roff),
+                                     (__attribute__((address_space(3))) void*)(ring[w] + (i & 15) * 1024),
+                                     16, 0, 0);
+    if constexpr (INF == 4) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if constexpr (INF == 8) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (ring[w][lane] == 123 && ring[w][lane + 1] == 45) sink[blockIdx.x] = 1;
+}
+
+// Split lines: 16 rows x 64 B per instruction, the two 64-B halves of each 128-B line loaded
+// by different instructions `lag` pairs apart (even instruction 2g: group g, half 0; odd
+// instruction 2g + 1: group g - lag, half 1) - the TN ring's A-lo / A-hi pattern.
+__global__ void __launch_bounds__(512, 1) dma_split_kernel(const char* buf, long region, int lag,
+                                                           int ni, unsigned* sink) {
+  __shared__ __attribute__((aligned(16))) char ring[8][16 * 1024];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long pitch = 2048;
+  const char* base = buf + (long)blockIdx.x * region;
+  for (int i = 0; i < ni; ++i) {
+    const int half = i & 1;
+    int grp = (i >> 1) - (half ? lag : 0);
+    if (grp < 0) grp += ni / 2;
+    const long r0 = ((long)(grp * 8 + w) * 16) % (region / pitch);   // rows wrap in the region
+    const long off = r0 * pitch + (long)(lane >> 2) * pitch + half * 64 + (lane & 3) * 16;
+    __builtin_amdgcn_global_load_lds((const void*)(base + off),
+                                     (__attribute__((address_space(3))) void*)(ring[w] + (i & 15) * 1024),
+                                     16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (ring[w][lane] == 123 && ring[w][lane + 1] == 45) sink[blockIdx.x] = 1;
+}
+
+// GEMM operand geometries, one private panel per block:
+//   mode 0 (TN, mn-major operand): per instruction 2 k-rows x 512 B (the tile's 256 columns) at
+//          row pitch `pitch`, k-rows advancing; the panel sits at column offset 512 * (b % 4)
+//   mode 1 (NT, k-major operand): per instruction 8 rows x 128 B of a 256-row panel at row pitch
+//          `pitch`; every 32 instructions (one K-tile's 256 rows) the column advances 128 B
+// rows wrap inside the block's `foot` bytes (small foot = L2-resident after the first pass)
+__global__ void __launch_bounds__(512, 1) dma_geom_kernel(const char* buf, long region, long foot,
+                                                          int mode, long pitch, int ni,
+                                                          unsigned* sink) {
+  __shared__ __attribute__((aligned(16))) char ring[8][16 * 1024];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const char* base = buf + (long)blockIdx.x * region;
+  const long nrows = foot / pitch;
+  for (int i = 0; i < ni; ++i) {
+    const long q = (long)i * 8 + w;   // block-wide instruction index
+    long off;
+    if (mode == 0) {
+      const long kr = (q * 2 + (lane >> 5)) % nrows;
+      off = kr * pitch + 512 * (blockIdx.x & 3) + (lane & 31) * 16;
+    } else {
+      const long r = (q * 8) % 256 + (lane >> 3);
+      const long col = ((q * 8 / 256) * 128) % pitch;
+      off = (r % nrows) * pitch + col + (lane & 7) * 16;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)(base + off),
+                                     (__attribute__((address_space(3))) void*)(ring[w] + (i & 15) * 1024),
+                                     16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (ring[w][lane] == 123 && ring[w][lane + 1] == 45) sink[blockIdx.x] = 1;
+}
+
+static void run_dma(char* buf, long region, unsigned* sink, int cus) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int ni = 2048;
+  for (long foot : {64L << 10, 1L << 20, 64L << 20})
+    for (int rows : {4, 8, 16})
+      for (int inf : {4, 8, 16}) {
+        const long pitch = 2048;   // a 1024-wide bf16 activation row
+        auto launch = [&] {
+          if (inf == 4) dma_kernel<4><<<cus, 512>>>(buf, region, foot, rows, pitch, ni, sink);
+          else if (inf == 8) dma_kernel<8><<<cus, 512>>>(buf, region, foot, rows, pitch, ni, sink);
+          else dma_kernel<16><<<cus, 512>>>(buf, region, foot, rows, pitch, ni, sink);
+        };
+        for (int i = 0; i < 2; ++i) launch();
+        CK(hipDeviceSynchronize());
+        const int reps = 10;
+        CK(hipEventRecord(e0));
+        for (int i = 0; i < reps; ++i) launch();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        const double us = 1e3 * ms / reps;
+        const double bytes = 8.0 * ni * 1024;   // per block
+        printf("{\"op\": \"dma\", \"rows\": %d, \"seg_bytes\": %d, \"inflight\": %d, "
+               "\"foot_kb\": %ld, \"us\": %.2f, \"GBps_per_cu\": %.1f, \"TBps_total\": %.2f}\n",
+               rows, 1024 / rows, inf, foot >> 10, us, bytes / us / 1e3, bytes * cus / us / 1e6);
+        fflush(stdout);
+      }
+  struct G { int mode; long pitch; long foot; };
+  const G geoms[] = {{0, 832, 1L << 20}, {0, 2048, 1L << 20}, {0, 8192, 1L << 20},
+                     {1, 131072, 32L << 20},
+                     {0, 832, 60L << 20}, {0, 1600, 60L << 20}, {0, 2048, 60L << 20},
+                     {0, 8192, 60L << 20}, {1, 2048, 60L << 20}, {1, 131072, 60L << 20}};
+  for (const G& gm : geoms) {
+    auto launch = [&] { dma_geom_kernel<<<cus, 512>>>(buf, region, gm.foot, gm.mode, gm.pitch, ni, sink); };
+    for (int i = 0; i < 2; ++i) launch();
+    CK(hipDeviceSynchronize());
+    const int reps = 10;
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i) launch();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = 1e3 * ms / reps;
+    const double bytes = 8.0 * ni * 1024;
+    printf("{\"op\": \"dma_geom\", \"mode\": \"%s\", \"pitch\": %ld, \"foot_kb\": %ld, "
+           "\"us\": %.2f, \"GBps_per_cu\": %.1f, \"TBps_total\": %.2f}\n",
+           gm.mode ? "nt" : "tn", gm.pitch, gm.foot >> 10, us, bytes / us / 1e3,
+           bytes * cus / us / 1e6);
+    fflush(stdout);
+  }
+  for (int lag : {0, 2, 8, 32, 128}) {   // HBM footprint (ni/2 groups x 8 waves x 16 rows x 2 KB)
+    auto launch = [&] { dma_split_kernel<<<cus, 512>>>(buf, region, lag, ni, sink); };
+    for (int i = 0; i < 2; ++i) launch();
+    CK(hipDeviceSynchronize());
+    const int reps = 10;
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i) launch();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = 1e3 * ms / reps;
+    const double bytes = 8.0 * ni * 1024;
+    printf("{\"op\": \"dma_split\", \"lag\": %d, \"us\": %.2f, \"GBps_per_cu\": %.1f, "
+           "\"TBps_total\": %.2f}\n", lag, us, bytes / us / 1e3, bytes * cus / us / 1e6);
+    fflush(stdout);
+  }
+}
+
 int main(int argc, char** argv) {
   int dev_cus = 256;
   hipDeviceProp_t p;
@@ -99,10 +260,14 @@ int main(int argc, char** argv) {
   CK(hipMemset(buf, 1, region * dev_cus));
   unsigned* sink;
   CK(hipMalloc(&sink, 4 * dev_cus));
+  if (argc > 1 && std::string(argv[1]) == "dma") {
+    run_dma(buf, region, sink, dev_cus);
+    return 0;
+  }
   std::vector<Shape> cases;
   // stores: (width, rows, gap), pitch 2048 (a bf16 1024-wide activation row) unless noted
   const int W[] = {1, 2, 4, 8, 16};
-  const bool full = argc > 1;
+  const bool full = argc > 1 && std::string(argv[1]) == "full";
   for (int ld = 0; ld < 2 && full; ++ld) {
     for (int w : W) cases.push_back({w, 1, 1, ld, 256, 2048});           // contiguous
     cases.push_back({16, 2, 1, ld, 256, 2048});                          // 2 rows x 512 B

@@ -55,6 +55,28 @@ def build(B: int, dev):
     ldjp = torch.empty((Dh + 127) // 128, B, device=dev)
     fns["cpl_fwd"] = (lambda: gemm.linear_fwd_coupling(h2, W3, b3, st, x, y, yb, ldjp, True, 1.0),
                       2.0 * B * 2 * Dh * H)
+    # probe: the last 8 features through cpl_edge_fwd_kernel instead of the fused edge tile
+
+    def cpl_edge_kernel():
+        prev = torch.ops.vinf.gemm_cpl_edge(1)
+        gemm.linear_fwd_coupling(h2, W3, b3, st, x, y, yb, ldjp, True, 1.0)
+        torch.ops.vinf.gemm_cpl_edge(prev)
+
+    fns["cpl_fwd_edge_kernel"] = (cpl_edge_kernel, 2.0 * B * 2 * Dh * H)
+    # probe: the same product with Dh = 384 features (3 whole 128-feature column tiles, no
+    # 8-feature edge tile) - what the edge tile costs
+    D3 = 384
+    W3e = torch.zeros(2 * D3, H, device=dev)
+    W3e[:] = torch.randn(2 * D3, H, device=dev, generator=g) * 0.03
+    W3e = W3e.to(bf)
+    st3 = torch.empty(B, 2 * D3, device=dev, dtype=bf)
+    x3 = torch.randn(B, D3, device=dev, generator=g)
+    y3 = torch.empty(B, D3, device=dev)
+    yb3 = torch.empty(B, D3, device=dev, dtype=bf)
+    ldjp3 = torch.empty(D3 // 128, B, device=dev)
+    fns["cpl_fwd_384"] = (lambda: gemm.linear_fwd_coupling(h2, W3e, b3[:2 * D3].contiguous(), st3,
+                                                           x3, y3, yb3, ldjp3, True, 1.0),
+                          2.0 * B * 2 * D3 * H)
     dst = rnd(B, Np)
     W3d = rnd(Np, H, scale=0.03)
     W3t = W3d.t().contiguous()

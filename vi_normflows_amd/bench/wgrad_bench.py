@@ -38,14 +38,65 @@ def build(B: int, layers: int, dev):
     return gemm.WgradPlan(items), grads
 
 
+def probe(B: int, iters: int, tag: str, dev):
+    """One 256-tile product at M = N = 4096, K = B, three ways: the TN weight-gradient kernel
+    on real operands, the same kernel on stride-0 operands (every k-row the same 8 KiB, so the
+    operand stream always hits cache: what the loop does without memory), and the k-major NT
+    forward kernel at the same FLOPs."""
+    from ..ops import gemm
+
+    bf = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(0)
+    n = 4096
+    dy = (torch.randn(B, n, device=dev, generator=g)).to(bf)
+    x = (torch.randn(B, n, device=dev, generator=g)).to(bf)
+    dW = torch.empty(n, n, device=dev)
+    db = torch.empty(n, device=dev)
+    row = (torch.randn(1, n, device=dev, generator=g)).to(bf)
+    dy0 = row.expand(B, n)
+    x0 = row.expand(B, n)
+    xt = x.t().contiguous()
+    dyt = dy.t().contiguous()
+    out = torch.empty(n, n, device=dev, dtype=bf)
+    cases = {
+        "tn_real": lambda: gemm.WgradPlan([(dy, x, dW, db)]).run(0, 256),
+        "tn_cached": lambda: gemm.WgradPlan([(dy0, x0, dW, db)]).run(0, 256),
+        "tn_a_cached": lambda: gemm.WgradPlan([(dy0, x, dW, db)]).run(0, 256),
+        "tn_b_cached": lambda: gemm.WgradPlan([(dy, x0, dW, db)]).run(0, 256),
+        "nt_real": lambda: gemm.linear_fwd(dyt, xt, None, out),
+    }
+    flops = 2.0 * B * n * n
+    for name, fn in cases.items():
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(iters):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            fn()
+            e.record()
+            e.synchronize()
+            ts.append(s.elapsed_time(e) * 1e3)
+        ts.sort()
+        med = ts[len(ts) // 2]
+        print(json.dumps({"tag": tag, "probe": name, "us_min": round(ts[0], 1),
+                          "us_med": round(med, 1), "tflops": round(flops / med / 1e6, 1)}),
+              flush=True)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--layers", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--tag", default=os.environ.get("VINF_BENCH_TAG", ""))
+    ap.add_argument("--probe", action="store_true")
     a = ap.parse_args(argv)
     dev = torch.device("cuda")
+    if a.probe:
+        probe(a.batch, a.iters, a.tag, dev)
+        return
     plan, _ = build(a.batch, a.layers, dev)
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     nl = plan.total // cus          # whole launches of one tile per CU
