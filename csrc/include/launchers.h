@@ -97,6 +97,11 @@ void nf_gemm256_set_depth(int d);
 void nf_gemm256_set_persist(int on);
 int nf_gemm256_get_persist();
 void nf_gemm256_set_cpl_edge(int on);
+int nf_launch_gemm_pp_nt(const void* x, long ldx, const void* W, long ldw, const void* bias,
+                         void* y, long ldy, int M, int N, int K, int relu, void* mask_out,
+                         long ld_mask, hipStream_t stream);
+int nf_gemm_pp_enabled();
+void nf_gemm_pp_set(int mask);
 int nf_gemm256_get_cpl_edge();
 // input gradient with W given transposed (Wt [N][K]): NT instantiation, bf16 (ReLU-mask) epilogue
 void nf_launch_gemm256_nt_dgrad(const void* dy, long lddy, const void* Wt, long ldwt,

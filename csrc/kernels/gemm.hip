@@ -407,6 +407,9 @@ void nf_launch_gemm_nt(const void* x, long ldx, const void* W, long ldw, const v
                        void* mask_out, long ld_mask) {
   if (M <= 0 || N <= 0) return;
   if (use_256(M, N, K)) {
+    if ((nf_gemm_pp_enabled() & 1) &&
+        nf_launch_gemm_pp_nt(x, ldx, W, ldw, bias, y, ldy, M, N, K, relu, mask_out, ld_mask, stream))
+      return;
     nf_launch_gemm256_nt(x, ldx, W, ldw, bias, y, ldy, M, N, K, relu, stream, mask_out, ld_mask);
     return;
   }

@@ -1219,6 +1219,8 @@ static int g_cpl_edge = [] {
 
 using namespace nf::gemm;
 
+int nf_launch_gemm_pp_cpl_bwd(const GemmArgs& a, hipStream_t stream);   // gemm_pp.hip
+
 void nf_gemm256_set_cpl_edge(int on) { g256::g_cpl_edge = on ? 1 : 0; }
 int nf_gemm256_get_cpl_edge() { return g256::g_cpl_edge; }
 
@@ -1475,6 +1477,10 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
     a.k_per_split = K;
     g256::launch_f8<EPI_CPL_BWD>(a, stream);
     return;
+  }
+  if (w_kmajor && mode == 0 && (nf_gemm_pp_enabled() & 2)) {
+    a.staged = 1;
+    if (nf_launch_gemm_pp_cpl_bwd(a, stream)) return;
   }
   if (w_kmajor) g256::launch<true, true, EPI_CPL_BWD>(a, 1, stream);   // W given as Wt [N][K]
   else g256::launch<true, false, EPI_CPL_BWD>(a, 1, stream);

@@ -28,12 +28,23 @@ case $name in
       VINF_BENCH_TAG=xcdpack0 VINF_WGRAD_XCD_PACK=0 timeout -k 10 180 python -m vi_normflows_amd.bench.wgrad_bench --layers 13 >> $O/wg.jsonl || exit 1
     done ;;
   wgrad_probe)    # TN weight-gradient loop: real vs cache-resident operands vs the NT kernel
-    VINF_BENCH_TAG=d4 timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 > $O/probe.jsonl &&
-    VINF_BENCH_TAG=d6 VINF_G256_DEPTH=6 timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 >> $O/probe.jsonl ;;
+    VINF_BENCH_TAG=${1:-cur} timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 > $O/probe.jsonl &&
+    true ;;
   wgrad_quick)    # weight-gradient correctness + the real deferred launch + the TN/NT probe
     timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 &&
     VINF_BENCH_TAG=${1:-cur} timeout -k 10 180 python -m vi_normflows_amd.bench.wgrad_bench --layers 13 >> $O/wg.jsonl &&
     VINF_BENCH_TAG=${1:-cur} timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 >> $O/probe.jsonl ;;
+  wgrad_pmc)      # L2 hit / miss and wave-state counters of the TN / NT probe (one counter pass)
+    export TMPDIR=/tmp
+    timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES \
+      -d $O/pmc -o probe --output-format csv -- python3 -m vi_normflows_amd.bench.wgrad_bench --probe --iters 2 > $O/probe.log 2>&1 ;;
+  pp_ab)          # two-blocks-per-CU forward GEMM: correctness, then per-product A/B
+    timeout -k 10 300 python -u -m pytest tests/test_gemm_pp_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
+    VINF_GEMM_PP=3 timeout -k 10 300 python -u -m pytest tests/test_realnvp_engine.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider >> $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
+    for r in 1 2; do
+      VINF_GEMM_PP=0 VINF_BENCH_TAG=g256 timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,cpl_bwd >> $O/sg.jsonl || exit 1
+      VINF_GEMM_PP=3 VINF_BENCH_TAG=pp timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,cpl_bwd >> $O/sg.jsonl || exit 1
+    done ;;
   mask_ab)        # forward product with / without the ReLU bitmask output, bitmask vs bf16 read
     for r in 1 2; do
       timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 \

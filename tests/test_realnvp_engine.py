@@ -259,6 +259,7 @@ def test_cpl_edge_kernel_matches_fused_edge_tile(gpu, M, K, init):
     its bf16 copy are bitwise equal; the pad columns are zeroed; the log-det partial row only
     differs in summation order (also under ldj accumulate)."""
     from vi_normflows_amd.ops import gemm
+    from vi_normflows_amd.ops._ext import native
 
     torch.manual_seed(11)
     Dh = 392
@@ -270,10 +271,10 @@ def test_cpl_edge_kernel_matches_fused_edge_tile(gpu, M, K, init):
     x = torch.randn(M, Dh, device=gpu)
     ldj0 = torch.randn(4, M, device=gpu)
     outs = []
-    prev = torch.ops.vinf.gemm_cpl_edge(1)
+    prev = native().gemm_cpl_edge(1)
     try:
         for on in (1, 0):
-            torch.ops.vinf.gemm_cpl_edge(on)
+            native().gemm_cpl_edge(on)
             st = torch.full((M, 800), 5.0, device=gpu).to(torch.bfloat16)
             y = torch.full((M, Dh), 7.0, device=gpu)
             yb = torch.full((M, 416), 3.0, device=gpu).to(torch.bfloat16)
@@ -281,7 +282,7 @@ def test_cpl_edge_kernel_matches_fused_edge_tile(gpu, M, K, init):
             gemm.linear_fwd_coupling(h, W, b, st, x, y, yb, ldjp, init, 0.5)
             outs.append((st[:, :Dh].clone(), y, yb, ldjp))
     finally:
-        torch.ops.vinf.gemm_cpl_edge(prev)
+        native().gemm_cpl_edge(prev)
     torch.cuda.synchronize()
     (s1, y1, b1, l1), (s2, y2, b2, l2) = outs
     assert torch.equal(s1, s2)

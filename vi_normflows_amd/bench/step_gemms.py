@@ -58,9 +58,11 @@ def build(B: int, dev):
     # probe: the last 8 features through cpl_edge_fwd_kernel instead of the fused edge tile
 
     def cpl_edge_kernel():
-        prev = torch.ops.vinf.gemm_cpl_edge(1)
+        from ..ops._ext import native
+
+        prev = native().gemm_cpl_edge(1)
         gemm.linear_fwd_coupling(h2, W3, b3, st, x, y, yb, ldjp, True, 1.0)
-        torch.ops.vinf.gemm_cpl_edge(prev)
+        native().gemm_cpl_edge(prev)
 
     fns["cpl_fwd_edge_kernel"] = (cpl_edge_kernel, 2.0 * B * 2 * Dh * H)
     # probe: the same product with Dh = 384 features (3 whole 128-feature column tiles, no

@@ -64,6 +64,7 @@ def probe(B: int, iters: int, tag: str, dev):
         "tn_a_cached": lambda: gemm.WgradPlan([(dy0, x, dW, db)]).run(0, 256),
         "tn_b_cached": lambda: gemm.WgradPlan([(dy, x0, dW, db)]).run(0, 256),
         "nt_real": lambda: gemm.linear_fwd(dyt, xt, None, out),
+        "nn_real": lambda: gemm.linear_dgrad(dyt, x, out),
     }
     flops = 2.0 * B * n * n
     for name, fn in cases.items():
