@@ -860,6 +860,9 @@ int64_t gemm_persist(int64_t on) {   // on < 0: query only; returns the previous
   if (on >= 0) nf_gemm256_set_persist((int)on);
   return prev;
 }
+int64_t gemm_grid_reserve(int64_t cus) {   // cus < 0: query only; returns the previous value
+  return nf_gemm256_set_reserve((int)cus);
+}
 int64_t gemm_pp(int64_t on) {   // on < 0: query only; returns the previous setting
   const int prev = nf_gemm_pp_enabled();
   if (on >= 0) nf_gemm_pp_set((int)on);
@@ -884,6 +887,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("gemm_persist(int on) -> int", &gemm_persist);
   m.def("gemm_cpl_edge(int on) -> int", &gemm_cpl_edge);
   m.def("gemm_pp(int on) -> int", &gemm_pp);
+  m.def("gemm_grid_reserve(int cus) -> int", &gemm_grid_reserve);
   m.def("gemm_wgrad_xcd_pack(int on) -> int", &gemm_wgrad_xcd_pack);
   m.def("fp8_quant_rows(Tensor x, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("fp8_quant_tensor(Tensor x, Tensor(a!) q, Tensor amax_prev, Tensor(b!) scale, Tensor(c!) amax_cur) -> ()");

@@ -96,6 +96,7 @@ void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, co
 void nf_gemm256_set_depth(int d);
 void nf_gemm256_set_persist(int on);
 int nf_gemm256_get_persist();
+int nf_gemm256_set_reserve(int cus);   // cus < 0: query; returns the previous value
 void nf_gemm256_set_cpl_edge(int on);
 int nf_launch_gemm_pp_nt(const void* x, long ldx, const void* W, long ldw, const void* bias,
                          void* y, long ldy, int M, int N, int K, int relu, void* mask_out,

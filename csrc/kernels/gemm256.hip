@@ -1008,6 +1008,11 @@ static int g_persist = [] {
   return e ? atoi(e) : 1;
 }();
 
+// CUs the persistent grid leaves free (nf_gemm256_set_reserve): a multi-rank backward runs
+// RCCL kernels beside the GEMMs, and a persistent block queued behind one would hold back its
+// whole tile list; grid = min(tiles, CUs - reserve) keeps every block startable
+static int g_reserve = 0;
+
 static int g_xcd_pack = [] {
   const char* e = getenv("VINF_WGRAD_XCD_PACK");
   return e ? atoi(e) : 1;
@@ -1082,7 +1087,9 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
       return e ? atoi(e) : 1;
     }();
     a.no_edge = edge_env ? 0 : 1;
-    const int ntiles = ntm * ntn, cus = device_cus_256();
+    const int ntiles = ntm * ntn;
+    int cus = (device_cus_256() - g_reserve) & ~7;   // whole XCD rounds: xcd_remap's b & 7
+    cus = cus > 8 ? cus : 8;
     const int G = ntiles < cus ? ntiles : cus;
     hipLaunchKernelGGL((gemm256_persistent_kernel<AK, BK_, EPI>), dim3(G), dim3(NTHR), 0, stream,
                        a);
@@ -1228,6 +1235,11 @@ int nf_gemm256_get_cpl_edge() { return g256::g_cpl_edge; }
 // earlier (VINF_G256_DEPTH at load, or set_mode's depth argument)
 void nf_gemm256_set_depth(int d) { g256::g_depth = d == 6 ? 6 : 4; }
 void nf_gemm256_set_persist(int on) { g256::g_persist = on ? 1 : 0; }
+int nf_gemm256_set_reserve(int cus) {
+  const int prev = g256::g_reserve;
+  if (cus >= 0) g256::g_reserve = cus;
+  return prev;
+}
 int nf_gemm256_xcd_pack(int on) {   // on < 0: query; returns the previous setting
   const int prev = g256::g_xcd_pack;
   if (on >= 0) g256::g_xcd_pack = on ? 1 : 0;

@@ -45,6 +45,15 @@ case $name in
       VINF_GEMM_PP=0 VINF_BENCH_TAG=g256 timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,cpl_bwd >> $O/sg.jsonl || exit 1
       VINF_GEMM_PP=3 VINF_BENCH_TAG=pp timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,cpl_bwd >> $O/sg.jsonl || exit 1
     done ;;
+  dp_policy)      # 1-rank RCCL path (--force-reduce): backward GEMM policy A/B
+    timeout -k 10 300 python -u -m pytest tests/test_gemm_persistent_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
+    for r in 1 2; do
+      for pol in 1 fwd reserve:16 reserve:8; do
+        p=${pol%%:*}; res=${pol#*:}; [ "$res" = "$pol" ] && res=0
+        VINF_DP_PERSIST=$p VINF_G256_RESERVE=$res timeout -k 10 240 python bench.py --steps 20 --warmup 5 --force-reduce > $O/b.json 2> $O/b.err || { tail -20 $O/b.err; exit 1; }
+        python -c "import json,sys;d=json.load(open('$O/b.json'));print(json.dumps({'policy':'$pol','ms':d['ms_per_step'],'replicas_identical':d['notes']['replicas_identical']}))" >> $O/ab.jsonl
+      done
+    done ;;
   mask_ab)        # forward product with / without the ReLU bitmask output, bitmask vs bf16 read
     for r in 1 2; do
       timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 \

@@ -146,6 +146,33 @@ def test_persistent_switch_bitwise(gpu):
     assert torch.equal(y0, y1)
 
 
+@pytest.mark.parametrize("reserve", [16, 40, 300])
+def test_persistent_grid_reserve_bitwise(gpu, reserve):
+    """gemm_grid_reserve(R) (the DP runner's "reserve" policy) shrinks the persistent grid to
+    min(tiles, CUs - R) rounded to whole XCD rounds (at least 8 blocks); every tile keeps its K
+    order, so the outputs are bitwise those of the full grid - including a reserve larger than
+    the chip."""
+    torch.manual_seed(8)
+    M, N, K = 70000, 1024, 416
+    x, W, b = _bf(M, K, device=gpu), _bf(N, K, device=gpu, scale=0.05), _bf(N, device=gpu)
+    y1 = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    y0 = torch.empty_like(y1)
+    m1 = torch.empty(M, N // 8, device=gpu, dtype=torch.uint8)
+    m0 = torch.empty_like(m1)
+    prev = torch.ops.vinf.gemm_persist(1)
+    prev_r = torch.ops.vinf.gemm_grid_reserve(0)
+    try:
+        torch.ops.vinf.gemm_nt(x, W, b, y1, 1, m1)
+        assert torch.ops.vinf.gemm_grid_reserve(reserve) == 0
+        torch.ops.vinf.gemm_nt(x, W, b, y0, 1, m0)
+        assert torch.ops.vinf.gemm_grid_reserve(-1) == reserve
+    finally:
+        torch.ops.vinf.gemm_persist(prev)
+        torch.ops.vinf.gemm_grid_reserve(prev_r)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1) and torch.equal(m0, m1)
+
+
 def test_engine_persistent_forward_only_bitwise(gpu):
     """DP policy (parallel/runner.py): persistent grid in the forward only, one block per tile in
     the backward. Same K order per tile -> loss and every gradient bitwise equal to the

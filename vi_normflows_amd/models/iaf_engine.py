@@ -388,10 +388,12 @@ class IAFEngine:
             from ..ops._ext import native
 
             prev = native().gemm_persist(1)
+            prev_r = native().gemm_grid_reserve(0)
         with trace_range("iaf_forward"):
             self.forward()
         if fwd_persist:
             native().gemm_persist(prev)
+            native().gemm_grid_reserve(prev_r)
         with trace_range("iaf_backward"):
             self.backward()
         if reduce_fn is not None:

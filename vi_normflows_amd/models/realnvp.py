@@ -584,13 +584,16 @@ class RealNVPVI:
         fwd_persist = self.persist_forward_only and self.device.type == "cuda"
         if fwd_persist:
             # DP: no collective is in flight during the forward (the optimizer waited for every
-            # bucket), so the one-block-per-CU persistent grid is safe there; the backward,
-            # where RCCL all-reduces hold CUs beside the GEMMs, launches one block per tile
+            # bucket), so the full one-block-per-CU persistent grid is safe there; the backward,
+            # where RCCL all-reduces hold CUs beside the GEMMs, runs the runner's policy (one
+            # block per tile, or a persistent grid with CUs reserved)
             prev = _ext_native().gemm_persist(1)
+            prev_r = _ext_native().gemm_grid_reserve(0)
         with trace_range("flow_forward+elbo"):
             self.forward()
         if fwd_persist:
             _ext_native().gemm_persist(prev)
+            _ext_native().gemm_grid_reserve(prev_r)
         with trace_range("flow_backward"):
             self.backward()
         if reduce_fn is not None:

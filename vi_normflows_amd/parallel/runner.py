@@ -54,18 +54,27 @@ class DataParallelRunner:
         force = force_reduce or os.environ.get("VINF_FORCE_REDUCE", "0") == "1"
         if force and info.world == 1 and not dist.is_initialized():
             _init_single_rank_group(info)
-        persist = os.environ.get("VINF_DP_PERSIST", "fwd")   # "1" all | "0" none | "fwd"
-        self._persist_prev = None     # process-global GEMM switch, restored by close()
+        # "1" all | "0" none | "fwd" (default) | "reserve"
+        persist = os.environ.get("VINF_DP_PERSIST", "fwd")
+        self._persist_prev = None     # process-global GEMM switches, restored by close()
+        self._reserve_prev = None
         if (info.world > 1 or force) and engine.device.type == "cuda" and persist != "1":
             # multi-rank: RCCL kernels run on CUs beside the backward's GEMMs; a persistent GEMM
             # grid (one block per CU, each owning a fixed tile list) would wait for every CU an
-            # all-reduce holds, so those products launch one block per tile instead. The
-            # forward has no collective in flight: engines that support it keep the persistent
-            # grid there (``persist_forward_only``).
+            # all-reduce holds. "fwd": the backward's products launch one block per tile;
+            # "reserve": they keep the persistent grid, sized to leave VINF_G256_RESERVE CUs
+            # (default 16, whole XCD rounds) to RCCL. The forward has no collective in flight:
+            # engines that support it run the full persistent grid there
+            # (``persist_forward_only``).
             from ..ops._ext import native
 
-            self._persist_prev = int(native().gemm_persist(0))
-            if persist == "fwd" and hasattr(engine, "persist_forward_only"):
+            if persist == "reserve":
+                self._persist_prev = int(native().gemm_persist(1))
+                self._reserve_prev = int(native().gemm_grid_reserve(
+                    int(os.environ.get("VINF_G256_RESERVE", "16"))))
+            else:
+                self._persist_prev = int(native().gemm_persist(0))
+            if persist in ("fwd", "reserve") and hasattr(engine, "persist_forward_only"):
                 engine.persist_forward_only = True
         if info.world > 1 or (force and dist.is_initialized()):
             P = engine.params
@@ -113,6 +122,9 @@ class DataParallelRunner:
 
             native().gemm_persist(self._persist_prev)
             self._persist_prev = None
+            if self._reserve_prev is not None:
+                native().gemm_grid_reserve(self._reserve_prev)
+                self._reserve_prev = None
         if hasattr(self.engine, "persist_forward_only"):
             self.engine.persist_forward_only = False
 
