@@ -54,6 +54,20 @@ case $name in
         python -c "import json,sys;d=json.load(open('$O/b.json'));print(json.dumps({'policy':'$pol','ms':d['ms_per_step'],'replicas_identical':d['notes']['replicas_identical']}))" >> $O/ab.jsonl
       done
     done ;;
+  step_ab)        # whole-step A/B of an environment switch: args NAME VALUE_A VALUE_B [rounds]
+    var=$1; va=$2; vb=$3; n=${4:-3}
+    for r in $(seq $n); do
+      for v in $va $vb; do
+        env $var=$v timeout -k 10 240 python bench.py --steps 20 --warmup 5 > $O/b.json 2> $O/b.err || { tail -20 $O/b.err; exit 1; }
+        python -c "import json;d=json.load(open('$O/b.json'));print(json.dumps({'$var':'$v','ms':d['ms_per_step'],'F':d['notes']['final_free_energy']}))" >> $O/ab.jsonl
+      done
+    done ;;
+  step_trace)     # kernel trace + stats of the headline step, graph off and on
+    export TMPDIR=/tmp
+    for gr in off on; do
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$gr -o step --output-format csv -- \
+        python3 bench.py --steps 10 --warmup 3 --graph $gr > $O/bench_$gr.json 2> $O/bench_$gr.err || { tail -20 $O/bench_$gr.err; exit 1; }
+    done ;;
   mask_ab)        # forward product with / without the ReLU bitmask output, bitmask vs bf16 read
     for r in 1 2; do
       timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 \

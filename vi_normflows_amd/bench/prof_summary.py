@@ -54,6 +54,45 @@ def _regions(path):
     return [(n, c, t) for n, (c, t) in acc.items()]
 
 
+def step_gaps(root: str, marker: str = "flat_optimizer_kernel", skip: int = 2) -> str:
+    """Per-step GPU occupancy from a kernel trace: steps end at each ``marker`` kernel; for
+    every step after the first ``skip`` report the span (previous marker end -> this marker
+    end), the union of kernel intervals (busy) and the idle remainder (launch gaps / host
+    stalls), as medians over the steps."""
+    paths = glob.glob(os.path.join(root, "**", "*kernel_trace.csv"), recursive=True)
+    if not paths:
+        return "no kernel_trace.csv under " + root
+    ks = []
+    with open(paths[0]) as f:
+        for r in csv.DictReader(f):
+            ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    ks.sort()
+    ends = [e for s, e, n in ks if marker in n]
+    rows = []
+    for i in range(1 + skip, len(ends)):
+        t0, t1 = ends[i - 1], ends[i]
+        iv = sorted((max(s, t0), min(e, t1)) for s, e, _ in ks if e > t0 and s < t1)
+        busy, cur_s, cur_e, gaps = 0, None, None, []
+        for s, e in iv:
+            if cur_e is None or s > cur_e:
+                if cur_e is not None:
+                    busy += cur_e - cur_s
+                    gaps.append(s - cur_e)
+                cur_s, cur_e = s, e
+            else:
+                cur_e = max(cur_e, e)
+        if cur_e is not None:
+            busy += cur_e - cur_s
+        rows.append((t1 - t0, busy, len(iv), sorted(gaps, reverse=True)[:5]))
+    if not rows:
+        return "fewer than %d steps in the trace" % (skip + 2)
+    med = sorted(rows)[len(rows) // 2]
+    span, busy, n, big = med
+    return (f"median step: span {span / 1e6:.3f} ms, kernels busy {busy / 1e6:.3f} ms "
+            f"({100 * busy / span:.1f} %), idle {(span - busy) / 1e6:.3f} ms, {n} kernels; "
+            f"largest gaps (us) {[round(g / 1e3, 1) for g in big]}")
+
+
 def summarize(root: str, steps: int | None = None, top: int = 30) -> str:
     dbs = glob.glob(os.path.join(root, "**", "*.db"), recursive=True)
     csvs = glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), recursive=True) or \
@@ -84,8 +123,11 @@ def main():
     ap.add_argument("root")
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--gaps", action="store_true", help="per-step busy / idle from the trace")
     a = ap.parse_args()
     print(summarize(a.root, a.steps, a.top))
+    if a.gaps:
+        print(step_gaps(a.root))
 
 
 if __name__ == "__main__":

@@ -169,8 +169,9 @@ class RealNVPVI:
         self.Act = torch.empty(L, cfg.n_hidden, B, H, dtype=self.cdt, device=dev)
         # ReLU bitmasks of the hidden activations, written by the forward GEMM epilogue and read
         # by the input-gradient epilogue instead of the bf16 activation (B*H/8 bytes vs 2*B*H)
+        # (VINF_RELU_BITS=0: no bitmask; the input gradient reads the bf16 activation)
         self.Mk = None
-        if dev.type == "cuda" and H % 8 == 0:
+        if dev.type == "cuda" and H % 8 == 0 and os.environ.get("VINF_RELU_BITS", "1") != "0":
             self.Mk = torch.empty(L, cfg.n_hidden, B, H // 8, dtype=torch.uint8, device=dev)
         # per-layer conditioner outputs [s_hat | t] (compute dtype): the backward recomputes
         # s = scale * tanh(s_hat) from them instead of reading a saved fp32 s
