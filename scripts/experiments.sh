@@ -68,6 +68,12 @@ case $name in
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$gr -o step --output-format csv -- \
         python3 bench.py --steps 10 --warmup 3 --graph $gr > $O/bench_$gr.json 2> $O/bench_$gr.err || { tail -20 $O/bench_$gr.err; exit 1; }
     done ;;
+  configs)        # north-star config refresh on the current tree (one line per run)
+    for args in "--config 0 --batch 128" "--config 0 --batch 1024" "--config 2 --batch 32768" "--config 2 --batch 65536" \
+                "--config 4 --batch 8192" "--config 4 --batch 32768" "--config 5 --precision bf16 --batch 32768" "--config 5 --precision fp8 --batch 32768" \
+                "--config 5 --precision bf16 --batch 32768" "--config 5 --precision fp8 --batch 32768"; do
+      timeout -k 10 240 python -m vi_normflows_amd.bench.configs $args >> $O/configs.jsonl 2>> $O/configs.err || { echo "FAIL $args"; tail -20 $O/configs.err; exit 1; }
+    done ;;
   mask_ab)        # forward product with / without the ReLU bitmask output, bitmask vs bf16 read
     for r in 1 2; do
       timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 \

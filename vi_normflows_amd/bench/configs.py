@@ -177,8 +177,13 @@ def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: b
         run = DataParallelRunner(eng, info)
         if graph and dev.type == "cuda":
             run.capture(warmup=2)
-        return run.step, B, dev, (("fp8 e4m3 forward (MX K=128 MFMA) + bf16 backward" if precision == "fp8"
-                                   else "bf16") + ", MAF engine" + (", hipGraph" if run.graph else ""))
+        if precision == "fp8":
+            label = ("fp8 e4m3 forward products (MX K=128 MFMA)"
+                     + (" + e4m3 input gradients" if getattr(eng, "fp8_bwd", False) else "")
+                     + ", bf16 weight gradients")
+        else:
+            label = "bf16"
+        return run.step, B, dev, label + ", MAF engine" + (", hipGraph" if run.graph else "")
     if cfg_id == 5:
         from ..models.maf_density import MAFConfig, MAFDensity, banana_samples
 
@@ -205,8 +210,9 @@ def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: b
             it[0] += 1
             xs.copy_(X[i * B:(i + 1) * B])
             g.replay() if g is not None else compute()
-        return step, B, dev, (("fp8 e4m3 forward (MX K=128 MFMA) + bf16 backward" if precision == "fp8"
-                               else "bf16 (MFMA masked GEMMs)") + (", hipGraph" if use_graph else ""))
+        return step, B, dev, (("fp8 e4m3 forward products (MX K=128 MFMA), bf16 backward (autograd)"
+                               if precision == "fp8" else "bf16 (MFMA masked GEMMs)")
+                              + (", hipGraph" if use_graph else ""))
     raise KeyError(cfg_id)
 
 
