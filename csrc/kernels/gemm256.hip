@@ -191,11 +191,11 @@ __device__ __forceinline__ void vmwait_count(int cnt) {
 template <int NP, bool F8 = false, typename RegionFn>
 __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&acc)[4][8],
                                                  int m0, int n0, int wr, int wc,
-                                                 RegionFn region_of, int lane) {
+                                                 RegionFn region_of, int lane, int tid_in = -1) {
   constexpr int RJ = 8 / NP, RROWS = 16 * RJ, ITS = 8 / NP;
   const int g = lane >> 4, c = lane & 15;
   const int j0 = n0 >> 1, tn = n0 / BN;
-  const int tid = threadIdx.x, f8 = tid & 15, rsub = tid >> 4;
+  const int tid = tid_in >= 0 ? tid_in : (int)threadIdx.x, f8 = tid & 15, rsub = tid >> 4;
   const int ws = f8 >> 3, q = f8 & 7;
   const int jf = j0 + f8 * 8;                                    // first of this thread's 8 features
   const bool fok = jf < a.cf_dh;
@@ -593,7 +593,12 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
 
   // ---------------------------------------------------------------- epilogue
   // acc[i][j]: n = n0 + wc*64 + i*16 + (lane>>4)*4 + r, m = m0 + wr*128 + j*16 + (lane&15)
-  const int g = lane >> 4, c = lane & 15;
+  // lane-derived epilogue offsets from an opaque zero, so they are computed here: hoisted
+  // above the K loop they stayed live across it at the 256-VGPR limit and were spilled
+  int zt;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(zt));
+  const int lane_e = lane + zt, tid_e = (int)threadIdx.x + zt;
+  const int g = lane_e >> 4, c = lane_e & 15;
   if (do_db && a.dbias != nullptr) {   // dbs[h]: m = wr*128 + h*64 + wc*16 + (lane & 15)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -609,7 +614,7 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
     // e4m3 operands: two 64-row passes (half the x rows in flight) - the F8 main loop leaves
     // fewer registers, and one pass spilled (scratch 120 B/lane)
     epi_coupling_fwd<F8 ? 2 : 1, F8>(a, acc, m0, n0, wr, wc,
-                                     [&](int w) { return smem + w * 16384; }, lane);
+                                     [&](int w) { return smem + w * 16384; }, lane_e, tid_e);
 #ifdef NF_G256_STAMPS
     NF_STAMP(3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -621,10 +626,10 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
     barrier();  // every wave is past its last operand read; each wave reuses 16 KiB of LDS
     if constexpr (BSPLIT)
       epi_tile_staged<EPI, 8, F8, 0, 8, true>(a, acc, m0 + wr * 128, n0 + wc * 32, split,
-                                              smem + wave * 16384, lane);
+                                              smem + wave * 16384, lane_e);
     else
       epi_tile_staged<EPI, 8, F8>(a, acc, m0 + wr * 128, n0 + wc * 64, split,
-                                  smem + wave * 16384, lane);
+                                  smem + wave * 16384, lane_e);
 #ifdef NF_G256_STAMPS
     NF_STAMP(3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -857,20 +862,25 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
     const int fs = (4 * (T - 1) + 2) & (NSLOT - 1);   // free slot pair of the last K-tile
     char* region = wave < 4 ? smem + fs * HALF_BYTES + wave * 8192
                             : smem + NSLOT * HALF_BYTES + (wave - 4) * 8192;
+    // the epilogue's lane-derived offsets from an opaque per-tile zero: hoisted above the tile
+    // loop they stayed live across the MFMA loop at the 256-VGPR limit and were spilled
+    int zt;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(zt));
+    const int lane_e = lane + zt, tid_e = (int)threadIdx.x + zt;
     if constexpr (EPI == EPI_CPL_FWD) {
       epi_coupling_fwd<2>(a, acc, m0, n0, wr, wc,
                           [&](int w) {
                             return w < 4 ? smem + fs * HALF_BYTES + w * 8192
                                          : smem + NSLOT * HALF_BYTES + (w - 4) * 8192;
                           },
-                          lane);
+                          lane_e, tid_e);
     } else if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK) {
       epi_tile_staged<EPI, 4, false, 0, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, 0, region, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own readback done before re-staging
       epi_tile_staged<EPI, 4, false, 4, 8>(a, acc, m0 + wr * 128 + 64, n0 + wc * 64, 0, region,
                                            lane);
     } else {
-      epi_tile_staged<EPI, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, 0, region, lane);
+      epi_tile_staged<EPI, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, 0, region, lane_e);
     }
     // the next tile's six halves (and this epilogue's stores) retired, and every wave's staging
     // reads done before the stream restages the slot pair

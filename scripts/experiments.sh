@@ -74,6 +74,24 @@ case $name in
                 "--config 5 --precision bf16 --batch 32768" "--config 5 --precision fp8 --batch 32768"; do
       timeout -k 10 240 python -m vi_normflows_amd.bench.configs $args >> $O/configs.jsonl 2>> $O/configs.err || { echo "FAIL $args"; tail -20 $O/configs.err; exit 1; }
     done ;;
+  lib_ab)         # default library vs a variant build (arg: variant name): GEMM tests on the
+                  # default, then per-product, headline and config-5 timings, alternating
+    v=$1; L=vi_normflows_amd/_native/libvinf_hip_$v.so
+    timeout -k 10 600 python -u -m pytest tests/test_gemm_gpu.py tests/test_gemm_persistent_gpu.py tests/test_realnvp_engine.py tests/test_maf_engine.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
+    tail -1 $O/pytest.txt
+    for r in 1 2; do
+      for lib in default $v; do
+        if [ $lib = default ]; then unset VINF_NATIVE_LIB; else export VINF_NATIVE_LIB=$L; fi
+        VINF_BENCH_TAG=$lib timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l2,cpl_fwd,dgrad_l2,cpl_bwd >> $O/sg.jsonl || exit 1
+        timeout -k 10 240 python bench.py --steps 20 --warmup 5 > $O/b.json 2> $O/b.err || { tail -20 $O/b.err; exit 1; }
+        python -c "import json;d=json.load(open('$O/b.json'));print(json.dumps({'lib':'$lib','ms':d['ms_per_step'],'F':d['notes']['final_free_energy']}))" >> $O/bench.jsonl
+        for pr in bf16 fp8; do
+          timeout -k 10 240 python -m vi_normflows_amd.bench.configs --config 5 --precision $pr --batch 32768 > $O/c.json 2>> $O/c.err || { tail -20 $O/c.err; exit 1; }
+          python -c "import json;d=json.load(open('$O/c.json'));print(json.dumps({'lib':'$lib','prec':'$pr','ms':d['ms_per_step'],'sps':d['samples_per_s']}))" >> $O/cfg5.jsonl
+        done
+      done
+    done
+    unset VINF_NATIVE_LIB ;;
   mask_ab)        # forward product with / without the ReLU bitmask output, bitmask vs bf16 read
     for r in 1 2; do
       timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 \
