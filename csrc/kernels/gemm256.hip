@@ -597,7 +597,7 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
   // above the K loop they stayed live across it at the 256-VGPR limit and were spilled
   int zt;
   asm volatile("s_mov_b32 %0, 0" : "=s"(zt));
-  const int lane_e = lane + zt, tid_e = (int)threadIdx.x + zt;
+  const int lane_e = lane + zt, tid_e = wave * 64 + lane_e;   // not v0: keeps it dead
   const int g = lane_e >> 4, c = lane_e & 15;
   if (do_db && a.dbias != nullptr) {   // dbs[h]: m = wr*128 + h*64 + wc*16 + (lane & 15)
 #pragma unroll
@@ -866,7 +866,7 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
     // loop they stayed live across the MFMA loop at the 256-VGPR limit and were spilled
     int zt;
     asm volatile("s_mov_b32 %0, 0" : "=s"(zt));
-    const int lane_e = lane + zt, tid_e = (int)threadIdx.x + zt;
+    const int lane_e = lane + zt, tid_e = wave * 64 + lane_e;   // not v0: keeps it dead
     if constexpr (EPI == EPI_CPL_FWD) {
       epi_coupling_fwd<2>(a, acc, m0, n0, wr, wc,
                           [&](int w) {
