@@ -68,6 +68,14 @@ case $name in
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$gr -o step --output-format csv -- \
         python3 bench.py --steps 10 --warmup 3 --graph $gr > $O/bench_$gr.json 2> $O/bench_$gr.err || { tail -20 $O/bench_$gr.err; exit 1; }
     done ;;
+  pmc_step)       # per-kernel counters of the headline step (graph off): two passes, each within
+                  # the per-block slot limits (8 SQ, 4 TCC, 2 GRBM), then one merged summary
+    export TMPDIR=/tmp
+    timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES TCC_HIT_sum TCC_MISS_sum \
+      -d $O/p1 -o step --output-format csv -- python3 bench.py --steps 3 --warmup 2 --graph off > $O/p1.log 2>&1 || { tail -20 $O/p1.log; exit 1; }
+    timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS \
+      -d $O/p2 -o step --output-format csv -- python3 bench.py --steps 3 --warmup 2 --graph off > $O/p2.log 2>&1 || { tail -20 $O/p2.log; exit 1; }
+    python3 -m vi_normflows_amd.bench.pmc_summary $O/p1 $O/p2 > $O/summary.txt && cat $O/summary.txt ;;
   configs)        # north-star config refresh on the current tree (one line per run)
     for args in "--config 0 --batch 128" "--config 0 --batch 1024" "--config 2 --batch 32768" "--config 2 --batch 65536" \
                 "--config 4 --batch 8192" "--config 4 --batch 32768" "--config 5 --precision bf16 --batch 32768" "--config 5 --precision fp8 --batch 32768" \
