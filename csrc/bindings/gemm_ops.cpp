@@ -212,11 +212,26 @@ void gemm_tn_group(at::TensorList dy, at::TensorList x, at::TensorList dW,
 
 // Many dense weight gradients, one whole 256x256 tile per block, no split-K: computes the
 // tiles [tile0, tile0 + ntiles) of the problem list (tiles numbered problem after problem).
-void gemm_tn_multi(at::TensorList dy, at::TensorList x, at::TensorList dW,
-                   const c10::List<c10::optional<at::Tensor>>& db, int64_t tile0, int64_t ntiles,
-                   const c10::List<c10::optional<at::Tensor>>& tiles,
-                   const c10::List<c10::optional<at::Tensor>>& cmask) {
+// f8_scales (e4m3 operands): one fp32 pool, dy / x of problem p dequantised by
+// f8_scales[sa_idx[p]] / f8_scales[sb_idx[p]]
+static void gemm_tn_multi_impl(at::TensorList dy, at::TensorList x, at::TensorList dW,
+                               const c10::List<c10::optional<at::Tensor>>& db, int64_t tile0,
+                               int64_t ntiles, const c10::List<c10::optional<at::Tensor>>& tiles,
+                               const c10::List<c10::optional<at::Tensor>>& cmask,
+                               const at::Tensor* f8_scales, at::IntArrayRef sa_idx,
+                               at::IntArrayRef sb_idx) {
   const size_t n = dy.size();
+  const bool f8 = f8_scales != nullptr;
+  const auto odt = f8 ? at::kFloat8_e4m3fn : at::kBFloat16;
+  if (f8) {
+    TORCH_CHECK(f8_scales->is_cuda() && f8_scales->scalar_type() == at::kFloat &&
+                    f8_scales->is_contiguous() && sa_idx.size() == n && sb_idx.size() == n,
+                "gemm_tn_multi_f8: fp32 scale pool and one (sa, sb) index pair per problem");
+    for (size_t p = 0; p < n; ++p)
+      TORCH_CHECK(sa_idx[p] >= 0 && sb_idx[p] >= 0 && sa_idx[p] < f8_scales->numel() &&
+                      sb_idx[p] < f8_scales->numel() && sb_idx[p] <= 0x7fff,
+                  "gemm_tn_multi_f8: scale index outside the pool");
+  }
   TORCH_CHECK(n >= 1 && n <= 40 && x.size() == n && dW.size() == n && db.size() == n,
               "gemm_tn_multi: 1..40 problems with matching lists");
   TORCH_CHECK((tiles.size() == 0 || tiles.size() == n) && (cmask.size() == 0 || cmask.size() == n),
@@ -224,13 +239,17 @@ void gemm_tn_multi(at::TensorList dy, at::TensorList x, at::TensorList dW,
   std::vector<NfTnProblem> pr(n);
   long total = 0;
   for (size_t p = 0; p < n; ++p) {
-    chk_mat(dy[p], "dy", at::kBFloat16);
-    chk_mat(x[p], "x", at::kBFloat16);
+    chk_mat(dy[p], "dy", odt);
+    chk_mat(x[p], "x", odt);
     chk_mat(dW[p], "dW", at::kFloat);
     const int K = dy[p].size(0), M = dy[p].size(1), N = x[p].size(1);
     TORCH_CHECK(x[p].size(0) == K, "batch mismatch");
     TORCH_CHECK(dW[p].size(0) == M && dW[p].size(1) == N, "dW shape");
     TORCH_CHECK(K % 32 == 0 && M % 8 == 0 && N % 8 == 0, "K % 32, M % 8, N % 8 required");
+    TORCH_CHECK(!f8 || (K % 128 == 0 && M % 16 == 0 && N % 16 == 0 && ld2(dy[p]) % 16 == 0 &&
+                        ld2(x[p]) % 16 == 0 && ld2(dW[p]) % 4 == 0 &&
+                        ((uintptr_t)dW[p].data_ptr() & 15) == 0),
+                "gemm_tn_multi_f8: K % 128, M / N / ld % 16, 16-B aligned dW");
     TORCH_CHECK(ld2(dy[p]) < (1L << 31) && ld2(x[p]) < (1L << 31) && ld2(dW[p]) < (1L << 31),
                 "leading dimensions must fit in int32");
     float* dbp = nullptr;
@@ -241,6 +260,10 @@ void gemm_tn_multi(at::TensorList dy, at::TensorList x, at::TensorList dW,
     }
     pr[p] = NfTnProblem{dy[p].data_ptr(), ld2(dy[p]), x[p].data_ptr(), ld2(x[p]),
                         dW[p].data_ptr<float>(), ld2(dW[p]), dbp, M, N, K};
+    if (f8) {
+      pr[p].sa_idx = (int)sa_idx[p];
+      pr[p].sb_idx = (int)sb_idx[p];
+    }
     int nt = nf_gemm256_tiles(M, N);
     if (tiles.size() == n) {
       const c10::optional<at::Tensor> tl = tiles.get(p);
@@ -264,7 +287,55 @@ void gemm_tn_multi(at::TensorList dy, at::TensorList x, at::TensorList dW,
   }
   TORCH_CHECK(tile0 >= 0 && ntiles >= 1 && tile0 + ntiles <= total, "tile range outside the ",
               total, " tiles of the problem list");
-  nf_launch_gemm256_tn_multi((int)n, pr.data(), (int)tile0, (int)ntiles, cur_stream());
+  nf_launch_gemm256_tn_multi((int)n, pr.data(), (int)tile0, (int)ntiles, cur_stream(),
+                             f8 ? f8_scales->data_ptr<float>() : nullptr);
+}
+
+void gemm_tn_multi(at::TensorList dy, at::TensorList x, at::TensorList dW,
+                   const c10::List<c10::optional<at::Tensor>>& db, int64_t tile0, int64_t ntiles,
+                   const c10::List<c10::optional<at::Tensor>>& tiles,
+                   const c10::List<c10::optional<at::Tensor>>& cmask) {
+  gemm_tn_multi_impl(dy, x, dW, db, tile0, ntiles, tiles, cmask, nullptr, {}, {});
+}
+
+// e4m3 weight gradients (dy, x: float8_e4m3fn [K = batch][M / N], per-tensor delayed scales)
+void gemm_tn_multi_f8(at::TensorList dy, at::TensorList x, at::TensorList dW,
+                      const c10::List<c10::optional<at::Tensor>>& db, int64_t tile0,
+                      int64_t ntiles, const c10::List<c10::optional<at::Tensor>>& tiles,
+                      const c10::List<c10::optional<at::Tensor>>& cmask, const at::Tensor& scales,
+                      at::IntArrayRef sa_idx, at::IntArrayRef sb_idx) {
+  gemm_tn_multi_impl(dy, x, dW, db, tile0, ntiles, tiles, cmask, &scales, sa_idx, sb_idx);
+}
+
+// s * column sums of e4m3 [K][N] tensors (bias gradients of the e4m3 weight gradients)
+void fp8_colsum(at::TensorList q, at::TensorList out, const at::Tensor& scales,
+                at::IntArrayRef sidx, const at::Tensor& part) {
+  const size_t n = q.size();
+  TORCH_CHECK(n >= 1 && n <= 40 && out.size() == n && sidx.size() == n,
+              "fp8_colsum: 1..40 tensors with matching lists");
+  TORCH_CHECK(scales.is_cuda() && scales.scalar_type() == at::kFloat && scales.is_contiguous(),
+              "fp8_colsum: fp32 scale pool");
+  std::vector<const void*> qp(n);
+  std::vector<long> ld(n);
+  std::vector<int> K(n), N(n), si(n);
+  std::vector<float*> op(n);
+  for (size_t i = 0; i < n; ++i) {
+    chk_mat(q[i], "q", at::kFloat8_e4m3fn);
+    K[i] = (int)q[i].size(0);
+    N[i] = (int)q[i].size(1);
+    TORCH_CHECK(out[i].is_cuda() && out[i].scalar_type() == at::kFloat && out[i].is_contiguous() &&
+                    out[i].numel() == N[i], "fp8_colsum: out[i] fp32 [N]");
+    TORCH_CHECK(sidx[i] >= 0 && sidx[i] < scales.numel(), "fp8_colsum: scale index");
+    qp[i] = q[i].data_ptr();
+    ld[i] = ld2(q[i]);
+    op[i] = out[i].data_ptr<float>();
+    si[i] = (int)sidx[i];
+  }
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
+                  part.numel() >= nf_fp8_colsum_workspace((int)n, N.data()),
+              "fp8_colsum: part workspace too small");
+  nf_launch_fp8_colsum((int)n, qp.data(), ld.data(), K.data(), N.data(), op.data(), si.data(),
+                       scales.data_ptr<float>(), part.data_ptr<float>(), cur_stream());
 }
 
 // Last conditioner product of coupling layer l with the layer's coupling forward in the epilogue:
@@ -460,7 +531,7 @@ void chk_scales(const c10::optional<at::Tensor>& sa, const c10::optional<at::Ten
 // masked input gradient on e4m3 operands with the ReLU-mask epilogue (gemm256.hip
 // nf_launch_gemm256_fp8_dgrad): dx = relu'(h) * (dyq sa)(Wtq sb)^T (bf16) + optional e4m3 dxq
 void fp8_dgrad(const at::Tensor& dyq, const at::Tensor& sa, const at::Tensor& Wtq,
-               const at::Tensor& sb, const at::Tensor& h, const at::Tensor& dx,
+               const at::Tensor& sb, const at::Tensor& h, const c10::optional<at::Tensor>& dx_opt,
                const at::Tensor& krange256, const c10::optional<at::Tensor>& dxq,
                const c10::optional<at::Tensor>& q_amax_prev,
                const c10::optional<at::Tensor>& q_scale,
@@ -468,10 +539,16 @@ void fp8_dgrad(const at::Tensor& dyq, const at::Tensor& sa, const at::Tensor& Wt
   chk_q(dyq, "dyq");
   chk_q(Wtq, "Wtq");
   chk_mat(h, "h", at::kBFloat16);
-  chk_mat(dx, "dx", at::kBFloat16);
   const int M = dyq.size(0), K = dyq.size(1), N = Wtq.size(0);
   TORCH_CHECK(Wtq.size(1) == K && K % 128 == 0 && N % 8 == 0, "Wtq [N, K], K % 128 == 0");
-  TORCH_CHECK(h.size(0) == M && h.size(1) == N && dx.size(0) == M && dx.size(1) == N, "h / dx");
+  TORCH_CHECK(h.size(0) == M && h.size(1) == N, "h");
+  // dx (bf16) may be omitted when only its e4m3 copy dxq is consumed
+  const bool has_dx = dx_opt && dx_opt->defined();
+  TORCH_CHECK(has_dx || (dxq && dxq->defined()), "fp8_dgrad: dx and / or dxq");
+  if (has_dx) {
+    chk_mat(*dx_opt, "dx", at::kBFloat16);
+    TORCH_CHECK(dx_opt->size(0) == M && dx_opt->size(1) == N, "dx");
+  }
   chk_scales(sa, sb, N);
   const long nt = (N + 255) / 256;
   const int segs = krange256.numel() == 4 * nt ? 2 : 1;
@@ -479,13 +556,15 @@ void fp8_dgrad(const at::Tensor& dyq, const at::Tensor& sa, const at::Tensor& Wt
   const F8Out o = f8_out(dxq, q_amax_prev, q_scale, q_amax_cur, M, N);
   nf_launch_gemm256_fp8_dgrad(dyq.data_ptr(), ld2(dyq), sa.data_ptr<float>(), Wtq.data_ptr(),
                               ld2(Wtq), sb.data_ptr<float>(), h.data_ptr(), ld2(h), 0,
-                              dx.data_ptr(), ld2(dx), M, N, K, krange256.data_ptr<int>(), segs,
+                              has_dx ? dx_opt->data_ptr() : nullptr, has_dx ? ld2(*dx_opt) : N,
+                              M, N, K, krange256.data_ptr<int>(), segs,
                               o.q, o.ldq, o.ap, o.qs, o.ac, cur_stream());
 }
 
 void maf_gemm_bwd(const at::Tensor& dy, const at::Tensor& Wt, const at::Tensor& krange256,
                   const at::Tensor& G, const at::Tensor& s_raw, const at::Tensor& u,
-                  const at::Tensor& dst, const at::Tensor& gx, double bound, double c,
+                  const c10::optional<at::Tensor>& dst_opt, const at::Tensor& gx, double bound,
+                  double c,
                   const c10::optional<at::Tensor>& sa, const c10::optional<at::Tensor>& sb,
                   const c10::optional<at::Tensor>& dstq,
                   const c10::optional<at::Tensor>& q_amax_prev,
@@ -502,7 +581,10 @@ void maf_gemm_bwd(const at::Tensor& dy, const at::Tensor& Wt, const at::Tensor& 
     TORCH_CHECK(!(dstq && dstq->defined()), "the e4m3 copy of dst belongs to the fp8 path");
   }
   chk_mat(s_raw, "s_raw", at::kBFloat16);
-  chk_mat(dst, "dst", at::kBFloat16);
+  // dst (bf16) may be omitted on the e4m3 path when only its e4m3 copy dstq is consumed
+  const bool has_dst = dst_opt && dst_opt->defined();
+  TORCH_CHECK(has_dst || (f8 && dstq && dstq->defined()), "maf_gemm_bwd: dst and / or dstq");
+  if (has_dst) chk_mat(*dst_opt, "dst", at::kBFloat16);
   chk_mat(G, "G", at::kFloat);
   chk_mat(u, "u", at::kFloat);
   chk_mat(gx, "gx", at::kFloat);
@@ -510,7 +592,8 @@ void maf_gemm_bwd(const at::Tensor& dy, const at::Tensor& Wt, const at::Tensor& 
   TORCH_CHECK(Wt.size(1) == K && K % 32 == 0 && D % 8 == 0, "Wt must be [D, K], K % 32 == 0");
   for (const at::Tensor* t : {&G, &s_raw, &u, &gx})
     TORCH_CHECK(t->size(0) == M && t->size(1) == D, "G / s_raw / u / gx: [M, D]");
-  TORCH_CHECK(dst.size(0) == M && dst.size(1) == 2 * D, "dst: bf16 [M, 2D]");
+  TORCH_CHECK(!has_dst || (dst_opt->size(0) == M && dst_opt->size(1) == 2 * D),
+              "dst: bf16 [M, 2D]");
   const long nt = (D + 255) / 256;
   const int segs = krange256.numel() == 4 * nt ? 2 : 1;
   chk_ranges(krange256, segs * nt, "krange256");
@@ -524,7 +607,8 @@ void maf_gemm_bwd(const at::Tensor& dy, const at::Tensor& Wt, const at::Tensor& 
   }
   nf_launch_gemm256_nn_cpl(dy.data_ptr(), ld2(dy), Wt.data_ptr(), ld2(Wt), G.data_ptr<float>(),
                            ld2(G), M, D, K, s_raw.data_ptr(), ld2(s_raw), u.data_ptr<float>(),
-                           ld2(u), dst.data_ptr(), ld2(dst), 2 * D, gx.data_ptr<float>(), ld2(gx),
+                           ld2(u), has_dst ? dst_opt->data_ptr() : nullptr,
+                           has_dst ? ld2(*dst_opt) : 2 * D, 2 * D, gx.data_ptr<float>(), ld2(gx),
                            D, (float)bound, (float)c, cur_stream(), 1, krange256.data_ptr<int>(),
                            segs, 1, f8 ? &fo : nullptr);
 }
@@ -901,11 +985,13 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db) -> ()");
   m.def("gemm_tn_group(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, Tensor?[] skip, Tensor?[] cmask) -> ()");
   m.def("gemm_tn_multi(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles, Tensor?[] tiles, Tensor?[] cmask) -> ()");
+  m.def("fp8_colsum(Tensor[] q, Tensor(a!)[] out, Tensor scales, int[] sidx, Tensor(b!) part) -> ()");
+  m.def("gemm_tn_multi_f8(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles, Tensor?[] tiles, Tensor?[] cmask, Tensor scales, int[] sa_idx, int[] sb_idx) -> ()");
   m.def("gemm_nt_cpl(Tensor h, Tensor W, Tensor? b, Tensor(a!) st, Tensor x, Tensor(b!) y, Tensor(c!)? yb, Tensor(d!) ldjp, bool ldj_init, float scale) -> ()");
   m.def("gemm_nn_cpl(Tensor dy, Tensor W, Tensor G, Tensor s_hat, Tensor x, Tensor(a!) dst, Tensor(b!) gx, float scale, float c, Tensor? Wt=None) -> ()");
   m.def("maf_gemm_fwd(Tensor h, Tensor? hs, Tensor W, Tensor? ws, Tensor? b, Tensor krange, Tensor(a!) s_out, Tensor x, Tensor(b!) u, Tensor(c!)? ubf, Tensor(d!) ldjp, bool ldj_init, float bound, Tensor(e!)? uq=None, Tensor? q_amax_prev=None, Tensor(f!)? q_scale=None, Tensor(g!)? q_amax_cur=None) -> ()");
-  m.def("maf_gemm_bwd(Tensor dy, Tensor Wt, Tensor krange256, Tensor G, Tensor s_raw, Tensor u, Tensor(a!) dst, Tensor(b!) gx, float bound, float c, Tensor? sa=None, Tensor? sb=None, Tensor(c!)? dstq=None, Tensor? q_amax_prev=None, Tensor(d!)? q_scale=None, Tensor(e!)? q_amax_cur=None) -> ()");
-  m.def("fp8_dgrad(Tensor dyq, Tensor sa, Tensor Wtq, Tensor sb, Tensor h, Tensor(a!) dx, Tensor krange256, Tensor(b!)? dxq=None, Tensor? q_amax_prev=None, Tensor(c!)? q_scale=None, Tensor(d!)? q_amax_cur=None) -> ()");
+  m.def("maf_gemm_bwd(Tensor dy, Tensor Wt, Tensor krange256, Tensor G, Tensor s_raw, Tensor u, Tensor(a!)? dst, Tensor(b!) gx, float bound, float c, Tensor? sa=None, Tensor? sb=None, Tensor(c!)? dstq=None, Tensor? q_amax_prev=None, Tensor(d!)? q_scale=None, Tensor(e!)? q_amax_cur=None) -> ()");
+  m.def("fp8_dgrad(Tensor dyq, Tensor sa, Tensor Wtq, Tensor sb, Tensor h, Tensor(a!)? dx, Tensor krange256, Tensor(b!)? dxq=None, Tensor? q_amax_prev=None, Tensor(c!)? q_scale=None, Tensor(d!)? q_amax_cur=None) -> ()");
   m.def("fp8_quant_rows_strided(Tensor x, int layer_stride, int rows_per, int layers, int C, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("maf_fwd(Tensor x, Tensor o, float bound, Tensor(a!) u, Tensor(b!)? ubf, Tensor(c!)? uq, Tensor? amax_prev, Tensor(d!)? scale, Tensor(e!)? amax_cur, Tensor(f!) ldj, bool ldj_init) -> ()");
   m.def("iaf_gate_fwd(Tensor o, Tensor z, float gate_bias, Tensor(a!) y, Tensor(b!) ldj, "
@@ -924,6 +1010,8 @@ TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
   m.impl("gemm_tn", &gemm_tn);
   m.impl("gemm_tn_group", &gemm_tn_group);
   m.impl("gemm_tn_multi", &gemm_tn_multi);
+  m.impl("gemm_tn_multi_f8", &gemm_tn_multi_f8);
+  m.impl("fp8_colsum", &fp8_colsum);
   m.impl("gemm_nn_cpl", &gemm_nn_cpl);
   m.impl("gemm_nt_cpl", &gemm_nt_cpl);
   m.impl("fp8_quant_rows", &fp8_quant_rows);

@@ -153,6 +153,35 @@ struct GroupArgs {
 
 __device__ __forceinline__ int mn_swz(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
 
+// e4m3 mn-major half-tile image: 128 k-rows x 128 m-bytes, 16-B chunk cm of k-row k at chunk
+// position cm ^ f8mn_swz(k). A ds_read_b64_tr_b8 32-lane half reads one chunk column of 8
+// k-rows per 16-lane group, the two groups 16 k-rows apart: (k & 1, chunk position) is then
+// distinct over those 16 rows, i.e. the 32 lanes cover 64 distinct banks (conflict-free).
+__device__ __forceinline__ int f8mn_swz(int k) { return ((k >> 1) & 3) | (((k >> 4) & 1) << 2); }
+
+// e4m3 fragment of the scaled 16x16x128 MFMA from an mn-major image: 16 k-bytes
+// [64 ks + 16 g, +16) of tile row r0 + (lane & 15), g = lane >> 4 - the k-set the k-major
+// read_frag gives a lane, so A and B fragments of either layout pair up. Two
+// ds_read_b64_tr_b8: per 16-lane group, lane 2q + p points at k-row kb + q, bytes 8p..8p+7 of
+// the row's chunk; lane i receives byte i of those 8 rows (measured on gfx950:
+// tools/tr8_probe.hip). The ISA needs EXEC all ones: every lane always reads.
+__device__ __forceinline__ v8s read_frag_f8mn(const char* lds_tile, int r0, int ks, int lane) {
+  typedef int v2i_ __attribute__((ext_vector_type(2)));
+  const int g = lane >> 4, q = (lane & 15) >> 1, p = lane & 1, cm = r0 >> 4;
+  int w[4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = ks * 64 + g * 16 + h * 8 + q;
+    const LDS_AS v2i_* ptr =
+        (const LDS_AS v2i_*)(lds_tile + k * 128 + ((cm ^ f8mn_swz(k)) << 4) + p * 8);
+    const v2i_ t = __builtin_amdgcn_ds_read_tr8_b64_v2i32((LDS_AS v2i_*)ptr);
+    w[2 * h] = t[0];
+    w[2 * h + 1] = t[1];
+  }
+  typedef int v4i_ __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(v8s, (v4i_){w[0], w[1], w[2], w[3]});
+}
+
 // 8 consecutive k (k-step ks in {0,1}) for tile row r0 + (lane & 15).
 template <bool KMAJOR>
 __device__ __forceinline__ v8s read_frag(const char* lds_tile, int r0, int ks, int lane) {
@@ -179,6 +208,14 @@ __device__ __forceinline__ v8s read_frag(const char* lds_tile, int r0, int ks, i
     }
     return out;
   }
+}
+
+// bf16 fragments (either layout) and e4m3 fragments (k-major: the same 16-B row read; mn-major:
+// read_frag_f8mn)
+template <bool KMAJOR, bool F8>
+__device__ __forceinline__ v8s read_frag_any(const char* lds_tile, int r0, int ks, int lane) {
+  if constexpr (F8 && !KMAJOR) return read_frag_f8mn(lds_tile, r0, ks, lane);
+  else return read_frag<KMAJOR>(lds_tile, r0, ks, lane);
 }
 
 // Epilogue for one accumulator fragment: 4 consecutive n of output row m.
@@ -386,7 +423,9 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
           const unsigned bits = pos2(o.x) | (pos2(o.y) << 2) | (pos2(o.z) << 4) | (pos2(o.w) << 6);
           a.mask_out[(long)m * a.ld_mask + (n >> 3)] = (unsigned char)bits;
         }
-        *reinterpret_cast<uint4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
+        // (C may be null on the e4m3 paths that only need the e4m3 copy: MAF engine, e4m3
+        // weight gradients)
+        if (a.C) *reinterpret_cast<uint4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
         if (f8out) {
           const unsigned w4[4] = {o.x, o.y, o.z, o.w};
           float f[8];
@@ -428,6 +467,9 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
     // e4m3 operands (EPI_CPL_BWD): acc * f8_sa[0] * f8_sb[n], and with f8_cq the e4m3 copy of
     // dst = [dS | dT] (the next fp8 input-gradient product's operand) under a delayed scale
     constexpr bool f8c = F8 && EPI == EPI_CPL_BWD;
+    // e4m3 weight gradients (EPI_F32): dW = acc * sa * sb, both per-tensor scales
+    float w8 = 1.f;
+    if constexpr (F8 && EPI == EPI_F32) w8 = a.f8_sa[0] * a.f8_sb[0];
     float qinv = 1.f, qamax = 0.f;
     if (f8c && a.f8_cq) {
       const float ap = *a.f8_q_amax_prev;
@@ -480,6 +522,9 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
         if constexpr (f8c) {
           v[0] *= sc8[0]; v[1] *= sc8[1]; v[2] *= sc8[2]; v[3] *= sc8[3];
         }
+        if constexpr (F8 && EPI == EPI_F32) {
+          v[0] *= w8; v[1] *= w8; v[2] *= w8; v[3] *= w8;
+        }
         const int m = m0 + hj * 16 * PJ + row, n = n0 + q * 4 + (SPLITN && q >= 8 ? 96 : 0);
         if (m < a.M && n < a.N) {
           if constexpr (EPI == EPI_CPL_BWD) {
@@ -517,8 +562,10 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
               ushort4 d0, d1;
               d0.x = f2bf(dsh[0]); d0.y = f2bf(dsh[1]); d0.z = f2bf(dsh[2]); d0.w = f2bf(dsh[3]);
               d1.x = f2bf(d1v[0]); d1.y = f2bf(d1v[1]); d1.z = f2bf(d1v[2]); d1.w = f2bf(d1v[3]);
-              *reinterpret_cast<ushort4*>(drow + n) = d0;
-              *reinterpret_cast<ushort4*>(drow + a.cpl_dh + n) = d1;
+              if (a.cpl_dst) {   // null: the e4m3 copy only (MAF engine, e4m3 weight gradients)
+                *reinterpret_cast<ushort4*>(drow + n) = d0;
+                *reinterpret_cast<ushort4*>(drow + a.cpl_dh + n) = d1;
+              }
               if (f8c && a.f8_cq) {
                 float f0[4], f1[4];
 #pragma unroll
@@ -536,7 +583,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
                 *reinterpret_cast<int*>(qr + n) = q0;
                 *reinterpret_cast<int*>(qr + a.cpl_dh + n) = q1;
               }
-            } else if (a.cpl_dh + n < a.cpl_pad) {   // zero the dst pad columns [2 Dh, pad)
+            } else if (a.cpl_dst && a.cpl_dh + n < a.cpl_pad) {   // zero the dst pad columns [2 Dh, pad)
               *reinterpret_cast<ushort4*>(drow + a.cpl_dh + n) = make_ushort4(0, 0, 0, 0);
             }
           } else if (EPI == EPI_F32) {

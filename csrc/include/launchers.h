@@ -80,6 +80,8 @@ struct NfTnProblem {
   // numbering and never written), ntiles_active of them; -1 = every tile
   const unsigned short* tiles = nullptr;
   int ntiles_active = -1;
+  // gemm256_tn_multi e4m3 launches: dy / x dequantisation scales = f8_scales[sa_idx / sb_idx]
+  int sa_idx = -1, sb_idx = -1;
 };
 long nf_gemm_tn_group_workspace(int nprob, const NfTnProblem* pr);
 void nf_launch_gemm_tn_group(int nprob, const NfTnProblem* pr, float* work, hipStream_t stream);
@@ -156,12 +158,18 @@ int nf_launch_gemm256_tn_partials(const void* dy, long lddy, const void* x, long
 // after problem, one launch computes [tile0, tile0 + ntiles)
 int nf_gemm256_tiles(int M, int N);
 void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int ntiles,
-                                hipStream_t stream);
+                                hipStream_t stream, const float* f8_scales = nullptr);
 // mode: 0 auto, 1 force 128x128, 2 force 256x256; depth: half-tiles in flight (3 or 4)
 void nf_gemm_set_mode(int mode, int depth);
 // fp8.hip (OCP e4m3): per-row quantisation and the MX-scaled K=128 MFMA GEMM
 void nf_launch_fp8_quant_rows(const void* x, int x_is_bf16, long ldx, int R, int C, void* q,
                               long ldq, int Cq, float* scale, hipStream_t stream);
+// fp8.hip: deterministic column sums s * sum_k q[k][n] of up to 40 e4m3 [K][N] tensors (the
+// bias gradients of the e4m3 weight-gradient launches); part = nf_fp8_colsum_workspace floats
+long nf_fp8_colsum_workspace(int n, const int* N);
+void nf_launch_fp8_colsum(int n, const void* const* q, const long* ld, const int* K, const int* N,
+                          float* const* out, const int* sidx, const float* scales, float* part,
+                          hipStream_t stream);
 void nf_launch_fp8_quant_tensor(const void* x, int x_is_bf16, long ldx, int R, int C, void* q,
                                 long ldq, int Cq, const float* amax_prev, float* scale_out,
                                 float* amax_cur, hipStream_t stream);

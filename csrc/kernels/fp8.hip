@@ -271,6 +271,77 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_fp8_nt_kernel(Fp8Args a) {
   if (a.Cq) block_amax_atomic(qamax, a.q_amax_cur);
 }
 
+// Column sums of e4m3 [K][N] tensors, s * sum_k q[k][n] (the bias gradients of the e4m3
+// weight-gradient launches, ops/gemm.py WgradPlan): deterministic two-pass. Pass 1: block =
+// (descriptor, 256-column chunk, K slab); 64 threads x 4 columns (one 4-B load per row), 4
+// row groups, the groups folded through LDS in a fixed order -> part[slab][column]. Pass 2: the
+// slabs of each column summed in slab order, times the tensor's scale.
+constexpr int CS_SLABS = 8;
+struct ColsumDesc {
+  const unsigned char* q;
+  long ld;
+  float* out;
+  int K, N, sidx, blk0, col0;   // blk0: first pass-1 block, col0: first column of the part rows
+};
+constexpr int CS_MAX = 40;
+struct ColsumArgs {
+  ColsumDesc d[CS_MAX];
+  int n, ncols;
+  const float* scales;
+  float* part;   // [CS_SLABS][ncols]
+};
+
+__device__ __forceinline__ int cs_desc(const ColsumArgs& a, int b) {
+  int p = 0;
+  for (int i = 1; i < a.n; ++i)
+    if (b >= a.d[i].blk0) p = i;
+  return p;
+}
+
+__global__ void __launch_bounds__(256) colsum_partial_kernel(ColsumArgs a) {
+  __shared__ float red[4][256];
+  const int p = cs_desc(a, blockIdx.x);
+  const ColsumDesc& d = a.d[p];
+  const int local = blockIdx.x - d.blk0;
+  const int chunk = local / CS_SLABS, slab = local % CS_SLABS;
+  const int t = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int n = chunk * 256 + t * 4;
+  const int rows = (d.K + CS_SLABS - 1) / CS_SLABS;
+  const int k0 = slab * rows, k1 = min(d.K, k0 + rows);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (n < d.N) {
+    const unsigned char* col = d.q + n;
+    for (int k = k0 + grp; k < k1; k += 4) {
+      const int w = *reinterpret_cast<const int*>(col + (long)k * d.ld);
+      s0 += __builtin_amdgcn_cvt_f32_fp8(w, 0);
+      s1 += __builtin_amdgcn_cvt_f32_fp8(w, 1);
+      s2 += __builtin_amdgcn_cvt_f32_fp8(w, 2);
+      s3 += __builtin_amdgcn_cvt_f32_fp8(w, 3);
+    }
+  }
+  red[grp][t * 4 + 0] = s0;
+  red[grp][t * 4 + 1] = s1;
+  red[grp][t * 4 + 2] = s2;
+  red[grp][t * 4 + 3] = s3;
+  __syncthreads();
+  const int c = threadIdx.x, nc = chunk * 256 + c;
+  if (nc < d.N)
+    a.part[(long)slab * a.ncols + d.col0 + nc] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+}
+
+__global__ void __launch_bounds__(256) colsum_final_kernel(ColsumArgs a) {
+  const int gc = blockIdx.x * 256 + threadIdx.x;
+  if (gc >= a.ncols) return;
+  int p = 0;
+  for (int i = 1; i < a.n; ++i)
+    if (gc >= a.d[i].col0) p = i;
+  const ColsumDesc& d = a.d[p];
+  float s = 0.f;
+#pragma unroll
+  for (int sl = 0; sl < CS_SLABS; ++sl) s += a.part[(long)sl * a.ncols + gc];
+  d.out[gc - d.col0] = s * a.scales[d.sidx];
+}
+
 }  // namespace fp8
 }  // namespace nf
 
@@ -334,5 +405,39 @@ void nf_launch_gemm_fp8_nt(const void* xq, long ldx, const float* sx, int sx_per
   a.M = M; a.N = N; a.K = K; a.relu = relu; a.krange = krange;
   const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
   hipLaunchKernelGGL(gemm_fp8_nt_kernel, dim3(ntm * ntn), dim3(NTHR), 0, stream, a);
+  NF_HIP_CHECK(hipGetLastError());
+}
+
+long nf_fp8_colsum_workspace(int n, const int* N) {
+  long c = 0;
+  for (int i = 0; i < n; ++i) c += N[i];
+  return c * nf::fp8::CS_SLABS;
+}
+
+void nf_launch_fp8_colsum(int n, const void* const* q, const long* ld, const int* K, const int* N,
+                          float* const* out, const int* sidx, const float* scales, float* part,
+                          hipStream_t stream) {
+  using nf::fp8::ColsumArgs;
+  if (n <= 0) return;
+  if (n > nf::fp8::CS_MAX) {
+    fprintf(stderr, "vinf: fp8_colsum: more than %d tensors\n", nf::fp8::CS_MAX);
+    abort();
+  }
+  ColsumArgs a{};
+  int blk = 0, col = 0;
+  for (int i = 0; i < n; ++i) {
+    if (N[i] % 4 || ld[i] % 4 || ((unsigned long)q[i] & 3)) {
+      fprintf(stderr, "vinf: fp8_colsum: N %% 4, ld %% 4, 4-B aligned rows\n");
+      abort();
+    }
+    auto& d = a.d[i];
+    d.q = (const unsigned char*)q[i]; d.ld = ld[i]; d.out = out[i];
+    d.K = K[i]; d.N = N[i]; d.sidx = sidx[i]; d.blk0 = blk; d.col0 = col;
+    blk += ((N[i] + 255) / 256) * nf::fp8::CS_SLABS;
+    col += N[i];
+  }
+  a.n = n; a.ncols = col; a.scales = scales; a.part = part;
+  hipLaunchKernelGGL(nf::fp8::colsum_partial_kernel, dim3(blk), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(nf::fp8::colsum_final_kernel, dim3((col + 255) / 256), dim3(256), 0, stream, a);
   NF_HIP_CHECK(hipGetLastError());
 }

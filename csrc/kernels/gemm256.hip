@@ -136,6 +136,17 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long
       int gk = k0 + lc * CE;
       gk = gk < K ? gk : K - CE;
       src = (const bf16_t*)((const char*)base + ((long)gr * ld + gk) * EB);
+    } else if constexpr (EB == 1) {
+      // e4m3, mn-major (the fp8 weight gradients, K = batch): a half is 128 k-rows x 128 m-bytes,
+      // 8 k-rows per 1 KiB piece; 16-B chunk cm of k-row kr sits at chunk position
+      // cm ^ f8mn_swz(kr) (the read side, read_frag_f8mn, applies the same involution)
+      const int kr = piece * 8 + (lane >> 3);
+      const int cm = (lane & 7) ^ f8mn_swz(kr);
+      int gk = k0 + kr;
+      gk = gk < K ? gk : K - 1;
+      int gm = row0 + half_row(is_a, hi, cm * 16);
+      gm = gm < rows_total ? gm : rows_total - 16;
+      src = (const bf16_t*)((const char*)base + (long)gk * ld + gm);
     } else {
       const int kr = piece * 4 + (lane >> 4);
       const int lc = (lane & 15) ^ mn_swz(kr);
@@ -443,7 +454,8 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
   // The wave-uniform switch picks the fragment once per half (indexing fa[wc] per instruction
   // compiled to a branch ladder). dbs[h]: partial over this lane's k chunks; lanes are reduced
   // over (lane >> 4) in the epilogue.
-  constexpr bool do_db = DODB;
+  // (e4m3 weight gradients: the bias sums would spill the loop; fp8_colsum computes them)
+  constexpr bool do_db = DODB && !F8;
   v8s fa[4][2], fbl[2][2], fbh[2][2];
   float dbs[2] = {0.f, 0.f};
   auto db_sum = [&](float& sacc, bool two_) {
@@ -528,12 +540,12 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          fbl[i][ks] = read_frag<B_KMAJOR>(slot(t, H_BLO), wc * 32 + i * 16, ks, lane);
+          fbl[i][ks] = read_frag_any<B_KMAJOR, F8>(slot(t, H_BLO), wc * 32 + i * 16, ks, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          fa[j][ks] = read_frag<A_KMAJOR>(slot(t, H_ALO), wr * 64 + j * 16, ks, lane);
+          fa[j][ks] = read_frag_any<A_KMAJOR, F8>(slot(t, H_ALO), wr * 64 + j * 16, ks, lane);
       issue_wait(4 * t + 6 + X, P + 1);
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -547,7 +559,7 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          fbh[i][ks] = read_frag<B_KMAJOR>(slot(t, H_BHI), wc * 32 + i * 16, ks, lane);
+          fbh[i][ks] = read_frag_any<B_KMAJOR, F8>(slot(t, H_BHI), wc * 32 + i * 16, ks, lane);
       issue_wait(4 * t + 7 + X, P + 2);
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -560,7 +572,7 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          fa[j][ks] = read_frag<A_KMAJOR>(slot(t, H_AHI), wr * 64 + j * 16, ks, lane);
+          fa[j][ks] = read_frag_any<A_KMAJOR, F8>(slot(t, H_AHI), wr * 64 + j * 16, ks, lane);
       issue_wait(4 * t + 8 + X, P + 3);
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -976,6 +988,7 @@ struct TnDesc {
   const unsigned short* tiles;   // active tile ids of a masked problem (others never launched)
   const unsigned char* cmask;    // [M][N] 0/1 applied to dW (MADE), or null
   int lda, ldb, ldc, M, N, K, start, staged;
+  int sidx;                      // e4m3 launches: scale-pool indices of dy (low 16 bits) and x
 };
 constexpr int TN_MULTI_MAX = 40;   // 80-B descriptors: the table stays inside the 4 KiB kernarg
 constexpr int TN_PERM_MAX = 256;   // + 512 B: 3724 B of kernarg with 40 descriptors
@@ -986,9 +999,13 @@ struct TnMulti {
   // [x * ntiles/8, (x+1) * ntiles/8) run on XCD x (xcd_remap), so the permutation keeps each
   // problem's tiles - which share A / B panels - inside one XCD's L2 where they fit
   unsigned short perm[TN_PERM_MAX];
+  const float* scales;   // e4m3 launches: per-tensor dequantisation scales, indexed by sidx
 };
+static_assert(sizeof(TnMulti) <= 4096, "TnMulti must fit the 4 KiB kernarg segment");
 
-template <int D>
+// F8: every problem of the launch has e4m3 operands (mn-major, K % 128 == 0, ld in bytes):
+// read through ds_read_b64_tr_b8 (read_frag_f8mn), dW = acc * s_dy * s_x, db = s_dy * row sums
+template <int D, bool F8 = false>
 __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
   __shared__ __attribute__((aligned(16))) char smem[smem_bytes(D)];
   const int pos = xcd_remap(blockIdx.x, t.ntiles);
@@ -1006,8 +1023,12 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
   a.k_per_split = ((d.K + BK - 1) / BK) * BK;
   a.staged = d.staged;
   a.cmask = d.cmask;
+  if constexpr (F8) {
+    a.f8_sa = t.scales + (d.sidx & 0xffff);
+    a.f8_sb = t.scales + (d.sidx >> 16);
+  }
   const int local = d.tiles ? (int)d.tiles[id - d.start] : id - d.start;
-  gemm256_body<false, false, EPI_F32, D, true>(a, local, 0, smem);
+  gemm256_body<false, false, EPI_F32, D, true, F8>(a, local, 0, smem);
 }
 
 // persistent plain products: VINF_G256_PERSIST at load, or nf_gemm256_set_persist (the DP
@@ -1575,9 +1596,11 @@ int nf_gemm256_tiles(int M, int N) {
 // tiles are numbered problem after problem (row-major tiles inside a problem); the launch
 // computes tiles [tile0, tile0 + ntiles) and may start or end inside a problem
 void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int ntiles,
-                                hipStream_t stream) {
+                                hipStream_t stream, const float* f8_scales) {
   if (ntiles <= 0) return;
+  const bool f8 = f8_scales != nullptr;
   g256::TnMulti t{};
+  t.scales = f8_scales;
   int base = 0;
   for (int p = 0; p < nprob; ++p) {
     const NfTnProblem& q = pr[p];
@@ -1586,6 +1609,11 @@ void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int
       if (t.n >= g256::TN_MULTI_MAX) {
         fprintf(stderr, "vinf: gemm256_tn_multi: more than %d problems in one launch\n",
                 g256::TN_MULTI_MAX);
+        abort();
+      }
+      if (f8 && (q.K % 128 || q.M % 16 || q.N % 16 || q.sa_idx < 0 || q.sb_idx < 0 ||
+                 q.sa_idx > 0xffff || q.sb_idx > 0x7fff)) {
+        fprintf(stderr, "vinf: gemm256_tn_multi e4m3: K %% 128, M/N %% 16, scale indices\n");
         abort();
       }
       if (q.skip || q.K % 32 || q.M % 8 || q.N % 8 || (q.cmask && q.lddw != q.N)) {
@@ -1597,14 +1625,19 @@ void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int
       d.A = (const nf::bf16_t*)q.dy; d.lda = (int)q.lddy;
       d.B = (const nf::bf16_t*)q.x; d.ldb = (int)q.ldx;
       d.C = q.dW; d.ldc = (int)q.lddw;
-      d.db = q.db;
+      d.db = f8 ? nullptr : q.db;   // e4m3: bias sums by nf_launch_fp8_colsum
       d.tiles = q.tiles;
       d.cmask = q.cmask;
       d.M = q.M; d.N = q.N; d.K = q.K;
       d.start = base;
+      d.sidx = f8 ? (q.sa_idx | (q.sb_idx << 16)) : 0;
       GemmArgs a{};
       a.C = q.dW; a.ldc = q.lddw; a.N = q.N;
       d.staged = staged_ok(a, EPI_F32);
+      if (f8 && !d.staged) {   // the dequantising epilogue is the staged one
+        fprintf(stderr, "vinf: gemm256_tn_multi e4m3: dW must be 16-B aligned, N %% 4\n");
+        abort();
+      }
     }
     base += tiles;
   }
@@ -1626,7 +1659,10 @@ void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int
     }
     t.use_perm = nf::wgrad_xcd_perm(t.n, seg_lo, seg_n, ntiles, t.perm) ? 1 : 0;
   }
-  if (g256::g_depth == 6)
+  if (f8)
+    hipLaunchKernelGGL((g256::gemm256_multi_kernel<4, true>), dim3(ntiles), dim3(g256::NTHR), 0,
+                       stream, t);
+  else if (g256::g_depth == 6)
     hipLaunchKernelGGL(g256::gemm256_multi_kernel<6>, dim3(ntiles), dim3(g256::NTHR), 0, stream, t);
   else
     hipLaunchKernelGGL(g256::gemm256_multi_kernel<4>, dim3(ntiles), dim3(g256::NTHR), 0, stream, t);

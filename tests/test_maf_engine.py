@@ -216,10 +216,11 @@ def test_engine_fp8_input_gradients(gpu, monkeypatch, dim, hidden, batch):
     data: the loss is the same forward, the gradient differs by the e4m3 rounding of dO / dH /
     (W*M)^T only (3 mantissa bits: ~3 % per product, averaged over the reduction)."""
     cfg = MAFEngineConfig(dim=dim, hidden=hidden, n_layers=4, precision="fp8", init_out_std=0.3)
+    monkeypatch.setenv("VINF_FP8_WGRAD", "0")      # input gradients only (weight gradients: below)
     a = MAFEngine(cfg, batch=batch, device=gpu, seed=4)
     monkeypatch.setenv("VINF_FP8_DGRAD", "0")
     b = MAFEngine(cfg, batch=batch, device=gpu, seed=4)
-    assert a.fp8_bwd and not b.fp8_bwd
+    assert a.fp8_bwd and not b.fp8_bwd and not a.f8_wgrad
     x = torch.randn(batch, dim, generator=torch.Generator().manual_seed(9)).to(gpu)
     for step in range(2):
         for e in (a, b):
@@ -241,3 +242,42 @@ def test_engine_fp8_input_gradients(gpu, monkeypatch, dim, hidden, batch):
         mk = a._mask(l)
         assert (a.params.g(f"l{l}.W1")[mk["M1"] == 0] == 0).all()
         assert (a.params.g(f"l{l}.W2")[mk["M2"] == 0] == 0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim,hidden,batch", [(256, 512, 1024), (1024, 1024, 16384)],
+                         ids=["small", "config5_width"])
+def test_engine_fp8_weight_gradients(gpu, monkeypatch, dim, hidden, batch):
+    """e4m3 weight gradients (per-layer e4m3 copies of x / h / dO / dH, the e4m3 TN multi-layer
+    launch, bias gradients by fp8_colsum) vs the same fp8 engine with bf16 weight gradients:
+    same loss, gradients apart by the e4m3 rounding of the weight-gradient operands only,
+    masked weights' gradients exactly zero, every bias gradient close."""
+    cfg = MAFEngineConfig(dim=dim, hidden=hidden, n_layers=4, precision="fp8", init_out_std=0.3)
+    a = MAFEngine(cfg, batch=batch, device=gpu, seed=4)
+    monkeypatch.setenv("VINF_FP8_WGRAD", "0")
+    b = MAFEngine(cfg, batch=batch, device=gpu, seed=4)
+    assert a.f8_wgrad and b.fp8_bwd and not b.f8_wgrad
+    x = torch.randn(batch, dim, generator=torch.Generator().manual_seed(9)).to(gpu)
+    for step in range(3):
+        for e in (a, b):
+            e.data_override = x
+            e._update_schedule()
+            e.forward()
+            e.backward()
+        torch.cuda.synchronize()
+        if step == 0:   # bootstrap step: bf16 backward in both
+            assert torch.equal(a.params.grad, b.params.grad)
+    assert a.loss.item() == b.loss.item()
+    ga, gb = a.params.grad, b.params.grad
+    assert torch.isfinite(ga).all()
+    rel = ((ga - gb).norm() / gb.norm()).item()
+    print(f"e4m3 weight gradients: relative gradient difference {rel:.4f}")
+    assert rel < 0.08
+    P = a.params
+    for l in range(cfg.n_layers):
+        mk = a._mask(l)
+        assert (P.g(f"l{l}.W1")[mk["M1"] == 0] == 0).all()
+        assert (P.g(f"l{l}.W2")[mk["M2"] == 0] == 0).all()
+        for n in (f"l{l}.b1", f"l{l}.b2"):
+            d = (P.g(n) - b.params.g(n)).norm() / b.params.g(n).norm()
+            assert d.item() < 0.08, (n, d.item())

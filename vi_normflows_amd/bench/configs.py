@@ -180,7 +180,8 @@ def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: b
         if precision == "fp8":
             label = ("fp8 e4m3 forward products (MX K=128 MFMA)"
                      + (" + e4m3 input gradients" if getattr(eng, "fp8_bwd", False) else "")
-                     + ", bf16 weight gradients")
+                     + (" + e4m3 weight gradients" if getattr(eng, "f8_wgrad", False)
+                        else ", bf16 weight gradients"))
         else:
             label = "bf16"
         return run.step, B, dev, label + ", MAF engine" + (", hipGraph" if run.graph else "")

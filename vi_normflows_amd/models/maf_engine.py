@@ -200,23 +200,66 @@ class MAFEngine:
             # scales, against e4m3 (W*M)^T with per-row scales; VINF_FP8_DGRAD=0 keeps bf16
             self.fp8_bwd = self.fuse and os.environ.get("VINF_FP8_DGRAD", "1") != "0"
             self.amax_pool = torch.zeros(4 * L, 1 + AMAX_SLOTS, dtype=f32, device=dev)
-            self.sx = [DelayedScale(dev, self.amax_pool[l]) for l in range(L)]      # input of l
-            self.sh = [DelayedScale(dev, self.amax_pool[L + l]) for l in range(L)]  # hidden of l
-            self.sdo = [DelayedScale(dev, self.amax_pool[2 * L + l]) for l in range(L)]  # dO_l
-            self.sdh = [DelayedScale(dev, self.amax_pool[3 * L + l]) for l in range(L)]  # dH_l
+            # the scales the producers quantise with this step, one pool (the e4m3 weight-
+            # gradient launches index it): input of l, hidden of l, dO_l, dH_l
+            self.f8_scale_pool = torch.ones(4 * L, dtype=f32, device=dev)
+            sp = self.f8_scale_pool
+            self.sx = [DelayedScale(dev, self.amax_pool[l], sp[l:l + 1]) for l in range(L)]
+            self.sh = [DelayedScale(dev, self.amax_pool[L + l], sp[L + l:L + l + 1])
+                       for l in range(L)]
+            self.sdo = [DelayedScale(dev, self.amax_pool[2 * L + l], sp[2 * L + l:2 * L + l + 1])
+                        for l in range(L)]
+            self.sdh = [DelayedScale(dev, self.amax_pool[3 * L + l], sp[3 * L + l:3 * L + l + 1])
+                        for l in range(L)]
             for st in self.sx + self.sh + self.sdo + self.sdh:
                 st.external = True
             self._wq_fresh = False
             self._gscale_ready = False
+            # e4m3 weight gradients (fp8 backward, deferred plan): every layer keeps the e4m3
+            # copies of its four GEMM operands (x, h, dO, dH: 10.7 GB at B = 32768, L = 64), and
+            # the weight gradients of all layers run on the e4m3 TN kernel (WgradPlan f8 form)
+            # instead of the bf16 one over bf16 copies; VINF_FP8_WGRAD=0 keeps bf16
+            self.f8_wgrad = (self.fp8_bwd and self.wgrad_defer
+                             and os.environ.get("VINF_FP8_WGRAD", "1") != "0")
+            self._wplan8 = None
+            if self.f8_wgrad:
+                self.XqL = torch.empty(L, B, D, dtype=e4, device=dev)
+                self.HqL = torch.empty(L, B, H, dtype=e4, device=dev)
+                self.Xq, self.Hq = self.XqL[0], self.HqL[0]
             if self.fp8_bwd:
-                self.dOq = torch.empty(B, 2 * D, dtype=e4, device=dev)
-                self.dHq = torch.empty(B, H, dtype=e4, device=dev)
+                if self.f8_wgrad:
+                    self.dOqL = torch.empty(L, B, 2 * D, dtype=e4, device=dev)
+                    self.dHqL = torch.empty(L, B, H, dtype=e4, device=dev)
+                    self.dOq, self.dHq = self.dOqL[0], self.dHqL[0]
+                else:
+                    self.dOq = torch.empty(B, 2 * D, dtype=e4, device=dev)
+                    self.dHq = torch.empty(B, H, dtype=e4, device=dev)
                 self.W1Tq = torch.empty(L * D, H, dtype=e4, device=dev)
                 self.W2Tq = torch.empty(L * H, 2 * D, dtype=e4, device=dev)
                 self.sW1T = torch.empty(L * D, dtype=f32, device=dev)
                 self.sW2T = torch.empty(L * H, dtype=f32, device=dev)
         else:
             self.fp8_bwd = False
+            self.f8_wgrad = False
+
+    def _lean8(self) -> bool:
+        """Steady fp8 steps with e4m3 weight gradients: the bf16 copies of x, dO and dH have no
+        reader left (the weight gradients read the e4m3 copies), so their producers skip them."""
+        return self.f8_wgrad and self._gscale_ready
+
+    # e4m3 operand copies of layer l: per-layer buffers with e4m3 weight gradients, else the
+    # one buffer each that the next product reads at once
+    def _xq(self, l):
+        return self.XqL[l] if self.f8_wgrad else self.Xq
+
+    def _hq(self, l):
+        return self.HqL[l] if self.f8_wgrad else self.Hq
+
+    def _doq(self, l):
+        return self.dOqL[l] if self.f8_wgrad else self.dOq
+
+    def _dhq(self, l):
+        return self.dHqL[l] if self.f8_wgrad else self.dHq
 
     def init_params(self, seed: int = 0):
         cfg = self.cfg
@@ -284,7 +327,8 @@ class MAFEngine:
         cfg, P = self.cfg, self.params
         D, H, L = cfg.dim, cfg.hidden, cfg.n_layers
         self._sample_data()
-        self.Xbf[0].copy_(self.X[0])
+        if not self._lean8():
+            self.Xbf[0].copy_(self.X[0])
         if self.fp8:
             from ..ops.fp8 import gemm_fp8
 
@@ -293,7 +337,7 @@ class MAFEngine:
             # amax_prev <- max(amax_cur slots), slots <- 0 for every state at once
             torch.amax(self.amax_pool[:, 1:], 1, out=self.amax_pool[:, 0])
             self.amax_pool[:, 1:].zero_()
-            _, sxs = self.sx[0].quantize(self.X[0], out=self.Xq)
+            _, sxs = self.sx[0].quantize(self.X[0], out=self._xq(0))
         if self.fuse:
             return self._forward_fused(sxs if self.fp8 else None)
         for l in range(L):
@@ -351,15 +395,17 @@ class MAFEngine:
             if self.fp8:
                 from ..ops.fp8 import gemm_fp8
 
-                _, sh = gemm_fp8(self.Xq, sxs, self.W1q[l * H:(l + 1) * H],
+                _, sh = gemm_fp8(self._xq(l), sxs, self.W1q[l * H:(l + 1) * H],
                                  self.s1[l * H:(l + 1) * H], b1, relu=True, krange=mk["P1"].fwd,
-                                 out=self.Hbf[l], out_q=self.Hq, out_scale=self.sh[l],
+                                 out=self.Hbf[l], out_q=self._hq(l), out_scale=self.sh[l],
                                  krange256=mk["P1"].fwd256)
                 nxt = None if last else self.sx[l + 1]
-                qargs = (self.Xq, nxt.amax[0:1], nxt.scale, nxt.cur) if nxt is not None else ()
-                native().maf_gemm_fwd(self.Hq, sh, self.W2q[l * 2 * D:(l + 1) * 2 * D],
+                qargs = ((self._xq(l + 1), nxt.amax[0:1], nxt.scale, nxt.cur)
+                         if nxt is not None else ())
+                ubf = None if self._lean8() else self.Xbf[l + 1]
+                native().maf_gemm_fwd(self._hq(l), sh, self.W2q[l * 2 * D:(l + 1) * 2 * D],
                                       self.s2[l * 2 * D:(l + 1) * 2 * D], b2, mk["P2pair"],
-                                      self.S[l], self.X[l], self.X[l + 1], self.Xbf[l + 1],
+                                      self.S[l], self.X[l], self.X[l + 1], ubf,
                                       self.ldjp, l == 0, float(cfg.alpha_bound), *qargs)
                 if nxt is not None:
                     sxs = nxt.scale
@@ -395,6 +441,29 @@ class MAFEngine:
             self._wplan = plan
         return self._wplan
 
+    def _wgrad_plan_f8(self):
+        """The e4m3 form of :meth:`_wgrad_plan`: dW2 = (dOq s_dO)^T (Hq s_h), dW1 = (dHq
+        s_dH)^T (Xq s_x) over the per-layer e4m3 copies, scales by index into the step's scale
+        pool, bias gradients by fp8_colsum; only the not-entirely-masked tiles."""
+        if self._wplan8 is None:
+            P, L = self.params, self.cfg.n_layers
+            items, idx, ends = [], [], []
+            for l in range(L - 1, -1, -1):
+                mk = self._mask(l)
+                items.append((self.dOqL[l], self.HqL[l], P.g(f"l{l}.W2"), P.g(f"l{l}.b2"),
+                              mk["P2"].wtiles256_nz, mk["M2u"]))
+                idx.append((2 * L + l, L + l))
+                items.append((self.dHqL[l], self.XqL[l], P.g(f"l{l}.W1"), P.g(f"l{l}.b1"),
+                              mk["P1"].wtiles256_nz, mk["M1u"]))
+                idx.append((3 * L + l, l))
+                ends.append(len(items) - 1)
+            plan = gemm.WgradPlan(items, f8_scales=self.f8_scale_pool, f8_idx=idx)
+            plan.unit_ends = [(l, plan.end_of(k)) for l, k in zip(range(L - 1, -1, -1), ends)]
+            # tiles left out of the plan are never written: their (masked) gradients stay 0
+            P.grad.zero_()
+            self._wplan8 = plan
+        return self._wplan8
+
     def _weights_t(self):
         """Refresh (W*M)^T of both masked weights of every layer (bf16, one launch): the
         masked input-gradient GEMMs then run NT (see models/realnvp.py ``wt_dgrad``)."""
@@ -428,11 +497,12 @@ class MAFEngine:
 
         cfg, P = self.cfg, self.params
         L = cfg.n_layers
-        plan = self._wgrad_plan()
+        steady8 = self.fp8_bwd and self._gscale_ready
+        plan = self._wgrad_plan_f8() if steady8 and self.f8_wgrad else self._wgrad_plan()
         sched = gemm.WgradScheduler(plan, plan.unit_ends, self._wchunk, self.unit_ready_hook)
         gu, gx = self.gU, self.gX
         WT = self._weights_t() if self.wt_dgrad else None
-        if self.fp8_bwd and self._gscale_ready:
+        if steady8:
             return self._backward_fused_fp8(plan, sched, WT)
         if self.fuse:
             self._backward_fused(plan, sched, WT)
@@ -510,20 +580,25 @@ class MAFEngine:
         fused.maf_bwd(gu, self.X[L], self.S[L - 1], self.dOL[L - 1], gx, bound=cfg.alpha_bound,
                       c_ldj=1.0 / self.B)
         st = self.sdo[L - 1]
-        native().fp8_quant_tensor(self.dOL[L - 1], self.dOq, st.amax[0:1], st.scale, st.cur)
+        native().fp8_quant_tensor(self.dOL[L - 1], self._doq(L - 1), st.amax[0:1], st.scale,
+                                  st.cur)
         bound, c = float(cfg.alpha_bound), 1.0 / self.B
         for k, l in enumerate(range(L - 1, -1, -1)):
             mk = self._mask(l)
             sdo, sdh = self.sdo[l], self.sdh[l]
-            qh = (self.dHq, sdh.amax[0:1], sdh.scale, sdh.cur) if l > 0 else ()
-            native().fp8_dgrad(self.dOq, sdo.scale, self.W2Tq[l * H:(l + 1) * H],
-                               self.sW2T[l * H:(l + 1) * H], self.Hbf[l], self.dHL[l],
-                               mk["P2"].bwd256, *qh)
+            # layer 0's dH feeds only its e4m3 weight gradient
+            qh = ((self._dhq(l), sdh.amax[0:1], sdh.scale, sdh.cur)
+                  if l > 0 or self.f8_wgrad else ())
+            lean = self._lean8()
+            native().fp8_dgrad(self._doq(l), sdo.scale, self.W2Tq[l * H:(l + 1) * H],
+                               self.sW2T[l * H:(l + 1) * H], self.Hbf[l],
+                               None if lean else self.dHL[l], mk["P2"].bwd256, *qh)
             if l > 0:
                 nx = self.sdo[l - 1]
-                native().maf_gemm_bwd(self.dHq, self.W1Tq[l * D:(l + 1) * D], mk["P1"].bwd256, gx,
-                                      self.S[l - 1], self.X[l], self.dOL[l - 1], gu, bound, c,
-                                      sdh.scale, self.sW1T[l * D:(l + 1) * D], self.dOq,
+                native().maf_gemm_bwd(self._dhq(l), self.W1Tq[l * D:(l + 1) * D], mk["P1"].bwd256,
+                                      gx, self.S[l - 1], self.X[l],
+                                      None if lean else self.dOL[l - 1], gu, bound, c,
+                                      sdh.scale, self.sW1T[l * D:(l + 1) * D], self._doq(l - 1),
                                       nx.amax[0:1], nx.scale, nx.cur)
                 gu, gx = gx, gu
             sched.ready(plan.unit_ends[k][1], final=(l == 0))

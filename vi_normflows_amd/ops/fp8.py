@@ -61,7 +61,8 @@ class DelayedScale:
     per-row absmax would couple every output to every input through the scale).
     """
 
-    def __init__(self, device, amax: torch.Tensor | None = None):
+    def __init__(self, device, amax: torch.Tensor | None = None,
+                 scale: torch.Tensor | None = None):
         # amax[0] = the previous call's amax (scale basis); amax[1:] = AMAX_SLOTS partial maxima
         # of the current call (producer blocks fold into slot blockIdx % AMAX_SLOTS, so they do
         # not serialise on one address). ``amax`` may be a [1 + AMAX_SLOTS] row of a pool shared
@@ -70,7 +71,11 @@ class DelayedScale:
         self.amax = amax if amax is not None else torch.zeros(1 + AMAX_SLOTS, device=device,
                                                               dtype=torch.float32)
         assert self.amax.numel() == 1 + AMAX_SLOTS
-        self.scale = torch.ones(1, device=device, dtype=torch.float32)
+        # ``scale`` may be a 1-element view of a pool (the e4m3 weight-gradient launches read
+        # every state's scale from one tensor by index)
+        self.scale = scale if scale is not None else torch.ones(1, device=device,
+                                                                dtype=torch.float32)
+        assert self.scale.numel() == 1
         self.ready = False
         self.external = False
 

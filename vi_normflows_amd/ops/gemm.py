@@ -231,11 +231,25 @@ class WgradPlan:
 
     MAX_PROBLEMS = 40   # kernarg descriptor table of one launch
 
-    def __init__(self, items):
+    def __init__(self, items, f8_scales: torch.Tensor | None = None, f8_idx=None):
         # (dy, x, dW, db) or (dy, x, dW, db, active_tiles, cmask): a masked (MADE) problem lists
         # its not-entirely-masked 256x256 tiles (int16, ops.masked.MaskPlan.wtiles256) and the
-        # dense uint8 mask applied to dW; its other tiles are never computed nor written
+        # dense uint8 mask applied to dW; its other tiles are never computed nor written.
+        # e4m3 plans (f8_scales given): dy / x are float8_e4m3fn [batch, M / N] copies under
+        # per-tensor scales, dy of item p dequantised by f8_scales[f8_idx[p][0]], x by
+        # f8_scales[f8_idx[p][1]]; the weight gradients run on the e4m3 TN kernel
+        # (gemm256_multi_kernel<4, true>) and the bias gradients on fp8_colsum, per launch, for
+        # the problems the launch completes
         self.items = [tuple(i) + (None, None) if len(i) == 4 else tuple(i) for i in items]
+        self.f8 = f8_scales is not None
+        self.f8_scales = f8_scales
+        self.f8_idx = [tuple(int(v) for v in t) for t in f8_idx] if self.f8 else None
+        self._part = None
+        if self.f8:
+            assert len(self.f8_idx) == len(self.items)
+            n_db = sum(int(it[0].shape[1]) for it in self.items if it[3] is not None)
+            self._part = torch.empty(8 * max(n_db, 1), dtype=torch.float32,
+                                     device=self.items[0][0].device)
         self.tiles = [wgrad_tiles(it[0].shape[1], it[1].shape[1]) if it[4] is None else
                       int(it[4].numel()) for it in self.items]
         self.starts = [0]
@@ -256,6 +270,9 @@ class WgradPlan:
         assert 0 <= tile0 and end <= self.total, (tile0, ntiles, self.total)
         first = bisect.bisect_right(self.starts, tile0) - 1
         last = bisect.bisect_left(self.starts, end) - 1        # problem holding tile end-1
+        if self.f8:
+            self._run_f8(tile0, end, first, last)
+            return
         if not all(_mfma_ok(it[0], it[1]) for it in self.items[first:last + 1]):
             for p in range(first, last + 1):
                 if tile0 < self.starts[p + 1] <= end:
@@ -278,6 +295,48 @@ class WgradPlan:
                                    [i[4] for i in ch] if masked else [],
                                    [i[5] for i in ch] if masked else [])
             t = stop
+
+
+    def _f8_deq(self, p: int):
+        dy, x = self.items[p][0], self.items[p][1]
+        sa, sb = self.f8_idx[p]
+        return dy.float() * self.f8_scales[sa], x.float() * self.f8_scales[sb]
+
+    def _run_f8(self, tile0: int, end: int, first: int, last: int) -> None:
+        import bisect
+
+        done = [p for p in range(first, last + 1) if tile0 < self.starts[p + 1] <= end]
+        if getattr(_state, "oracle", False) or not self.items[first][0].is_cuda:
+            # fp32 reference on the dequantised operands (tests): each problem once, when the
+            # range covering its last tile runs
+            for p in done:
+                dy, x = self._f8_deq(p)
+                _, _, dW, db, _, cm = self.items[p]
+                dW.copy_(dy.t() @ x)
+                if cm is not None:
+                    dW.mul_(cm)
+                if db is not None:
+                    db.copy_(dy.sum(0))
+            return
+        from ._ext import native
+
+        t = tile0
+        while t < end:
+            p0 = bisect.bisect_right(self.starts, t) - 1
+            p1 = min(last, p0 + self.MAX_PROBLEMS - 1)
+            stop = min(end, self.starts[p1 + 1])
+            ch = self.items[p0:p1 + 1]
+            idx = self.f8_idx[p0:p1 + 1]
+            native().gemm_tn_multi_f8([i[0] for i in ch], [i[1] for i in ch], [i[2] for i in ch],
+                                      [None] * len(ch), t - self.starts[p0], stop - t,
+                                      [i[4] for i in ch], [i[5] for i in ch], self.f8_scales,
+                                      [a for a, _ in idx], [b for _, b in idx])
+            t = stop
+        dbs = [p for p in done if self.items[p][3] is not None]
+        for k in range(0, len(dbs), self.MAX_PROBLEMS):
+            ps = dbs[k:k + self.MAX_PROBLEMS]
+            native().fp8_colsum([self.items[p][0] for p in ps], [self.items[p][3] for p in ps],
+                                self.f8_scales, [self.f8_idx[p][0] for p in ps], self._part)
 
 
 class WgradScheduler:

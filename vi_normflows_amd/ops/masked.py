@@ -112,6 +112,10 @@ class MaskPlan:
         tn = (m.shape[1] + 255) // 256
         act = [t for t in range(sk.numel()) if not sk[t] or t % tn == 0]
         self.wtiles256 = torch.tensor(act, dtype=torch.int16).to(dev)
+        # e4m3 weight gradients compute the bias gradient separately (fp8_colsum): only the
+        # tiles that are not entirely masked
+        self.wtiles256_nz = torch.tensor([t for t in range(sk.numel()) if not sk[t]],
+                                         dtype=torch.int16).to(dev)
 
 
 _PLANS: dict = {}
