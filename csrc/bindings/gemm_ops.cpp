@@ -538,10 +538,17 @@ void fp8_dgrad(const at::Tensor& dyq, const at::Tensor& sa, const at::Tensor& Wt
                const c10::optional<at::Tensor>& q_amax_cur) {
   chk_q(dyq, "dyq");
   chk_q(Wtq, "Wtq");
-  chk_mat(h, "h", at::kBFloat16);
   const int M = dyq.size(0), K = dyq.size(1), N = Wtq.size(0);
   TORCH_CHECK(Wtq.size(1) == K && K % 128 == 0 && N % 8 == 0, "Wtq [N, K], K % 128 == 0");
-  TORCH_CHECK(h.size(0) == M && h.size(1) == N, "h");
+  // h: the bf16 activation, or its ReLU bitmask (uint8 [M, N/8], bit e of byte n/8 <-> n + e)
+  const bool h_bits = h.scalar_type() == at::kByte;
+  if (h_bits) {
+    TORCH_CHECK(h.is_cuda() && h.dim() == 2 && h.size(0) == M && h.size(1) * 8 >= N &&
+                    h.stride(1) == 1, "h bitmask: uint8 [M, N/8]");
+  } else {
+    chk_mat(h, "h", at::kBFloat16);
+  }
+  TORCH_CHECK(h.size(0) == M && (h_bits || h.size(1) == N), "h");
   // dx (bf16) may be omitted when only its e4m3 copy dxq is consumed
   const bool has_dx = dx_opt && dx_opt->defined();
   TORCH_CHECK(has_dx || (dxq && dxq->defined()), "fp8_dgrad: dx and / or dxq");
@@ -555,7 +562,7 @@ void fp8_dgrad(const at::Tensor& dyq, const at::Tensor& sa, const at::Tensor& Wt
   chk_ranges(krange256, segs * nt, "krange256");
   const F8Out o = f8_out(dxq, q_amax_prev, q_scale, q_amax_cur, M, N);
   nf_launch_gemm256_fp8_dgrad(dyq.data_ptr(), ld2(dyq), sa.data_ptr<float>(), Wtq.data_ptr(),
-                              ld2(Wtq), sb.data_ptr<float>(), h.data_ptr(), ld2(h), 0,
+                              ld2(Wtq), sb.data_ptr<float>(), h.data_ptr(), ld2(h), h_bits ? 1 : 0,
                               has_dx ? dx_opt->data_ptr() : nullptr, has_dx ? ld2(*dx_opt) : N,
                               M, N, K, krange256.data_ptr<int>(), segs,
                               o.q, o.ldq, o.ap, o.qs, o.ac, cur_stream());
@@ -872,17 +879,32 @@ void fp8_quant_tensor(const at::Tensor& x, const at::Tensor& q, const at::Tensor
 
 // y = act((xq * sx) (wq * sw)^T + b) -> bf16; K % 128 == 0; optional MADE krange per 128-row tile
 // sx: [M] per-row or [1] per-tensor
+// y may be omitted (only the e4m3 copy yq and / or the ReLU bitmask mask_out [M][N/8] are
+// consumed: the MAF engine's e4m3 weight-gradient steps); those forms run on the 256 kernel
 void gemm_fp8_nt(const at::Tensor& xq, const at::Tensor& sx, const at::Tensor& wq,
-                 const at::Tensor& sw, const c10::optional<at::Tensor>& b, const at::Tensor& y,
-                 int64_t relu, const c10::optional<at::Tensor>& krange,
+                 const at::Tensor& sw, const c10::optional<at::Tensor>& b,
+                 const c10::optional<at::Tensor>& y_opt, int64_t relu,
+                 const c10::optional<at::Tensor>& krange,
                  const c10::optional<at::Tensor>& yq, const c10::optional<at::Tensor>& q_amax_prev,
                  const c10::optional<at::Tensor>& q_scale, const c10::optional<at::Tensor>& q_amax_cur,
-                 const c10::optional<at::Tensor>& krange256) {
+                 const c10::optional<at::Tensor>& krange256,
+                 const c10::optional<at::Tensor>& mask_out) {
   chk_q(xq, "xq");
   chk_q(wq, "wq");
-  chk_mat(y, "y", at::kBFloat16);
+  const bool has_y = y_opt && y_opt->defined();
+  const bool has_mask = mask_out && mask_out->defined();
   const int M = xq.size(0), K = xq.size(1), N = wq.size(0);
-  TORCH_CHECK(wq.size(1) == K && y.size(0) == M && y.size(1) == N, "shapes");
+  TORCH_CHECK(wq.size(1) == K, "shapes");
+  if (has_y) {
+    chk_mat(*y_opt, "y", at::kBFloat16);
+    TORCH_CHECK(y_opt->size(0) == M && y_opt->size(1) == N, "y shape");
+  }
+  TORCH_CHECK(has_y || (yq && yq->defined()) || has_mask, "gemm_fp8_nt: no output");
+  if (has_mask) {
+    TORCH_CHECK(mask_out->is_cuda() && mask_out->scalar_type() == at::kByte && mask_out->dim() == 2 &&
+                    mask_out->size(0) == M && mask_out->size(1) * 8 >= N && mask_out->stride(1) == 1 &&
+                    relu, "mask_out: uint8 [M, N/8] bitmask of a ReLU product");
+  }
   TORCH_CHECK(K % 128 == 0 && N % 8 == 0, "K % 128 and N % 8 required");
   TORCH_CHECK(sx.is_cuda() && sx.scalar_type() == at::kFloat && (sx.numel() == M || sx.numel() == 1) &&
                   sx.is_contiguous(), "sx [M] or [1]");
@@ -917,8 +939,10 @@ void gemm_fp8_nt(const at::Tensor& xq, const at::Tensor& sx, const at::Tensor& w
   // product has a tile per CU (same rule as the bf16 products)
   const bool dense = !(krange && krange->defined());
   const bool has256 = krange256 && krange256->defined();
-  if ((dense || has256) && nf_gemm_prefer_256(M, N, K) && ld2(xq) % 16 == 0 && ld2(wq) % 16 == 0 &&
-      ld2(y) % 8 == 0 && (!qp || ldq % 8 == 0)) {
+  const long ldy = has_y ? ld2(*y_opt) : N;
+  const bool lean = !has_y || has_mask;
+  if ((dense || has256) && (lean || nf_gemm_prefer_256(M, N, K)) && ld2(xq) % 16 == 0 &&
+      ld2(wq) % 16 == 0 && ldy % 8 == 0 && (!qp || ldq % 8 == 0)) {
     const int* k256 = nullptr;
     if (has256) {
       chk_ranges(*krange256, (N + 255) / 256, "krange256");
@@ -926,13 +950,16 @@ void gemm_fp8_nt(const at::Tensor& xq, const at::Tensor& sx, const at::Tensor& w
     }
     nf_launch_gemm256_fp8_nt(xq.data_ptr(), ld2(xq), sx.data_ptr<float>(),
                              sx.numel() == M && M > 1, wq.data_ptr(), ld2(wq), sw.data_ptr<float>(),
-                             bp, y.data_ptr(), ld2(y), M, N, K, (int)relu, k256, qp, ldq, qap, qs,
-                             qac, cur_stream());
+                             bp, has_y ? y_opt->data_ptr() : nullptr, ldy, M, N, K, (int)relu,
+                             k256, qp, ldq, qap, qs, qac, cur_stream(),
+                             has_mask ? mask_out->data_ptr<uint8_t>() : nullptr,
+                             has_mask ? ld2(*mask_out) : 0);
     return;
   }
+  TORCH_CHECK(!lean, "gemm_fp8_nt: y-less / bitmask forms need the 256 kernel (krange256, 16-B rows)");
   nf_launch_gemm_fp8_nt(xq.data_ptr(), ld2(xq), sx.data_ptr<float>(), sx.numel() == M && M > 1,
                         wq.data_ptr(), ld2(wq),
-                        sw.data_ptr<float>(), bp, y.data_ptr(), ld2(y), M, N, K, (int)relu, kr,
+                        sw.data_ptr<float>(), bp, y_opt->data_ptr(), ldy, M, N, K, (int)relu, kr,
                         qp, ldq, qap, qs, qac, cur_stream());
 }
 
@@ -975,7 +1002,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("gemm_wgrad_xcd_pack(int on) -> int", &gemm_wgrad_xcd_pack);
   m.def("fp8_quant_rows(Tensor x, Tensor(a!) q, Tensor(b!) scale) -> ()");
   m.def("fp8_quant_tensor(Tensor x, Tensor(a!) q, Tensor amax_prev, Tensor(b!) scale, Tensor(c!) amax_cur) -> ()");
-  m.def("gemm_fp8_nt(Tensor xq, Tensor sx, Tensor wq, Tensor sw, Tensor? b, Tensor(a!) y, int relu, Tensor? krange, Tensor(b!)? yq=None, Tensor? q_amax_prev=None, Tensor(c!)? q_scale=None, Tensor(d!)? q_amax_cur=None, Tensor? krange256=None) -> ()");
+  m.def("gemm_fp8_nt(Tensor xq, Tensor sx, Tensor wq, Tensor sw, Tensor? b, Tensor(a!)? y, int relu, Tensor? krange, Tensor(b!)? yq=None, Tensor? q_amax_prev=None, Tensor(c!)? q_scale=None, Tensor(d!)? q_amax_cur=None, Tensor? krange256=None, Tensor(e!)? mask_out=None) -> ()");
   m.def("masked_gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu, Tensor krange, Tensor? krange256=None) -> ()");
   m.def("masked_gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, Tensor krange, bool accumulate=False, Tensor? krange256=None, Tensor? Wt=None) -> ()");
   m.def("masked_gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db, Tensor skip) -> ()");

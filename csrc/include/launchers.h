@@ -187,7 +187,8 @@ void nf_launch_gemm256_fp8_nt(const void* xq, long ldx, const float* sx, int sx_
                               const void* wq, long ldw, const float* sw, const void* bias, void* y,
                               long ldy, int M, int N, int K, int relu, const int* krange,
                               void* yq, long ldyq, const float* q_amax_prev, float* q_scale_out,
-                              float* q_amax_cur, hipStream_t stream);
+                              float* q_amax_cur, hipStream_t stream,
+                              unsigned char* mask_out = nullptr, long ld_mask = 0);
 
 // planar.hip / radial.hip (fused K-layer stacks; per-row parameter gradients)
 void nf_launch_planar_fwd(const float* z, const float* W, const float* U, const float* B, float* zK,

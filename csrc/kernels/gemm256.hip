@@ -1555,9 +1555,11 @@ void nf_launch_gemm256_fp8_nt(const void* xq, long ldx, const float* sx, int sx_
                               const void* wq, long ldw, const float* sw, const void* bias, void* y,
                               long ldy, int M, int N, int K, int relu, const int* krange,
                               void* yq, long ldyq, const float* q_amax_prev, float* q_scale_out,
-                              float* q_amax_cur, hipStream_t stream) {
+                              float* q_amax_cur, hipStream_t stream, unsigned char* mask_out,
+                              long ld_mask) {
   if (M <= 0 || N <= 0) return;
   GemmArgs a{};
+  a.mask_out = mask_out; a.ld_mask = ld_mask;   // ReLU bitmask (y may then be null)
   a.A = (const nf::bf16_t*)xq; a.lda = ldx;
   a.B = (const nf::bf16_t*)wq; a.ldb = ldw;
   a.C = y; a.ldc = ldy;

@@ -225,6 +225,10 @@ class MAFEngine:
             if self.f8_wgrad:
                 self.XqL = torch.empty(L, B, D, dtype=e4, device=dev)
                 self.HqL = torch.empty(L, B, H, dtype=e4, device=dev)
+                # ReLU bitmasks of h (B*H/8 bytes per layer): the steady fp8 backward's
+                # input-gradient epilogue reads them instead of the bf16 h, which is then never
+                # written (only the bf16 bootstrap step needs it)
+                self.MkL = torch.empty(L, B, H // 8, dtype=torch.uint8, device=dev)
                 self.Xq, self.Hq = self.XqL[0], self.HqL[0]
             if self.fp8_bwd:
                 if self.f8_wgrad:
@@ -395,10 +399,12 @@ class MAFEngine:
             if self.fp8:
                 from ..ops.fp8 import gemm_fp8
 
+                lean = self._lean8()
                 _, sh = gemm_fp8(self._xq(l), sxs, self.W1q[l * H:(l + 1) * H],
                                  self.s1[l * H:(l + 1) * H], b1, relu=True, krange=mk["P1"].fwd,
                                  out=self.Hbf[l], out_q=self._hq(l), out_scale=self.sh[l],
-                                 krange256=mk["P1"].fwd256)
+                                 krange256=mk["P1"].fwd256,
+                                 mask_out=self.MkL[l] if lean else None, write_y=not lean)
                 nxt = None if last else self.sx[l + 1]
                 qargs = ((self._xq(l + 1), nxt.amax[0:1], nxt.scale, nxt.cur)
                          if nxt is not None else ())
@@ -591,7 +597,7 @@ class MAFEngine:
                   if l > 0 or self.f8_wgrad else ())
             lean = self._lean8()
             native().fp8_dgrad(self._doq(l), sdo.scale, self.W2Tq[l * H:(l + 1) * H],
-                               self.sW2T[l * H:(l + 1) * H], self.Hbf[l],
+                               self.sW2T[l * H:(l + 1) * H], self.MkL[l] if lean else self.Hbf[l],
                                None if lean else self.dHL[l], mk["P2"].bwd256, *qh)
             if l > 0:
                 nx = self.sdo[l - 1]

@@ -110,7 +110,8 @@ class DelayedScale:
 
 
 def gemm_fp8(xq, sx, wq, sw, bias=None, relu=False, krange=None, out=None, out_q=None,
-             out_scale: "DelayedScale | None" = None, krange256=None):
+             out_scale: "DelayedScale | None" = None, krange256=None, mask_out=None,
+             write_y: bool = True):
     """y = act((xq*sx) (wq*sw)^T + bias) in bf16 (GPU kernel). With ``out_q``/``out_scale``
     the epilogue also writes the e4m3 copy of y under ``out_scale``'s delayed scale (the next
     fp8 GEMM's operand, no separate quantisation pass); returns (y, scale) then.
@@ -119,13 +120,16 @@ def gemm_fp8(xq, sx, wq, sw, bias=None, relu=False, krange=None, out=None, out_q
     from ._ext import native
 
     M, N = xq.shape[0], wq.shape[0]
-    y = out if out is not None else torch.empty(M, N, device=xq.device, dtype=torch.bfloat16)
+    # write_y=False: only the e4m3 copy and / or the ReLU bitmask ``mask_out`` [M, N/8] are
+    # produced (bf16 y skipped; 256-tile kernel)
+    y = None if not write_y else (
+        out if out is not None else torch.empty(M, N, device=xq.device, dtype=torch.bfloat16))
     b = bias.to(torch.bfloat16).contiguous() if bias is not None else None
     if out_q is not None:
         st = out_scale
         st.roll()
         native().gemm_fp8_nt(xq, sx, wq, sw, b, y, int(relu), krange, out_q, st.amax[0:1],
-                             st.scale, st.cur, krange256)
+                             st.scale, st.cur, krange256, mask_out)
         return y, st.scale
     native().gemm_fp8_nt(xq, sx, wq, sw, b, y, int(relu), krange, None, None, None, None,
                          krange256)
