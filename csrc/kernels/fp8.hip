@@ -273,9 +273,10 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_fp8_nt_kernel(Fp8Args a) {
 
 // Column sums of e4m3 [K][N] tensors, s * sum_k q[k][n] (the bias gradients of the e4m3
 // weight-gradient launches, ops/gemm.py WgradPlan): deterministic two-pass. Pass 1: block =
-// (descriptor, 256-column chunk, K slab); 64 threads x 4 columns (one 4-B load per row), 4
-// row groups, the groups folded through LDS in a fixed order -> part[slab][column]. Pass 2: the
-// slabs of each column summed in slab order, times the tensor's scale.
+// (descriptor, 256-column chunk, K slab); 16 lanes x 16 columns (one 16-B load per row and
+// lane), 16 row groups, 4 rows in flight per lane; the groups folded through LDS in a fixed
+// order -> part[slab][column]. Pass 2: each column's slabs summed in slab order, times the
+// tensor's scale.
 constexpr int CS_SLABS = 8;
 struct ColsumDesc {
   const unsigned char* q;
@@ -298,35 +299,57 @@ __device__ __forceinline__ int cs_desc(const ColsumArgs& a, int b) {
   return p;
 }
 
+__device__ __forceinline__ void cs_add16(float (&s)[16], uint4 w) {
+  const int ws[4] = {(int)w.x, (int)w.y, (int)w.z, (int)w.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(ws[e], false);
+    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8(ws[e], true);
+    s[4 * e] += lo[0];
+    s[4 * e + 1] += lo[1];
+    s[4 * e + 2] += hi[0];
+    s[4 * e + 3] += hi[1];
+  }
+}
+
 __global__ void __launch_bounds__(256) colsum_partial_kernel(ColsumArgs a) {
-  __shared__ float red[4][256];
+  __shared__ float red[16][257];
   const int p = cs_desc(a, blockIdx.x);
   const ColsumDesc& d = a.d[p];
   const int local = blockIdx.x - d.blk0;
   const int chunk = local / CS_SLABS, slab = local % CS_SLABS;
-  const int t = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int n = chunk * 256 + t * 4;
+  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int n = chunk * 256 + cl * 16;
   const int rows = (d.K + CS_SLABS - 1) / CS_SLABS;
   const int k0 = slab * rows, k1 = min(d.K, k0 + rows);
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  float s[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) s[e] = 0.f;
   if (n < d.N) {
     const unsigned char* col = d.q + n;
-    for (int k = k0 + grp; k < k1; k += 4) {
-      const int w = *reinterpret_cast<const int*>(col + (long)k * d.ld);
-      s0 += __builtin_amdgcn_cvt_f32_fp8(w, 0);
-      s1 += __builtin_amdgcn_cvt_f32_fp8(w, 1);
-      s2 += __builtin_amdgcn_cvt_f32_fp8(w, 2);
-      s3 += __builtin_amdgcn_cvt_f32_fp8(w, 3);
+    int k = k0 + grp;
+    for (; k + 48 < k1; k += 64) {   // 4 rows in flight per lane
+      const uint4 w0 = *reinterpret_cast<const uint4*>(col + (long)k * d.ld);
+      const uint4 w1 = *reinterpret_cast<const uint4*>(col + (long)(k + 16) * d.ld);
+      const uint4 w2 = *reinterpret_cast<const uint4*>(col + (long)(k + 32) * d.ld);
+      const uint4 w3 = *reinterpret_cast<const uint4*>(col + (long)(k + 48) * d.ld);
+      cs_add16(s, w0);
+      cs_add16(s, w1);
+      cs_add16(s, w2);
+      cs_add16(s, w3);
     }
+    for (; k < k1; k += 16) cs_add16(s, *reinterpret_cast<const uint4*>(col + (long)k * d.ld));
   }
-  red[grp][t * 4 + 0] = s0;
-  red[grp][t * 4 + 1] = s1;
-  red[grp][t * 4 + 2] = s2;
-  red[grp][t * 4 + 3] = s3;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) red[grp][cl * 16 + e] = s[e];
   __syncthreads();
   const int c = threadIdx.x, nc = chunk * 256 + c;
-  if (nc < d.N)
-    a.part[(long)slab * a.ncols + d.col0 + nc] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+  if (nc < d.N) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += red[g][c];
+    a.part[(long)slab * a.ncols + d.col0 + nc] = t;
+  }
 }
 
 __global__ void __launch_bounds__(256) colsum_final_kernel(ColsumArgs a) {
@@ -426,8 +449,8 @@ void nf_launch_fp8_colsum(int n, const void* const* q, const long* ld, const int
   ColsumArgs a{};
   int blk = 0, col = 0;
   for (int i = 0; i < n; ++i) {
-    if (N[i] % 4 || ld[i] % 4 || ((unsigned long)q[i] & 3)) {
-      fprintf(stderr, "vinf: fp8_colsum: N %% 4, ld %% 4, 4-B aligned rows\n");
+    if (N[i] % 16 || ld[i] % 16 || ((unsigned long)q[i] & 15)) {
+      fprintf(stderr, "vinf: fp8_colsum: N %% 16, ld %% 16, 16-B aligned rows\n");
       abort();
     }
     auto& d = a.d[i];
