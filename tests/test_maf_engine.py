@@ -281,3 +281,38 @@ def test_engine_fp8_weight_gradients(gpu, monkeypatch, dim, hidden, batch):
         for n in (f"l{l}.b1", f"l{l}.b2"):
             d = (P.g(n) - b.params.g(n)).norm() / b.params.g(n).norm()
             assert d.item() < 0.08, (n, d.item())
+
+
+@pytest.mark.gpu
+def test_fp8_vs_bf16_nll_trajectory_500_steps(gpu):
+    """Training with every product in e4m3 (forward, input and weight gradients) follows the
+    bf16 engine: MAF-8 at the config-5 width (1024-d, hidden 1024), B = 4096, Adam lr 1e-4
+    (the config-5 preset; at 2e-4 and above the bf16 run itself spikes without clipping), 500
+    steps on the same data stream. Stated tolerance: after the first 50 steps the two NLL
+    trajectories differ by at most 2 % of the bf16 run's NLL decrease so far (median over
+    steps), the last-50-step means agree within 1.5 % of the total decrease, and both runs
+    cover at least 5 % of the gap between the initial NLL and the data entropy."""
+    runs = {}
+    for prec in ("bf16", "fp8"):
+        cfg = MAFEngineConfig(dim=1024, hidden=1024, n_layers=8, precision=prec)
+        eng = MAFEngine(cfg, batch=4096, device=gpu, seed=21, lr=1e-4)
+        if prec == "fp8":
+            assert eng.fp8_bwd and eng.f8_wgrad
+        nll = torch.empty(500, device=gpu)
+        for i in range(500):
+            eng.train_step()
+            nll[i] = eng.loss
+        runs[prec] = nll.cpu().double()
+        floor = cfg.entropy()
+    b, f = runs["bf16"], runs["fp8"]
+    assert torch.isfinite(f).all() and torch.isfinite(b).all()
+    drop = b[0] - b                        # bf16 progress so far
+    rel = ((f - b).abs() / drop.clamp_min(1e-6))[50:]
+    tail_b, tail_f = b[-50:].mean().item(), f[-50:].mean().item()
+    total = (b[0] - b[-50:].mean()).item()
+    print(f"NLL bf16 {b[0]:.1f} -> {tail_b:.2f}, fp8 {f[0]:.1f} -> {tail_f:.2f}, floor {floor:.2f}; "
+          f"median |diff| / progress {rel.median():.4f}, max {rel.max():.4f}")
+    assert rel.median().item() < 0.02
+    assert abs(tail_f - tail_b) < 0.015 * total
+    for r in (b, f):
+        assert (r[0] - r[-50:].mean()).item() > 0.05 * (r[0].item() - floor)
