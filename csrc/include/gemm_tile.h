@@ -425,7 +425,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
         }
         // (C may be null on the e4m3 paths that only need the e4m3 copy: MAF engine, e4m3
         // weight gradients)
-        if (a.C) *reinterpret_cast<uint4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
+        if (!F8 || a.C) *reinterpret_cast<uint4*>((bf16_t*)a.C + (long)m * a.ldc + n) = o;
         if (f8out) {
           const unsigned w4[4] = {o.x, o.y, o.z, o.w};
           float f[8];
@@ -562,7 +562,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
               ushort4 d0, d1;
               d0.x = f2bf(dsh[0]); d0.y = f2bf(dsh[1]); d0.z = f2bf(dsh[2]); d0.w = f2bf(dsh[3]);
               d1.x = f2bf(d1v[0]); d1.y = f2bf(d1v[1]); d1.z = f2bf(d1v[2]); d1.w = f2bf(d1v[3]);
-              if (a.cpl_dst) {   // null: the e4m3 copy only (MAF engine, e4m3 weight gradients)
+              if (!F8 || a.cpl_dst) {   // null (e4m3 only): the e4m3 copy alone (MAF engine)
                 *reinterpret_cast<ushort4*>(drow + n) = d0;
                 *reinterpret_cast<ushort4*>(drow + a.cpl_dh + n) = d1;
               }
@@ -583,7 +583,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
                 *reinterpret_cast<int*>(qr + n) = q0;
                 *reinterpret_cast<int*>(qr + a.cpl_dh + n) = q1;
               }
-            } else if (a.cpl_dst && a.cpl_dh + n < a.cpl_pad) {   // zero the dst pad columns [2 Dh, pad)
+            } else if ((!F8 || a.cpl_dst) && a.cpl_dh + n < a.cpl_pad) {   // zero the dst pad [2 Dh, pad)
               *reinterpret_cast<ushort4*>(drow + a.cpl_dh + n) = make_ushort4(0, 0, 0, 0);
             }
           } else if (EPI == EPI_F32) {
