@@ -219,7 +219,7 @@ class MAFEngine:
             # copies of its four GEMM operands (x, h, dO, dH: 10.7 GB at B = 32768, L = 64), and
             # the weight gradients of all layers run on the e4m3 TN kernel (WgradPlan f8 form)
             # instead of the bf16 one over bf16 copies; VINF_FP8_WGRAD=0 keeps bf16
-            self.f8_wgrad = (self.fp8_bwd and self.wgrad_defer
+            self.f8_wgrad = (self.fp8_bwd and self.wgrad_defer and B % 128 == 0
                              and os.environ.get("VINF_FP8_WGRAD", "1") != "0")
             self._wplan8 = None
             if self.f8_wgrad:
