@@ -219,8 +219,9 @@ static void gemm_tn_multi_impl(at::TensorList dy, at::TensorList x, at::TensorLi
                                int64_t ntiles, const c10::List<c10::optional<at::Tensor>>& tiles,
                                const c10::List<c10::optional<at::Tensor>>& cmask,
                                const at::Tensor* f8_scales, at::IntArrayRef sa_idx,
-                               at::IntArrayRef sb_idx) {
+                               at::IntArrayRef sb_idx, int layout = 0) {
   const size_t n = dy.size();
+  TORCH_CHECK(layout >= 0 && layout <= 2 && (layout == 0 || !f8_scales), "layout 0..2, bf16");
   const bool f8 = f8_scales != nullptr;
   const auto odt = f8 ? at::kFloat8_e4m3fn : at::kBFloat16;
   if (f8) {
@@ -242,8 +243,11 @@ static void gemm_tn_multi_impl(at::TensorList dy, at::TensorList x, at::TensorLi
     chk_mat(dy[p], "dy", odt);
     chk_mat(x[p], "x", odt);
     chk_mat(dW[p], "dW", at::kFloat);
-    const int K = dy[p].size(0), M = dy[p].size(1), N = x[p].size(1);
-    TORCH_CHECK(x[p].size(0) == K, "batch mismatch");
+    // layout 1: x given as [N][K]; layout 2: dy given as [M][K]
+    const int K = layout == 2 ? dy[p].size(1) : dy[p].size(0);
+    const int M = layout == 2 ? dy[p].size(0) : dy[p].size(1);
+    const int N = layout == 1 ? x[p].size(0) : x[p].size(1);
+    TORCH_CHECK((layout == 1 ? x[p].size(1) : x[p].size(0)) == K, "batch mismatch");
     TORCH_CHECK(dW[p].size(0) == M && dW[p].size(1) == N, "dW shape");
     TORCH_CHECK(K % 32 == 0 && M % 8 == 0 && N % 8 == 0, "K % 32, M % 8, N % 8 required");
     TORCH_CHECK(!f8 || (K % 128 == 0 && M % 16 == 0 && N % 16 == 0 && ld2(dy[p]) % 16 == 0 &&
@@ -288,7 +292,15 @@ static void gemm_tn_multi_impl(at::TensorList dy, at::TensorList x, at::TensorLi
   TORCH_CHECK(tile0 >= 0 && ntiles >= 1 && tile0 + ntiles <= total, "tile range outside the ",
               total, " tiles of the problem list");
   nf_launch_gemm256_tn_multi((int)n, pr.data(), (int)tile0, (int)ntiles, cur_stream(),
-                             f8 ? f8_scales->data_ptr<float>() : nullptr);
+                             f8 ? f8_scales->data_ptr<float>() : nullptr, layout);
+}
+
+// operand-layout A/B of the bf16 weight-gradient launch (bench/wgrad_bench.py --probe)
+void gemm_tn_multi_layout(at::TensorList dy, at::TensorList x, at::TensorList dW,
+                          const c10::List<c10::optional<at::Tensor>>& db, int64_t tile0,
+                          int64_t ntiles, int64_t layout) {
+  const c10::List<c10::optional<at::Tensor>> none;
+  gemm_tn_multi_impl(dy, x, dW, db, tile0, ntiles, none, none, nullptr, {}, {}, (int)layout);
 }
 
 void gemm_tn_multi(at::TensorList dy, at::TensorList x, at::TensorList dW,
@@ -1012,6 +1024,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db) -> ()");
   m.def("gemm_tn_group(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, Tensor?[] skip, Tensor?[] cmask) -> ()");
   m.def("gemm_tn_multi(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles, Tensor?[] tiles, Tensor?[] cmask) -> ()");
+  m.def("gemm_tn_multi_layout(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles, int layout) -> ()");
   m.def("fp8_colsum(Tensor[] q, Tensor(a!)[] out, Tensor scales, int[] sidx, Tensor(b!) part) -> ()");
   m.def("gemm_tn_multi_f8(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles, Tensor?[] tiles, Tensor?[] cmask, Tensor scales, int[] sa_idx, int[] sb_idx) -> ()");
   m.def("gemm_nt_cpl(Tensor h, Tensor W, Tensor? b, Tensor(a!) st, Tensor x, Tensor(b!) y, Tensor(c!)? yb, Tensor(d!) ldjp, bool ldj_init, float scale) -> ()");
@@ -1039,6 +1052,7 @@ TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
   m.impl("gemm_tn_multi", &gemm_tn_multi);
   m.impl("gemm_tn_multi_f8", &gemm_tn_multi_f8);
   m.impl("fp8_colsum", &fp8_colsum);
+  m.impl("gemm_tn_multi_layout", &gemm_tn_multi_layout);
   m.impl("gemm_nn_cpl", &gemm_nn_cpl);
   m.impl("gemm_nt_cpl", &gemm_nt_cpl);
   m.impl("fp8_quant_rows", &fp8_quant_rows);

@@ -158,7 +158,10 @@ int nf_launch_gemm256_tn_partials(const void* dy, long lddy, const void* x, long
 // after problem, one launch computes [tile0, tile0 + ntiles)
 int nf_gemm256_tiles(int M, int N);
 void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int ntiles,
-                                hipStream_t stream, const float* f8_scales = nullptr);
+                                hipStream_t stream, const float* f8_scales = nullptr,
+                                int layout = 0);
+// layout: 0 = dy [K][M], x [K][N] (batch-major, TN); 1 = x given transposed [N][K] (k-major);
+// 2 = dy given transposed [M][K] - the operand-layout A/B (bench/wgrad_bench.py --probe)
 // mode: 0 auto, 1 force 128x128, 2 force 256x256; depth: half-tiles in flight (3 or 4)
 void nf_gemm_set_mode(int mode, int depth);
 // fp8.hip (OCP e4m3): per-row quantisation and the MX-scaled K=128 MFMA GEMM

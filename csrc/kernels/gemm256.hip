@@ -1005,7 +1005,9 @@ static_assert(sizeof(TnMulti) <= 4096, "TnMulti must fit the 4 KiB kernarg segme
 
 // F8: every problem of the launch has e4m3 operands (mn-major, K % 128 == 0, ld in bytes):
 // read through ds_read_b64_tr_b8 (read_frag_f8mn), dW = acc * s_dy * s_x, db = s_dy * row sums
-template <int D, bool F8 = false>
+// A_KM / B_KM: operand layouts of every problem (false = batch-major, the TN weight-gradient form;
+// true = a transposed [M or N][batch] copy, k-major) - the layout A/B of wgrad_bench --probe
+template <int D, bool F8 = false, bool A_KM = false, bool B_KM = false>
 __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
   __shared__ __attribute__((aligned(16))) char smem[smem_bytes(D)];
   const int pos = xcd_remap(blockIdx.x, t.ntiles);
@@ -1028,7 +1030,7 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
     a.f8_sb = t.scales + (d.sidx >> 16);
   }
   const int local = d.tiles ? (int)d.tiles[id - d.start] : id - d.start;
-  gemm256_body<false, false, EPI_F32, D, true, F8>(a, local, 0, smem);
+  gemm256_body<A_KM, B_KM, EPI_F32, D, true, F8>(a, local, 0, smem);
 }
 
 // persistent plain products: VINF_G256_PERSIST at load, or nf_gemm256_set_persist (the DP
@@ -1598,7 +1600,7 @@ int nf_gemm256_tiles(int M, int N) {
 // tiles are numbered problem after problem (row-major tiles inside a problem); the launch
 // computes tiles [tile0, tile0 + ntiles) and may start or end inside a problem
 void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int ntiles,
-                                hipStream_t stream, const float* f8_scales) {
+                                hipStream_t stream, const float* f8_scales, int layout) {
   if (ntiles <= 0) return;
   const bool f8 = f8_scales != nullptr;
   g256::TnMulti t{};
@@ -1661,7 +1663,17 @@ void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int
     }
     t.use_perm = nf::wgrad_xcd_perm(t.n, seg_lo, seg_n, ntiles, t.perm) ? 1 : 0;
   }
-  if (f8)
+  if (layout != 0 && f8) {
+    fprintf(stderr, "vinf: gemm256_tn_multi: transposed-operand layouts are bf16 only\n");
+    abort();
+  }
+  if (layout == 1)
+    hipLaunchKernelGGL((g256::gemm256_multi_kernel<4, false, false, true>), dim3(ntiles),
+                       dim3(g256::NTHR), 0, stream, t);
+  else if (layout == 2)
+    hipLaunchKernelGGL((g256::gemm256_multi_kernel<4, false, true, false>), dim3(ntiles),
+                       dim3(g256::NTHR), 0, stream, t);
+  else if (f8)
     hipLaunchKernelGGL((g256::gemm256_multi_kernel<4, true>), dim3(ntiles), dim3(g256::NTHR), 0,
                        stream, t);
   else if (g256::g_depth == 6)

@@ -86,6 +86,65 @@ def probe(B: int, iters: int, tag: str, dev):
               flush=True)
 
 
+def layout_probe(B: int, layers: int, iters: int, tag: str, dev):
+    """The real deferred weight-gradient launch (per layer dW3 [800 x 1024], dW2 [1024 x 1024],
+    dW1 [1024 x 416], chunks of one tile per CU) with three operand layouts: 0 = dy, x both
+    batch-major (TN, what the engine runs), 1 = x as a transposed [N][batch] copy (k-major B),
+    2 = dy as a transposed [M][batch] copy (k-major A). Results must agree; one JSON line per
+    layout with the median launch time."""
+    from ..ops._ext import native
+    from ..ops.gemm import wgrad_tiles
+
+    bf = torch.bfloat16
+    H, Dp, Np = 1024, 416, 800
+    g = torch.Generator(device=dev).manual_seed(0)
+    dys, xs, outs, dbs, starts = [], [], [], [], [0]
+    for _ in range(layers):
+        for (o, i) in ((Np, H), (H, H), (H, Dp)):
+            dys.append(torch.randn(B, o, device=dev, generator=g).to(bf))
+            xs.append(torch.randn(B, i, device=dev, generator=g).to(bf))
+            outs.append(torch.empty(o, i, device=dev))
+            dbs.append(torch.empty(o, device=dev))
+            starts.append(starts[-1] + wgrad_tiles(o, i))
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    total = starts[-1]
+    nl = total // cus
+    ops = {0: (dys, xs), 1: (dys, [x.t().contiguous() for x in xs]),
+           2: ([d.t().contiguous() for d in dys], xs)}
+    ref = None
+    flops = 2.0 * B * cus * 256 * 256
+    import bisect
+
+    for layout, (D_, X_) in ops.items():
+        def run(c):
+            t0, t1 = c * cus, (c + 1) * cus
+            p0 = bisect.bisect_right(starts, t0) - 1
+            p1 = bisect.bisect_left(starts, t1) - 1
+            native().gemm_tn_multi_layout(D_[p0:p1 + 1], X_[p0:p1 + 1], outs[p0:p1 + 1],
+                                          dbs[p0:p1 + 1], t0 - starts[p0], cus, layout)
+        for c in range(nl):
+            run(c)
+        torch.cuda.synchronize()
+        got = torch.cat([o.flatten() for o in outs[:3 * (nl * cus // 40)]])
+        if ref is None:
+            ref = got.clone()
+        err = ((got - ref).abs().max() / ref.abs().max()).item()
+        ts = []
+        for _ in range(iters):
+            for c in range(nl):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                run(c)
+                e.record()
+                e.synchronize()
+                ts.append(s.elapsed_time(e) * 1e3)
+        ts.sort()
+        med = ts[len(ts) // 2]
+        print(json.dumps({"tag": tag, "layout": layout, "launches": nl, "us_min": round(ts[0], 1),
+                          "us_med": round(med, 1), "tflops_padded": round(flops / med / 1e6, 1),
+                          "max_rel_diff_vs_layout0": err}), flush=True)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536)
@@ -93,10 +152,14 @@ def main(argv=None):
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--tag", default=os.environ.get("VINF_BENCH_TAG", ""))
     ap.add_argument("--probe", action="store_true")
+    ap.add_argument("--layout-probe", action="store_true")
     a = ap.parse_args(argv)
     dev = torch.device("cuda")
     if a.probe:
         probe(a.batch, a.iters, a.tag, dev)
+        return
+    if a.layout_probe:
+        layout_probe(a.batch, a.layers, a.iters, a.tag, dev)
         return
     plan, _ = build(a.batch, a.layers, dev)
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
