@@ -400,7 +400,7 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
   // slower on the grouped weight-gradient launch (428 -> 447 us, profiles/r2_bcontig_ab.txt),
   // kept as an opt-in A/B build (-D NF_G256_BCONTIG)
 #ifdef NF_G256_BCONTIG
-  constexpr bool BSPLIT = !A_KMAJOR && !B_KMAJOR;
+  constexpr bool BSPLIT = !A_KMAJOR && !B_KMAJOR && !F8;
 #else
   constexpr bool BSPLIT = false;
 #endif
