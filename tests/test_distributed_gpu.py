@@ -176,3 +176,45 @@ def test_rccl_reducer_iaf_engine(tmp_path):
     assert torch.equal(r["plain"], r["rccl_eager"]), d_e
     assert torch.equal(r["plain"], r["rccl_graph"]), d_g
     assert r["plain_loss"] == r["rccl_eager_loss"] == r["rccl_graph_loss"]
+
+
+def _rccl_maf_fp8_worker(rank, port, out_dir):
+    """Config-5 engine, fp8 with e4m3 weight gradients, on the DP runner: plain vs 1-rank RCCL
+    reduce, eager and graph-captured (the e4m3 weight-gradient plan, its column sums and the
+    bucket hooks inside one hipGraph)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0")
+    from vi_normflows_amd.models.maf_engine import MAFEngine, MAFEngineConfig
+    from vi_normflows_amd.parallel import dist as vdist
+    from vi_normflows_amd.parallel.runner import DataParallelRunner
+
+    info = vdist.init()
+    dev = info.device
+    cfg = MAFEngineConfig(dim=256, hidden=512, n_layers=4, precision="fp8", init_out_std=0.3)
+    out = {}
+    for name in ("plain", "rccl_eager", "rccl_graph"):
+        eng = MAFEngine(cfg, batch=1024, device=dev, seed=5)
+        assert eng.f8_wgrad
+        run = DataParallelRunner(eng, info, bucket_cap_mb=1.0, force_reduce=(name != "plain"))
+        if name == "rccl_graph":
+            assert run.capture(warmup=2), "hipGraph capture of the fp8 MAF step failed"
+            run.step()
+            run.step()
+        else:
+            for _ in range(4):
+                run.step()
+        torch.cuda.synchronize()
+        out[name] = eng.params.master.cpu()
+        out[name + "_loss"] = float(eng.loss.item())
+    torch.save(out, os.path.join(out_dir, "rccl_maf.pt"))
+    dist.destroy_process_group()
+
+
+def test_rccl_reducer_maf_fp8_engine(tmp_path):
+    mp.spawn(_rccl_maf_fp8_worker, args=(_port(), str(tmp_path)), nprocs=1, join=True)
+    r = torch.load(tmp_path / "rccl_maf.pt", weights_only=True)
+    assert torch.isfinite(r["plain"]).all()
+    # a 1-rank SUM is the identity and the step is deterministic (column sums included)
+    assert torch.equal(r["plain"], r["rccl_eager"])
+    assert torch.equal(r["plain"], r["rccl_graph"])
+    assert r["plain_loss"] == r["rccl_eager_loss"] == r["rccl_graph_loss"]
