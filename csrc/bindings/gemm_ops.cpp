@@ -230,7 +230,8 @@ static void gemm_tn_multi_impl(at::TensorList dy, at::TensorList x, at::TensorLi
                 "gemm_tn_multi_f8: fp32 scale pool and one (sa, sb) index pair per problem");
     for (size_t p = 0; p < n; ++p)
       TORCH_CHECK(sa_idx[p] >= 0 && sb_idx[p] >= 0 && sa_idx[p] < f8_scales->numel() &&
-                      sb_idx[p] < f8_scales->numel() && sb_idx[p] <= 0x7fff,
+                      sb_idx[p] < f8_scales->numel() && sa_idx[p] <= 0xffff &&
+                      sb_idx[p] <= 0x7fff,
                   "gemm_tn_multi_f8: scale index outside the pool");
   }
   TORCH_CHECK(n >= 1 && n <= 40 && x.size() == n && dW.size() == n && db.size() == n,
