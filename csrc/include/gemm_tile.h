@@ -416,12 +416,25 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
           }
         }
         if (EPI == EPI_BF16 && a.mask_out) {  // 1(y > 0) of the stored bf16, 8 bits per lane
+#ifdef NF_MASK_OLD   // A/B build: per-half compares and selects
           auto pos2 = [](unsigned w) {
             return (((w & 0xffffu) != 0 && !(w & 0x8000u)) ? 1u : 0u) |
                    (((w >> 16) != 0 && !(w & 0x80000000u)) ? 2u : 0u);
           };
           const unsigned bits = pos2(o.x) | (pos2(o.y) << 2) | (pos2(o.z) << 4) | (pos2(o.w) << 6);
+#else
+          // branch-free: half h > 0 (bf16) <=> h in [1, 0x7fff] <=> bit 15 of
+          // ((h & 0x7fff) + 0x7fff) & ~h; both halves at once (no carry: each sum <= 0xfffe),
+          // then bits 15 / 31 of the 4 words gathered to bits 2e / 2e + 1 of one byte
+          auto pos = [](unsigned w) { return ((w & 0x7fff7fffu) + 0x7fff7fffu) & ~w & 0x80008000u; };
+          const unsigned t = (pos(o.x) >> 15) | (pos(o.y) >> 13) | (pos(o.z) >> 11) | (pos(o.w) >> 9);
+          const unsigned bits = (t | (t >> 15)) & 0xffu;
+#endif
+#ifdef NF_MASK_NOSTORE   // diagnostic build: the bits are computed but not stored
+          asm volatile("" ::"v"(bits));
+#else
           a.mask_out[(long)m * a.ld_mask + (n >> 3)] = (unsigned char)bits;
+#endif
         }
         // (C may be null on the e4m3 paths that only need the e4m3 copy: MAF engine, e4m3
         // weight gradients)
