@@ -76,6 +76,36 @@ case $name in
     timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS \
       -d $O/p2 -o step --output-format csv -- python3 bench.py --steps 3 --warmup 2 --graph off > $O/p2.log 2>&1 || { tail -20 $O/p2.log; exit 1; }
     python3 -m vi_normflows_amd.bench.pmc_summary $O/p1 $O/p2 > $O/summary.txt && cat $O/summary.txt ;;
+  iaf_graph)      # IAF engine: eager vs graph-replayed forward + backward, buffer by buffer; a
+                  # test failure is data here (the chain continues), a hang / fault is not
+    timeout -k 10 300 python -u -m pytest tests/test_iaf_engine.py -m gpu -k graph -v --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1
+    rc=$?; grep -E "PASS|FAIL|assert|differs|Error" $O/pytest.txt | head -20
+    [ $rc -le 1 ] || exit $rc ;;
+  cumask)         # CU-mask stream probe: mask bit -> XCD / SE / CU, and graph replay vs the mask
+    /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/cumask_probe.hip -o $O/cumask_probe &&
+    timeout -k 10 120 $O/cumask_probe > $O/cumask.jsonl && tail -3 $O/cumask.jsonl ;;
+  tests)          # selected GPU test files: args "<pytest paths / -k expr>" [tag]
+    tag=${2:-t}
+    timeout -k 10 900 python -u -m pytest $1 -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > $O/$tag.txt 2>&1 || { tail -40 $O/$tag.txt; exit 1; }
+    tail -3 $O/$tag.txt ;;
+  bench)          # headline bench on this box: args [tag] [extra bench args]
+    tag=${1:-base}; shift
+    timeout -k 10 240 python bench.py --steps 20 --warmup 5 "$@" > $O/$tag.json 2> $O/$tag.err || { tail -20 $O/$tag.err; exit 1; }
+    python -c "import json;d=json.load(open('$O/$tag.json'));print('BENCH $tag', d['ms_per_step'], d['value'], d['notes']['final_free_energy'])" ;;
+  roofline)       # per-family HBM bytes / MFMA roofline of a step (bench/roofline.py): two counter
+                  # passes (EA read requests by size + MFMA; EA write requests + L2 hit/miss) and an
+                  # un-profiled kernel trace of the same command. args: TAG [bench / configs args]
+    export TMPDIR=/tmp
+    tag=${1:-step}; shift
+    cmd="python3 bench.py --steps 3 --warmup 2 --graph off"; model="--model realnvp32"
+    if [ $# -gt 0 ]; then cmd="python3 -m vi_normflows_amd.bench.configs --graph off --steps 3 --warmup 2 $*"; model=""; fi
+    R=$O/$tag; mkdir -p $R
+    timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_32B_sum GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES \
+      -d $R/rd -o step --output-format csv -- $cmd > $R/rd.log 2>&1 || { tail -20 $R/rd.log; exit 1; }
+    timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE \
+      -d $R/wr -o step --output-format csv -- $cmd > $R/wr.log 2>&1 || { tail -20 $R/wr.log; exit 1; }
+    timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/trace -o step --output-format csv -- $cmd > $R/trace.log 2>&1 || { tail -20 $R/trace.log; exit 1; }
+    python3 -m vi_normflows_amd.bench.roofline --pmc $R/rd $R/wr --trace $R/trace --steps 0 $model > $R/roofline.txt && cat $R/roofline.txt ;;
   configs)        # north-star config refresh on the current tree (one line per run)
     for args in "--config 0 --batch 128" "--config 0 --batch 1024" "--config 2 --batch 32768" "--config 2 --batch 65536" \
                 "--config 4 --batch 8192" "--config 4 --batch 32768" "--config 5 --precision bf16 --batch 32768" "--config 5 --precision fp8 --batch 32768" \

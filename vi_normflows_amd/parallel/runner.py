@@ -39,6 +39,36 @@ def _init_single_rank_group(info: DistInfo) -> None:
     info.backend = backend
 
 
+# Process-global multi-rank GEMM policy, reference counted: the first runner that needs it
+# saves the library's persistent-grid / CU-reserve switches, every live runner keeps it applied,
+# the last one to close restores the saved values (LIFO-safe whatever order runners close in).
+_POLICY = {"refs": 0, "saved": None}
+
+
+def _policy_acquire(reserve_mode: bool, reserve_cus: int) -> None:
+    from ..ops._ext import native
+
+    if _POLICY["refs"] == 0:
+        _POLICY["saved"] = (int(native().gemm_persist(-1)), int(native().gemm_grid_reserve(-1)))
+    _POLICY["refs"] += 1
+    if reserve_mode:
+        native().gemm_persist(1)
+        native().gemm_grid_reserve(reserve_cus)
+    else:
+        native().gemm_persist(0)
+
+
+def _policy_release() -> None:
+    from ..ops._ext import native
+
+    _POLICY["refs"] = max(0, _POLICY["refs"] - 1)
+    if _POLICY["refs"] == 0 and _POLICY["saved"] is not None:
+        persist, reserve = _POLICY["saved"]
+        native().gemm_persist(persist)
+        native().gemm_grid_reserve(reserve)
+        _POLICY["saved"] = None
+
+
 class DataParallelRunner:
     """``force_reduce`` (or ``VINF_FORCE_REDUCE=1``) keeps the bucketed all-reduce on at world
     size 1 when a process group exists: a 1-rank RCCL communicator then runs the exact
@@ -56,8 +86,7 @@ class DataParallelRunner:
             _init_single_rank_group(info)
         # "1" all | "0" none | "fwd" (default) | "reserve"
         persist = os.environ.get("VINF_DP_PERSIST", "fwd")
-        self._persist_prev = None     # process-global GEMM switches, restored by close()
-        self._reserve_prev = None
+        self._policy_held = False     # this runner holds a reference on the global GEMM policy
         if (info.world > 1 or force) and engine.device.type == "cuda" and persist != "1":
             # multi-rank: RCCL kernels run on CUs beside the backward's GEMMs; a persistent GEMM
             # grid (one block per CU, each owning a fixed tile list) would wait for every CU an
@@ -66,14 +95,9 @@ class DataParallelRunner:
             # (default 16, whole XCD rounds) to RCCL. The forward has no collective in flight:
             # engines that support it run the full persistent grid there
             # (``persist_forward_only``).
-            from ..ops._ext import native
-
-            if persist == "reserve":
-                self._persist_prev = int(native().gemm_persist(1))
-                self._reserve_prev = int(native().gemm_grid_reserve(
-                    int(os.environ.get("VINF_G256_RESERVE", "16"))))
-            else:
-                self._persist_prev = int(native().gemm_persist(0))
+            reserve = int(os.environ.get("VINF_G256_RESERVE", "16")) if persist == "reserve" else 0
+            _policy_acquire(persist == "reserve", reserve)
+            self._policy_held = True
             if persist in ("fwd", "reserve") and hasattr(engine, "persist_forward_only"):
                 engine.persist_forward_only = True
         if info.world > 1 or (force and dist.is_initialized()):
@@ -116,15 +140,14 @@ class DataParallelRunner:
             self.engine.train_step(reduce_fn=fn)
 
     def close(self) -> None:
-        """Restore the process-global persistent-GEMM switch this runner changed."""
-        if self._persist_prev is not None:
-            from ..ops._ext import native
-
-            native().gemm_persist(self._persist_prev)
-            self._persist_prev = None
-            if self._reserve_prev is not None:
-                native().gemm_grid_reserve(self._reserve_prev)
-                self._reserve_prev = None
+        """Release this runner's reference on the process-global persistent-GEMM policy (the
+        settings that were in force before the FIRST live runner are restored when the LAST
+        one closes) and the engine's forward-only persistence. Explicit (or ``with``): no
+        ``__del__``, so garbage-collection order can never restore a policy under a live
+        runner."""
+        if self._policy_held:
+            self._policy_held = False
+            _policy_release()
         if hasattr(self.engine, "persist_forward_only"):
             self.engine.persist_forward_only = False
 
@@ -133,12 +156,6 @@ class DataParallelRunner:
 
     def __exit__(self, *exc):
         self.close()
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
 
     def capture(self, warmup: int = 2) -> bool:
         """Capture one training step into a hipGraph. Returns False if capture is unsupported
