@@ -399,11 +399,22 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
         uint4 o = make_uint4(v[0], v[1], v[2], v[3]);
         if constexpr (EPI == EPI_BF16_RELUMASK) {
           // keep element e iff aux_e > 0 (bf16: sign clear and not +0), per 16-bit half
+#ifdef NF_MASK_OLD   // A/B build: per-half compares and selects
           auto keep = [](unsigned hw) {
             const unsigned lo = (hw & 0xffffu) != 0 && !(hw & 0x8000u) ? 0xffffu : 0u;
             const unsigned hi = (hw >> 16) != 0 && !(hw & 0x80000000u) ? 0xffff0000u : 0u;
             return lo | hi;
           };
+#else
+          // branch-free, both halves at once: bit 15 / 31 of p is set iff that bf16 half is in
+          // [1, 0x7fff] (> 0; see the bitmask epilogue below), and (p << 1) - (p >> 15)
+          // widens each marked bit to its whole half (mod 2^32: bit 31's shifted-out carry is
+          // what turns 0 - 0x10000 into 0xffff0000)
+          auto keep = [](unsigned hw) {
+            const unsigned p = ((hw & 0x7fff7fffu) + 0x7fff7fffu) & ~hw & 0x80008000u;
+            return (p << 1) - (p >> 15);
+          };
+#endif
           if (a.aux_bits) {
             const unsigned b = hb[it];
             auto kb = [b](int e) {

@@ -218,6 +218,21 @@ def test_train_cli_iaf_uses_engine(gpu, tmp_path):
 
 
 @pytest.mark.gpu
+def test_train_cli_iaf_sgd_uses_engine(gpu, tmp_path):
+    """A non-Adam rule (SGD-momentum, experimentation.py:109) stays on the engine too."""
+    import json
+
+    from vi_normflows_amd.train import main
+
+    final = main(["--config", "config4_iaf10_vae", "iters=20", "log_every=10", "batch=1024",
+                  "optimizer=sgd", "lr=1e-2", f"out_dir={tmp_path}", "name=iaf_sgd",
+                  "extra.n_data=2048"])
+    assert final["engine"] == "iaf_engine" and math.isfinite(final["free_energy"])
+    rec = [json.loads(l) for l in (tmp_path / "iaf_sgd" / "metrics.jsonl").read_text().splitlines()]
+    assert all(r["path"] == "engine" and r["optimizer"] == "sgd" for r in rec)
+
+
+@pytest.mark.gpu
 def test_train_cli_annealed_iaf_uses_engine(gpu, tmp_path):
     """An annealed config-4 run (reference beta_t) takes the engine path, and the logged beta
     follows optimization.py:71-72 from t = 0 (the capture warm-up is rolled back)."""

@@ -22,8 +22,13 @@ def test_config3_preset_trains_at_full_width(tmp_path):
            (tmp_path / "config3_realnvp32_dp8" / "metrics.jsonl").read_text().splitlines()]
     F = [r["F"] for r in rec]
     assert len(F) >= 9 and all(math.isfinite(f) for f in F), F
-    # measured at B = 8192 (profiles/r3/pytest_gpu_c2.txt): F 188 at the first log -> 98 at
-    # step 200, falling at every log point but the noise of a small batch
-    assert F[-1] < 0.7 * F[0], F
-    assert sum(b < a for a, b in zip(F, F[1:])) >= 0.75 * (len(F) - 1), F
+    # F[0] is the first training step's free energy (logged from the first step). Requirement
+    # from an independent run, the bench configuration's own 2000-step trajectory at B = 65536
+    # (profiles/r2_headline_convergence_split_lr1e-3_b65536.jsonl): F 836 at step 1 -> 95 at
+    # step 200, a ratio of 0.114; at 1/8 of that batch the bound leaves 2x margin on it. (The
+    # round-3 form compared with the step-20 F, after the initial collapse: 188 -> 98 measured.)
+    assert F[-1] < 0.25 * F[0], F
+    # past the initial collapse, F falls at most log points (small-batch noise aside)
+    late = F[1:]
+    assert sum(b < a for a, b in zip(late, late[1:])) >= 0.75 * (len(late) - 1), F
     assert out["skipped_steps"] == 0.0 and rec[-1]["skipped"] == 0.0

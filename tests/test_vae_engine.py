@@ -181,6 +181,25 @@ def test_train_cli_planar_vae_uses_engine(gpu, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("opt", ["rmsprop", "sgd", "rmsprop_momentum"])
+def test_train_cli_planar_vae_every_optimizer_on_engine(gpu, tmp_path, opt):
+    """Every reference optimizer runs on the engine (the fused flat update, optim.hip): the
+    reference trains this workload with RMSProp (get_data.py:140), SGD-momentum
+    (experimentation.py:109) and RMSProp + momentum (theano_implement.py:187-188). The
+    metrics record names the path and the rule."""
+    import json
+
+    from vi_normflows_amd.train import main
+
+    final = main(["--config", "mnist_planar_vae", "iters=60", "log_every=20", f"optimizer={opt}",
+                  f"out_dir={tmp_path}", "name=vae_opt", "extra.n_data=300"])
+    assert final["engine"] == "vae_engine"
+    assert math.isfinite(final["free_energy_per_sample"])
+    rec = [json.loads(l) for l in (tmp_path / "vae_opt" / "metrics.jsonl").read_text().splitlines()]
+    assert rec and all(r["path"] == "engine" and r["optimizer"] == opt for r in rec), rec[-1]
+
+
+@pytest.mark.gpu
 def test_fused_bernoulli_loglik_matches_composite(gpu):
     """PlanarVAE.log_joint's fused HIP likelihood (elbo.hip, value + gradient in one pass) vs
     the softplus composite, value and gradient."""

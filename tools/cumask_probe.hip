@@ -28,7 +28,7 @@ __global__ void where_kernel(unsigned* out, int spin) {
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
   // keep the block resident a little so many blocks of one launch spread over the allowed CUs
-  for (int i = 0; i < spin; ++i) __builtin_amdgcn_s_sleep(8);
+  for (int i = 0; i < spin; ++i) __builtin_amdgcn_s_sleep(8);   // ~0.1 us per 8 sleeps
   if (threadIdx.x == 0) {
     out[2 * blockIdx.x] = xcc;
     out[2 * blockIdx.x + 1] = hw;
@@ -43,7 +43,6 @@ int main() {
   unsigned* d = nullptr;
   CK(hipMalloc(&d, 2 * 1024 * sizeof(unsigned)));
   std::vector<unsigned> h(2 * 1024);
-  std::vector<int> bit_xcc(ncu, -1);
   for (int b = 0; b < ncu; ++b) {
     std::vector<uint32_t> m(words, 0u);
     m[b / 32] = 1u << (b % 32);
@@ -52,27 +51,35 @@ int main() {
     hipLaunchKernelGGL(where_kernel, dim3(1), dim3(64), 0, s, d, 0);
     CK(hipStreamSynchronize(s));
     CK(hipMemcpy(h.data(), d, 2 * sizeof(unsigned), hipMemcpyDeviceToHost));
-    bit_xcc[b] = (int)(h[0] & 7u);
     printf("{\"bit\": %d, \"xcc\": %u, \"hw_id\": %u, \"cu\": %u, \"sh\": %u, \"se\": %u}\n", b,
            h[0] & 7u, h[1], (h[1] >> 8) & 15u, (h[1] >> 12) & 1u, (h[1] >> 13) & 7u);
     CK(hipStreamDestroy(s));
   }
-  // a mask of every bit that landed on XCC 0, then a 256-block launch: eager and graph replay
-  std::vector<uint32_t> m(words, 0u);
-  int nbits = 0;
-  for (int b = 0; b < ncu; ++b)
-    if (bit_xcc[b] == 0) {
-      m[b / 32] |= 1u << (b % 32);
-      ++nbits;
-    }
-  hipStream_t s, plain;
-  CK(hipExtStreamCreateWithCUMask(&s, words, m.data()));
+  // multi-block launches under a few masks: distinct (XCC, HW_ID & CU/SH/SE) seen, eagerly and
+  // replayed from a graph captured on the masked stream (1024 blocks, each resident ~20 us)
+  hipStream_t plain;
   CK(hipStreamCreate(&plain));
-  auto report = [&](const char* tag) {
-    CK(hipMemcpy(h.data(), d, 2 * 256 * sizeof(unsigned), hipMemcpyDeviceToHost));
-    std::set<unsigned> xs;
-    for (int i = 0; i < 256; ++i) xs.insert(h[2 * i] & 7u);
-    printf("{\"graph\": \"%s\", \"mask_bits\": %d, \"xcc_seen\": [", tag, nbits);
+  const int NB = 1024;
+  unsigned* d2 = nullptr;
+  CK(hipMalloc(&d2, 2 * NB * sizeof(unsigned)));
+  std::vector<unsigned> h2(2 * NB);
+  struct MaskCase { const char* name; std::vector<uint32_t> m; };
+  std::vector<MaskCase> cases;
+  cases.push_back({"bit0", std::vector<uint32_t>(words, 0u)});
+  cases.back().m[0] = 1u;
+  cases.push_back({"low16_of_each_word", std::vector<uint32_t>(words, 0x0000ffffu)});
+  cases.push_back({"first_half_words", std::vector<uint32_t>(words, 0u)});
+  for (int w = 0; w < words / 2; ++w) cases.back().m[w] = 0xffffffffu;
+  cases.push_back({"even_bits", std::vector<uint32_t>(words, 0x55555555u)});
+  auto census = [&](const char* mask, const char* how) {
+    CK(hipMemcpy(h2.data(), d2, 2 * NB * sizeof(unsigned), hipMemcpyDeviceToHost));
+    std::set<unsigned> xs, cus;
+    for (int i = 0; i < NB; ++i) {
+      xs.insert(h2[2 * i] & 7u);
+      cus.insert(((h2[2 * i] & 7u) << 16) | ((h2[2 * i + 1] >> 8) & 0xffu));
+    }
+    printf("{\"mask\": \"%s\", \"how\": \"%s\", \"n_xcc\": %zu, \"n_cu\": %zu, \"xcc\": [", mask,
+           how, xs.size(), cus.size());
     bool first = true;
     for (unsigned x : xs) {
       printf("%s%u", first ? "" : ", ", x);
@@ -80,27 +87,35 @@ int main() {
     }
     printf("]}\n");
   };
-  hipLaunchKernelGGL(where_kernel, dim3(256), dim3(64), 0, s, d, 200);
-  CK(hipStreamSynchronize(s));
-  report("eager_masked_stream");
-  hipGraph_t g;
-  hipGraphExec_t ge;
-  CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
-  hipLaunchKernelGGL(where_kernel, dim3(256), dim3(64), 0, s, d, 200);
-  CK(hipStreamEndCapture(s, &g));
-  CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-  CK(hipMemset(d, 0xff, 2 * 256 * sizeof(unsigned)));
-  CK(hipGraphLaunch(ge, s));
-  CK(hipStreamSynchronize(s));
-  report("graph_replayed_on_masked_stream");
-  CK(hipMemset(d, 0xff, 2 * 256 * sizeof(unsigned)));
-  CK(hipGraphLaunch(ge, plain));
+  for (auto& c : cases) {
+    hipStream_t s;
+    CK(hipExtStreamCreateWithCUMask(&s, words, c.m.data()));
+    hipLaunchKernelGGL(where_kernel, dim3(NB), dim3(64), 0, s, d2, 2000);
+    CK(hipStreamSynchronize(s));
+    census(c.name, "eager");
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+    hipLaunchKernelGGL(where_kernel, dim3(NB), dim3(64), 0, s, d2, 2000);
+    CK(hipStreamEndCapture(s, &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    CK(hipMemset(d2, 0, 2 * NB * sizeof(unsigned)));
+    CK(hipGraphLaunch(ge, s));
+    CK(hipStreamSynchronize(s));
+    census(c.name, "graph_on_masked_stream");
+    CK(hipMemset(d2, 0, 2 * NB * sizeof(unsigned)));
+    CK(hipGraphLaunch(ge, plain));
+    CK(hipStreamSynchronize(plain));
+    census(c.name, "graph_on_plain_stream");
+    CK(hipGraphExecDestroy(ge));
+    CK(hipGraphDestroy(g));
+    CK(hipStreamDestroy(s));
+  }
+  hipLaunchKernelGGL(where_kernel, dim3(NB), dim3(64), 0, plain, d2, 2000);
   CK(hipStreamSynchronize(plain));
-  report("graph_replayed_on_plain_stream");
-  CK(hipGraphExecDestroy(ge));
-  CK(hipGraphDestroy(g));
-  CK(hipStreamDestroy(s));
+  census("none", "plain_stream");
   CK(hipStreamDestroy(plain));
+  CK(hipFree(d2));
   CK(hipFree(d));
   return 0;
 }

@@ -16,6 +16,7 @@ import torch
 from torch import nn
 
 from ..ops import fused
+from ..ops.linear import MfmaLinear
 from .base import Flow
 
 
@@ -54,12 +55,50 @@ def coupling_transform(st, x_b, scale: float = 1.0):
     return _CouplingFn.apply(st, x_b, float(scale))
 
 
+class _CouplingInvFn(torch.autograd.Function):
+    """x_b = (y_b - t) e^-s, ldj = -sum s: the forward on the HIP kernel (coupling.hip's inverse
+    epilogue on the GPU, the torch composite on the CPU), an element-wise backward:
+    dL/dy_b = g e^-s, dL/dt = -g e^-s, dL/ds_hat = (-g x_b - gl)(scale - s^2 / scale)."""
+
+    @staticmethod
+    def forward(ctx, st, y, scale: float):
+        B, Dh = y.shape
+        dt = torch.float32 if y.is_cuda else (y.dtype if y.dtype == torch.float64 else torch.float32)
+        x = torch.empty(B, Dh, device=y.device, dtype=dt)
+        s = torch.empty(B, Dh, device=y.device, dtype=dt)
+        ldj = torch.empty(B, device=y.device, dtype=dt)
+        fused.coupling_fwd(st, y.to(dt).contiguous(), x, None, s, ldj, scale=scale, inverse=True,
+                           ldj_init=True)
+        ctx.save_for_backward(s, x)
+        ctx.scale, ctx.st_dtype, ctx.st_cols = scale, st.dtype, st.shape[1]
+        return x, ldj
+
+    @staticmethod
+    def backward(ctx, gx, gldj):
+        s, x = ctx.saved_tensors
+        B, Dh = x.shape
+        gx = gx if gx is not None else torch.zeros_like(x)
+        gl = gldj if gldj is not None else torch.zeros(B, device=x.device, dtype=x.dtype)
+        es = torch.exp(-s)
+        gy = gx * es
+        gs = (-gx * x - gl[:, None]) * (ctx.scale - s * s / ctx.scale)
+        dst = torch.zeros(B, ctx.st_cols, device=x.device, dtype=torch.float32)
+        dst[:, :Dh] = gs
+        dst[:, Dh:2 * Dh] = -gy
+        return dst.to(ctx.st_dtype), gy, None
+
+
+def coupling_inverse(st, y_b, scale: float = 1.0):
+    """Fused x_b, ldj of the inverse coupling (differentiable w.r.t. st and y_b)."""
+    return _CouplingInvFn.apply(st, y_b, float(scale))
+
+
 def mlp(d_in, hidden, n_hidden, d_out, act=nn.ReLU, zero_last=True):
     layers, d = [], d_in
     for _ in range(n_hidden):
-        layers += [nn.Linear(d, hidden), act()]
+        layers += [MfmaLinear(d, hidden), act()]
         d = hidden
-    last = nn.Linear(d, d_out)
+    last = MfmaLinear(d, d_out)
     if zero_last:
         nn.init.zeros_(last.weight)
         nn.init.zeros_(last.bias)
@@ -102,10 +141,8 @@ class AffineCoupling(Flow):
     def inverse(self, y, context=None):
         ya, yb = self._split(y)
         st = self._st(ya, context)
-        s = self.scale * torch.tanh(st[:, :self.d_b])
-        t = st[:, self.d_b:]
-        xb = (yb - t) * torch.exp(-s)
-        return self._join(ya, xb), -s.sum(1)
+        xb, ldj = coupling_inverse(st, yb, self.scale)
+        return self._join(ya, xb.to(y.dtype)), ldj
 
 
 class RealNVP(Flow):

@@ -19,6 +19,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from ..ops.linear import MfmaLinear
 from .base import Flow
 
 
@@ -94,7 +95,7 @@ class MADE(nn.Module):
         self.layers = nn.ModuleList(MaskedLinear(dims[i], dims[i + 1], masks[i])
                                     for i in range(len(masks)))
         self.act = act()
-        self.ctx = nn.Linear(context_dim, hidden) if (context_dim > 0 and n_hidden > 0) else None
+        self.ctx = MfmaLinear(context_dim, hidden) if (context_dim > 0 and n_hidden > 0) else None
         last = self.layers[-1]
         nn.init.zeros_(last.bias)
         with torch.no_grad():

@@ -50,12 +50,16 @@ class IAFEngine:
     def __init__(self, cfg: IAFVAEConfig, batch: int, data: torch.Tensor, device="cuda",
                  seed: int = 0, rank: int = 0, lr: float = 3e-4, betas=(0.9, 0.999),
                  eps: float = 1e-8, beta: float = 1.0, max_grad_norm: float = 0.0,
-                 model: IAFVAE | None = None, anneal: str = "none", anneal_iters: int = 10000):
+                 model: IAFVAE | None = None, anneal: str = "none", anneal_iters: int = 10000,
+                 optimizer="adam"):
         self.cfg, self.B = cfg, int(batch)
         self.device = torch.device(device)
         self.cdt = torch.bfloat16 if self.device.type == "cuda" else torch.float32
         self.seed, self.rank = int(seed), int(rank)
-        self.lr, self.betas, self.eps, self.beta = lr, betas, eps, float(beta)
+        # update rule: adam | rmsprop | sgd | rmsprop_momentum (fused flat kernel, optim.hip)
+        self.opt = fused.resolve_optimizer(optimizer, betas, eps)
+        self.lr, self.beta = lr, float(beta)
+        self.betas, self.eps = (self.opt.b1, self.opt.b2), self.opt.eps
         if anneal not in ("none", "reference", "theano"):
             raise ValueError(f"IAFEngine anneal must be none | reference | theano, got {anneal!r}")
         self.anneal, self.anneal_iters = anneal, int(anneal_iters)
@@ -95,6 +99,7 @@ class IAFEngine:
                     for n, s in ((f"dec.W{i}", (o, k)), (f"dec.b{i}", (o,)))])
         self.layout = L
         self.params = FlatParams(L, self.device, self.cdt)
+        self.params.v_init = self.opt.v_init
 
     def _alloc(self):
         cfg, B, dev, cdt = self.cfg, self.B, self.device, self.cdt
@@ -177,8 +182,7 @@ class IAFEngine:
                     s = self.layout.slots[name]
                     self.flow_mask[s.offset - lo:s.offset - lo + s.numel].copy_(m.reshape(-1))
         P.sync_compute()
-        P.m.zero_()
-        P.v.zero_()
+        P.reset_optimizer_state()
         self.step_t.zero_()
         self.rng_offset.zero_()
         if not hasattr(self, "_plans"):
@@ -359,7 +363,7 @@ class IAFEngine:
                           scale=self.gscale, max_norm=self.max_grad_norm,
                           base_scale=self.grad_scale_host)
         b1, b2 = self.betas
-        fused.flat_optimizer(fused.OPT_ADAM, P.master, P.grad, P.m, P.v,
+        fused.flat_optimizer(self.opt.kind, P.master, P.grad, P.m, P.v,
                              pbf=None if P.compute is P.master else P.compute, lr=self.lr,
                              b1=b1, b2=b2, eps=self.eps, wd=0.0, step=self.step_t,
                              gscale=self.gscale, skip=self.skip)

@@ -18,6 +18,7 @@ from torch import nn
 from ..distributions.functional import log_bern_logits, log_std_norm
 from ..flows.made import IAF
 from ..inference.elbo import FreeEnergy
+from ..ops.linear import MfmaLinear
 
 LOG2PI = math.log(2 * math.pi)
 
@@ -43,12 +44,14 @@ class IAFVAE(nn.Module):
         super().__init__()
         self.cfg = cfg
         H, dz, C = cfg.hidden, cfg.dim_z, cfg.context
-        self.encoder = nn.Sequential(nn.Linear(cfg.dim_x, H), nn.ReLU(), nn.Linear(H, H), nn.ReLU())
-        self.enc_out = nn.Linear(H, 2 * dz + C)
+        # dense layers: MFMA kernels on the GPU (ops.linear.MfmaLinear, bf16 operands, fp32
+        # accumulate), F.linear on the CPU
+        self.encoder = nn.Sequential(MfmaLinear(cfg.dim_x, H), nn.ReLU(), MfmaLinear(H, H), nn.ReLU())
+        self.enc_out = MfmaLinear(H, 2 * dz + C)
         self.flows = nn.ModuleList(IAF(dz, cfg.made_hidden, 1, context_dim=C, reverse=bool(k % 2))
                                    for k in range(cfg.n_flows))
-        self.decoder = nn.Sequential(nn.Linear(dz, H), nn.ReLU(), nn.Linear(H, H), nn.ReLU(),
-                                     nn.Linear(H, cfg.dim_x))
+        self.decoder = nn.Sequential(MfmaLinear(dz, H), nn.ReLU(), MfmaLinear(H, H), nn.ReLU(),
+                                     MfmaLinear(H, cfg.dim_x))
         nn.init.zeros_(self.enc_out.weight)
         nn.init.zeros_(self.enc_out.bias)
 

@@ -19,6 +19,7 @@ from torch import nn
 from ..distributions.functional import log_mvn
 from ..flows.planar import AmortizedPlanar
 from ..inference.elbo import amortized_free_energy
+from ..ops.linear import MfmaLinear, linear
 
 LOG2PI = math.log(2 * math.pi)
 
@@ -31,9 +32,9 @@ class AffineEncoder(nn.Module):
         self.dz, self.K = dim_z, K
         out = 2 * dim_z + 2 * dim_z * K + K
         if hidden:
-            self.net = nn.Sequential(nn.Linear(dim_x, hidden), nn.ReLU(), nn.Linear(hidden, out))
+            self.net = nn.Sequential(MfmaLinear(dim_x, hidden), nn.ReLU(), MfmaLinear(hidden, out))
         else:
-            self.net = nn.Linear(dim_x, out)
+            self.net = MfmaLinear(dim_x, out)
         for p in self.net.parameters():
             nn.init.normal_(p, std=0.05)
 
@@ -60,7 +61,7 @@ class LinearGaussianLatent(nn.Module):
         self.logvar_lik = nn.Parameter(torch.zeros(dim_x))
 
     def log_joint(self, x, z):
-        xhat = z @ self.A.t() + self.B
+        xhat = linear(z, self.A, self.B)      # x = A z + B
         return log_mvn(x, xhat, self.logvar_lik.expand_as(x)) + log_mvn(
             z, self.mu_z.expand_as(z), self.logvar_z.expand_as(z))
 
@@ -106,7 +107,7 @@ class GMMPriorLatent(nn.Module):
         return torch.logsumexp(comps + lw, 1)
 
     def log_joint(self, x, z):
-        xhat = z @ self.A.t() + self.B
+        xhat = linear(z, self.A, self.B)
         return log_mvn(x, xhat, self.logvar_lik.expand_as(x)) + self.log_prior(z)
 
     def loss(self, x, beta: float = 1.0, generator=None):

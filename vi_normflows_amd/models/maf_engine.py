@@ -73,7 +73,8 @@ class MAFEngineConfig:
 class MAFEngine:
     def __init__(self, cfg: MAFEngineConfig, batch: int, device="cuda", seed: int = 0,
                  rank: int = 0, lr: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, max_grad_norm: float = 0.0, lr_warmup: float = 0.0):
+                 weight_decay: float = 0.0, max_grad_norm: float = 0.0, lr_warmup: float = 0.0,
+                 optimizer="adam"):
         self.cfg = cfg
         self.B = int(batch)
         self.device = torch.device(device)
@@ -81,8 +82,9 @@ class MAFEngine:
         self.cdt = torch.bfloat16 if gpu else torch.float32
         self.fp8 = gpu and cfg.precision == "fp8"
         self.seed, self.rank = int(seed), int(rank)
-        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
-        self.opt_kind = fused.OPT_ADAM
+        self.opt = fused.resolve_optimizer(optimizer, betas, eps)
+        self.lr, self.wd = lr, weight_decay
+        self.opt_kind, self.betas, self.eps = self.opt.kind, (self.opt.b1, self.opt.b2), self.opt.eps
         self.max_grad_norm = float(max_grad_norm)
         self.lr_warmup = float(lr_warmup)
         self.grad_scale_host = 1.0
@@ -97,6 +99,7 @@ class MAFEngine:
                              (f"l{l}.W2", (2 * D, H)), (f"l{l}.b2", (2 * D,))])
         self.layout = layout
         self.params = FlatParams(layout, self.device, self.cdt)
+        self.params.v_init = self.opt.v_init
         s0, s1 = layout.slots["l0.W1"], layout.slots["l1.W1"] if L > 1 else None
         self.layer_stride = (s1.offset - s0.offset) if s1 is not None else layout.total
         self._build_masks()
@@ -281,8 +284,7 @@ class MAFEngine:
             P.p(f"l{l}.W2").copy_(W2.to(self.device) * mk["M2"])
             P.p(f"l{l}.b2").zero_()
         P.sync_compute()
-        P.m.zero_()
-        P.v.zero_()
+        P.reset_optimizer_state()
         self.step_t.zero_()
         self.rng_offset.zero_()
         if self.fp8:

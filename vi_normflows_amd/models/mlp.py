@@ -23,6 +23,8 @@ import numpy as np
 import torch
 from torch import nn
 
+from ..ops.linear import MfmaLinear
+
 
 def flat_size(Din: int, H: int, L: int, Dout: int) -> int:
     return Din * H + H + Dout * H + Dout + (L - 1) * (H * H + H)
@@ -204,7 +206,8 @@ class FlatMLP(nn.Module):
         super().__init__()
         self.Din, self.H, self.L, self.Dout = Din, H, L, Dout
         dims = [Din] + [H] * L + [Dout]
-        self.linears = nn.ModuleList(nn.Linear(dims[i], dims[i + 1]) for i in range(L + 1))
+        # GPU: the MFMA kernels (ops.linear), CPU: F.linear - same parameters as nn.Linear
+        self.linears = nn.ModuleList(MfmaLinear(dims[i], dims[i + 1]) for i in range(L + 1))
         self.act = act
         self.out_act = out_act
 

@@ -109,7 +109,7 @@ class RealNVPVI:
 
     def __init__(self, cfg: RealNVPConfig, batch: int, device="cuda",
                  compute_dtype: torch.dtype | None = None, seed: int = 0, rank: int = 0,
-                 lr: float = 1e-4, optimizer: int = fused.OPT_ADAM, betas=(0.9, 0.999),
+                 lr: float = 1e-4, optimizer="adam", betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.0, max_grad_norm: float = 0.0,
                  lr_warmup: float = 0.0):
         self.cfg = cfg
@@ -120,7 +120,10 @@ class RealNVPVI:
         self.cdt = compute_dtype
         self.seed = int(seed)
         self.rank = int(rank)
-        self.lr, self.opt_kind, self.betas, self.eps, self.wd = lr, optimizer, betas, eps, weight_decay
+        # update rule: adam | rmsprop | sgd | rmsprop_momentum (or an OPT_* kind), fused flat kernel
+        self.opt = fused.resolve_optimizer(optimizer, betas, eps)
+        self.lr, self.wd = lr, weight_decay
+        self.opt_kind, self.betas, self.eps = self.opt.kind, (self.opt.b1, self.opt.b2), self.opt.eps
         self.max_grad_norm = float(max_grad_norm)
         self.lr_warmup = float(lr_warmup)   # linear lr ramp over the first steps (device step)
         self.grad_scale_host = 1.0
@@ -140,6 +143,7 @@ class RealNVPVI:
             layout.add_unit(ts)
         self.layout = layout
         self.params = FlatParams(layout, self.device, self.cdt)
+        self.params.v_init = self.opt.v_init
         self._alloc_state()
         self._alloc_workspace()
         self.init_params(seed)
@@ -278,8 +282,7 @@ class RealNVPVI:
         P.p("base.mu").zero_()
         P.p("base.logvar").zero_()
         P.sync_compute()
-        P.m.zero_()
-        P.v.zero_()
+        P.reset_optimizer_state()
         self.step_t.zero_()
         self.rng_offset.zero_()
 
@@ -619,6 +622,50 @@ class RealNVPVI:
         z = torch.cat([A, Bh], 1)[:n].clone()
         logq = (self.logq0 - self.ldj)[:n].clone()
         return z, logq
+
+    @torch.no_grad()
+    def inverse(self, z: torch.Tensor):
+        """z_K -> (z0, ldj_inv) through the coupling layers in reverse, on the workspace
+        (n <= batch rows; overwrites the step's saved activations, so call it between steps):
+
+            h_l = (h_{l+2} - t(h_{l+1})) e^{-s(h_{l+1})},  ldj_inv = -sum_l sum_j s_l
+
+        Each layer's conditioner runs on the MFMA kernels from the bf16 copy of h_{l+1} (the
+        operand the forward used), and the inverse affine map + log-det on the HIP coupling
+        epilogue (coupling.hip, ``inverse``), which also writes the bf16 conditioner input of
+        the next (lower) layer. The reference's flows are forward-only
+        (``normflows/normflows/flows.py:8-34``); the inverse is a north-star addition."""
+        cfg = self.cfg
+        n, D = z.shape
+        assert D == cfg.dim and n <= self.B, (z.shape, self.B)
+        Dh, L = cfg.half, cfg.n_layers
+        A, Bh, ia, ib = self.zK_halves()
+        A.zero_()
+        Bh.zero_()
+        A[:n].copy_(z[:, :Dh])
+        Bh[:n].copy_(z[:, Dh:])
+        # bf16 conditioner input of layer L-1: h_L (zero pad columns)
+        top = self.Hbf[L - 1]
+        top[:, Dh:].zero_()
+        top[:, :Dh].copy_(self.h(L))
+        for l in range(L - 1, -1, -1):
+            st = self._conditioner_fwd(l, self.Hbf[l])
+            nxt = self.Hbf[l - 1] if l > 0 else None
+            fused.coupling_fwd(st, self.h(l + 2), self.h(l), ybf=nxt, ssav=None, ldj=self.ldj,
+                               scale=cfg.scale_bound, inverse=True, ldj_init=(l == L - 1))
+        return self.z0[:n].clone(), self.ldj[:n].clone()
+
+    @torch.no_grad()
+    def log_prob(self, z: torch.Tensor) -> torch.Tensor:
+        """log q_K(z) of given points z [n, D]: the inverse (see :meth:`inverse`) back to z0,
+        plus the learnable diagonal-Gaussian base density,
+        log q_K(z) = log q0(z0) - sum_l log|det J_l| = log q0(z0) + ldj_inv."""
+        z0, ldj_inv = self.inverse(z)
+        P = self.params
+        mu, lv = P.p("base.mu"), P.p("base.logvar")
+        q = (z0 - mu) * torch.exp(-0.5 * lv)
+        lq0 = -0.5 * self.cfg.dim * math.log(2 * math.pi) - 0.5 * lv.sum() - 0.5 * (q * q).sum(1)
+        return lq0 + ldj_inv
 
     def state_dict(self) -> dict:
         return {"params": self.params.state_dict(), "step": self.step_t.detach().cpu(),

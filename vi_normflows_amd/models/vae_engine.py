@@ -45,7 +45,8 @@ class PlanarVAEEngine:
 
     def __init__(self, cfg: VAEConfig | None = None, batch: int = 128, device="cuda",
                  seed: int = 0, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 anneal: str = "none", anneal_iters: int = 10000, init_scale: float = 0.05):
+                 anneal: str = "none", anneal_iters: int = 10000, init_scale: float = 0.05,
+                 optimizer="adam"):
         cfg = cfg or VAEConfig()
         if cfg.flow_variant != "paper" or cfg.encode_layout != "paper":
             raise ValueError("the engine implements the paper planar update / encoder layout")
@@ -55,7 +56,9 @@ class PlanarVAEEngine:
         self.B = int(batch)
         self.device = torch.device(device)
         self.seed = int(seed)
-        self.lr, self.betas, self.eps = lr, betas, eps
+        # update rule: adam | rmsprop | sgd | rmsprop_momentum (fused flat kernel, optim.hip)
+        self.opt = fused.resolve_optimizer(optimizer, betas, eps)
+        self.lr, self.betas, self.eps = lr, (self.opt.b1, self.opt.b2), self.opt.eps
         self.anneal, self.anneal_iters = anneal, anneal_iters
         dz, K, L, Din = cfg.dim_z, cfg.K, cfg.hidden_layers, cfg.dim_x
         self.De = 2 * dz + 2 * dz * K + K
@@ -69,6 +72,8 @@ class PlanarVAEEngine:
             layout.add_unit(ts)
         self.layout = layout
         self.params = FlatParams(layout, self.device, torch.float32)
+        self.params.v_init = self.opt.v_init
+        self.params.reset_optimizer_state()
         self.offs = [layout.slots[n].offset for n in _mlp_names("enc", L) + _mlp_names("dec", L)]
         dev = self.device
         self.x = torch.zeros(self.B, Din, device=dev)
@@ -187,19 +192,18 @@ class PlanarVAEEngine:
         if not (1 <= L <= 4 and 1 <= dz <= 64 and dz % 4 == 0 and 0 <= K <= 8
                 and Din % 4 == 0 and 4 <= Din <= 1024):
             return False
-        try:
-            from ..ops._ext import native
+        # the native library's own LDS budget: a missing / broken library raises here (a GPU job
+        # never drops to the module path because the engine could not load)
+        from ..ops._ext import native
 
-            return int(native().vae_rows_lds_bytes(Din, dz, K)) <= 163840
-        except Exception:   # no native library on this machine: the engine cannot run anyway
-            return False
+        return int(native().vae_rows_lds_bytes(Din, dz, K)) <= 163840
 
     def optimizer_step(self):
         P = self.params
         fused.sumsq_guard(P.grad, self._partials, out_sumsq=self.gnorm2, skip=self.skip,
                           scale=self.gscale, max_norm=0.0, base_scale=self.grad_scale_host)
         b1, b2 = self.betas
-        fused.flat_optimizer(fused.OPT_ADAM, P.master, P.grad, P.m, P.v, pbf=None, lr=self.lr,
+        fused.flat_optimizer(self.opt.kind, P.master, P.grad, P.m, P.v, pbf=None, lr=self.lr,
                              b1=b1, b2=b2, eps=self.eps, wd=0.0, step=self.step_t,
                              gscale=self.gscale, skip=self.skip)
         self.n_skipped.add_(self.skip)

@@ -7,6 +7,8 @@ training step built from them is allocation-free and hipGraph-capturable.
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
+
 import torch
 
 from . import reference as ref
@@ -20,6 +22,57 @@ OPT_ADAM = 0
 OPT_RMSPROP = 1
 OPT_SGD_MOMENTUM = 2
 OPT_RMSPROP_MOMENTUM = 3
+
+
+@dataclass(frozen=True)
+class EngineOptimizer:
+    """One of the reference's four update rules as the fused flat kernel runs it
+    (csrc/kernels/optim.hip ``opt_update``), with the hyper-parameters of the rule it
+    reproduces (inference/optimizers.py):
+
+    * ``adam``              autograd / torch Adam (b1 0.9, b2 0.999, eps 1e-8)  optimization.py:118
+    * ``rmsprop``           autograd rmsprop (gamma 0.9, eps 1e-8, accumulator starts at 1)
+                            get_data.py:140
+    * ``sgd``               autograd sgd, mass 0.9: v = m v - (1 - m) g; x += lr v
+                            experimentation.py:109
+    * ``rmsprop_momentum``  Lasagne rmsprop (rho 0.9, eps 1e-6) + momentum 0.9
+                            theano_implement.py:187-188
+    """
+    name: str
+    kind: int
+    b1: float = 0.9
+    b2: float = 0.999
+    eps: float = 1e-8
+    v_init: float = 0.0
+
+
+def engine_optimizer(name: str, **kw) -> EngineOptimizer:
+    n = name.lower().replace("+", "_")
+    if n == "adam":
+        b = kw.get("betas", (0.9, 0.999))
+        return EngineOptimizer("adam", OPT_ADAM, b[0], b[1], kw.get("eps", 1e-8), 0.0)
+    if n == "rmsprop":
+        return EngineOptimizer("rmsprop", OPT_RMSPROP, 0.0, kw.get("gamma", 0.9),
+                               kw.get("eps", 1e-8), 1.0)
+    if n == "sgd":
+        return EngineOptimizer("sgd", OPT_SGD_MOMENTUM, kw.get("mass", 0.9), 0.0, 0.0, 0.0)
+    if n == "rmsprop_momentum":
+        return EngineOptimizer("rmsprop_momentum", OPT_RMSPROP_MOMENTUM, kw.get("momentum", 0.9),
+                               kw.get("rho", 0.9), kw.get("eps", 1e-6), 0.0)
+    raise KeyError(f"unknown optimizer {name!r} (adam | rmsprop | sgd | rmsprop_momentum)")
+
+
+_KIND_NAMES = {OPT_ADAM: "adam", OPT_RMSPROP: "rmsprop", OPT_SGD_MOMENTUM: "sgd",
+               OPT_RMSPROP_MOMENTUM: "rmsprop_momentum"}
+
+
+def resolve_optimizer(spec, betas=(0.9, 0.999), eps: float = 1e-8) -> EngineOptimizer:
+    """An engine's ``optimizer`` argument: an :class:`EngineOptimizer`, a rule name, or an
+    ``OPT_*`` kind; ``betas`` / ``eps`` are Adam's (the other rules use the reference's own)."""
+    if isinstance(spec, EngineOptimizer):
+        return spec
+    name = _KIND_NAMES[int(spec)] if isinstance(spec, int) else str(spec)
+    return engine_optimizer(name, betas=betas, eps=eps) if name == "adam" else engine_optimizer(name)
 
 
 def _gpu(t: torch.Tensor) -> bool:

@@ -26,6 +26,12 @@ from .utils.faults import maybe_inject
 from .utils.metrics import JsonlLogger, append_free_energy
 
 
+# update rules the fused flat optimizer of every engine runs (ops.fused.engine_optimizer): the
+# reference's Adam (optimization.py:118), RMSProp (get_data.py:140), SGD-momentum
+# (experimentation.py:109) and RMSProp + momentum (theano_implement.py:187-188)
+ENGINE_OPTIMIZERS = ("adam", "rmsprop", "sgd", "rmsprop_momentum", "rmsprop+momentum")
+
+
 def _device(cfg, info):
     if cfg.device == "cpu":
         return torch.device("cpu")
@@ -65,7 +71,8 @@ def run_realnvp(cfg, out, info, logger):
                        target=cfg.extra.get("target", "banana"), anneal=cfg.schedule,
                        anneal_iters=cfg.iters, banana_pairing=cfg.pairing)
     eng = RealNVPVI(rc, batch=cfg.batch, device=dev, seed=cfg.seed, rank=info.rank, lr=cfg.lr,
-                    lr_warmup=cfg.lr_warmup, max_grad_norm=cfg.max_grad_norm)
+                    lr_warmup=cfg.lr_warmup, max_grad_norm=cfg.max_grad_norm,
+                    optimizer=cfg.optimizer)
     ckpt = out / "ckpt.pt"
     if cfg.extra.get("resume"):
         load_engine(eng, cfg.extra["resume"], info.rank)
@@ -84,7 +91,7 @@ def run_realnvp(cfg, out, info, logger):
     for t in range(start, cfg.iters):
         maybe_inject(t, info.rank)
         run.step()
-        if t % cfg.log_every == 0 or t == cfg.iters - 1:
+        if t == start or t % cfg.log_every == 0 or t == cfg.iters - 1:   # first step logged too
             F = float(eng.loss.item())
             el = time.perf_counter() - t0
             logger.log({"step": t, "F": F, "beta": float(eng.beta.item()),
@@ -134,7 +141,7 @@ def run_planar_vae(cfg, out, info, logger):
     # CPU: only on request (extra.engine="force": the engine's autograd reference step, e.g.
     # the gloo DP tests of the engine's runner contract)
     want = cfg.extra.get("engine", True)
-    engine_ok = (cfg.optimizer == "adam" and cfg.schedule in ("none", "reference")
+    engine_ok = (cfg.optimizer in ENGINE_OPTIMIZERS and cfg.schedule in ("none", "reference")
                  and ((dev.type == "cuda" and want is not False and PlanarVAEEngine.supported(vcfg))
                       or (dev.type != "cuda" and want == "force" and cfg.hidden == 64)))
     if engine_ok:
@@ -144,7 +151,8 @@ def run_planar_vae(cfg, out, info, logger):
         from .parallel.runner import DataParallelRunner
 
         eng = PlanarVAEEngine(vcfg, batch=cfg.batch, device=dev, seed=rank_seed(cfg.seed, info.rank),
-                              lr=cfg.lr, anneal=cfg.schedule, anneal_iters=cfg.iters)
+                              lr=cfg.lr, anneal=cfg.schedule, anneal_iters=cfg.iters,
+                              optimizer=cfg.optimizer)
         eng.load_module(vae)
 
         def full(xb):   # the graph has a static batch: a short last batch is topped up by
@@ -155,8 +163,7 @@ def run_planar_vae(cfg, out, info, logger):
         run = DataParallelRunner(eng, info)
         if dev.type == "cuda" and cfg.extra.get("graph", True):
             run.capture(warmup=1)
-        eng.params.m.zero_()           # the capture warm-up stepped Adam: start from the init
-        eng.params.v.zero_()
+        eng.params.reset_optimizer_state()   # the capture warm-up stepped the optimizer
         eng.load_module(vae)
         eng.step_t.zero_()
         eng.n_skipped.zero_()
@@ -172,7 +179,8 @@ def run_planar_vae(cfg, out, info, logger):
                 # (read from the step itself, no extra passes: SURVEY Q10), plus skipped steps
                 F = eng.loss.item()
                 if logger is not None:
-                    logger.log({"step": t + 1, "F": F, "beta": eng.beta.item(),
+                    logger.log({"step": t + 1, "F": F, "beta": eng.beta.item(), "path": "engine",
+                                "optimizer": eng.opt.name,
                                 "grad_norm": math.sqrt(max(float(eng.gnorm2.item()), 0.0)),
                                 "skipped": float(eng.n_skipped.item())})
             if info.is_main and recon_every > 0 and ((t + 1) % recon_every == 0 or last):
@@ -207,7 +215,7 @@ def run_planar_vae(cfg, out, info, logger):
     if info.is_main:
         vae.cpu().save_reference(out / f"weights_phi_{cfg.K}.npy", out / f"weights_theta_{cfg.K}.npy")
         append_free_energy(out / "free_energy.txt", cfg.K, F * cfg.batch)  # per-batch units (Q8)
-    return {"free_energy_per_sample": F}
+    return {"free_energy_per_sample": F, "engine": "module"}
 
 
 def run_iaf_vae(cfg, out, info, logger):
@@ -220,7 +228,7 @@ def run_iaf_vae(cfg, out, info, logger):
     model = IAFVAE(icfg).to(dev)
     X = synthetic_images(cfg.extra.get("n_data", 8192), seed=cfg.seed + info.rank, device=dev)
     nb = X.shape[0] // cfg.batch
-    if (dev.type == "cuda" and cfg.optimizer == "adam" and nb > 0
+    if (dev.type == "cuda" and cfg.optimizer in ENGINE_OPTIMIZERS and nb > 0
             and cfg.schedule in ("none", "reference", "theano") and cfg.extra.get("engine", True)):
         # models/iaf_engine.py: flat buffers, explicit backward, one hipGraph (DP: the runner's
         # bucketed all-reduce; rank 0's parameters are broadcast)
@@ -230,13 +238,13 @@ def run_iaf_vae(cfg, out, info, logger):
 
         eng = IAFEngine(icfg, cfg.batch, X[:nb * cfg.batch].reshape(nb * cfg.batch, -1),
                         device=dev, seed=rank_seed(cfg.seed, info.rank), rank=info.rank,
-                        lr=cfg.lr, model=model, anneal=cfg.schedule, anneal_iters=cfg.iters)
+                        lr=cfg.lr, model=model, anneal=cfg.schedule, anneal_iters=cfg.iters,
+                        optimizer=cfg.optimizer)
         run = DataParallelRunner(eng, info)
         if cfg.extra.get("graph", True):
             run.capture(warmup=1)
             eng.load_module(model)     # the capture warm-up stepped Adam: start from the init
-            eng.params.m.zero_()
-            eng.params.v.zero_()
+            eng.params.reset_optimizer_state()
             eng.step_t.zero_()         # ... and advanced the schedule: beta_t restarts at t = 0
             eng.n_skipped.zero_()
         t0 = time.perf_counter()
@@ -244,7 +252,8 @@ def run_iaf_vae(cfg, out, info, logger):
             run.step()
             if t % cfg.log_every == 0 or t == cfg.iters - 1:
                 F = float(eng.loss.item())
-                logger.log({"step": t, "F": F, "beta": float(eng.beta_t.item()),
+                logger.log({"step": t, "F": F, "beta": float(eng.beta_t.item()), "path": "engine",
+                            "optimizer": eng.opt.name,
                             "grad_norm": math.sqrt(max(float(eng.gnorm2.item()), 0.0)),
                             "skipped": float(eng.n_skipped.item()),
                             "samples_per_s": (t + 1) * cfg.batch * info.world
@@ -262,7 +271,7 @@ def run_iaf_vae(cfg, out, info, logger):
                  TrainConfig(iters=cfg.iters, lr=cfg.lr, optimizer=cfg.optimizer,
                              schedule=cfg.schedule, log_every=cfg.log_every), logger=logger)
     tr.fit()
-    return {"free_energy": tr.history[-1]["F"]}
+    return {"free_energy": tr.history[-1]["F"], "engine": "module"}
 
 
 def run_maf(cfg, out, info, logger):
@@ -276,7 +285,8 @@ def run_maf(cfg, out, info, logger):
 
         mc = MAFEngineConfig(dim=cfg.dim, n_layers=cfg.K, hidden=cfg.hidden,
                              precision=cfg.extra.get("precision", "fp8"))
-        eng = MAFEngine(mc, batch=cfg.batch, device=dev, seed=cfg.seed, rank=info.rank, lr=cfg.lr)
+        eng = MAFEngine(mc, batch=cfg.batch, device=dev, seed=cfg.seed, rank=info.rank, lr=cfg.lr,
+                        optimizer=cfg.optimizer)
         run = DataParallelRunner(eng, info)
         if dev.type == "cuda" and cfg.extra.get("graph", True):
             run.capture(warmup=1)

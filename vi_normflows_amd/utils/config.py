@@ -104,6 +104,14 @@ PRESETS: dict[str, RunConfig] = {
                                        device="cuda", K=32, dim=784, hidden=1024, batch=65536,
                                        iters=200, lr=1e-3, lr_warmup=100.0, schedule="none",
                                        pairing="split"),
+    # the reference's annealed objective on the headline model: beta_t = min(1, 0.001 +
+    # t / min(iters / 4, 1e4)) (normflows/optimization.py:71-72) with the reference's Adam lr
+    # 1e-4 - plus the 100-step warm-up this 72 M-parameter flow needs (without it the first
+    # sign step diverged); the non-annealed presets above are what bench.py times
+    "config3_realnvp32_annealed": RunConfig(name="config3_realnvp32_annealed", task="realnvp_vi",
+                                            device="cuda", K=32, dim=784, hidden=1024,
+                                            batch=65536, iters=2000, lr=1e-4, lr_warmup=100.0,
+                                            schedule="reference", pairing="split"),
     "config4_iaf10_vae": RunConfig(name="config4_iaf10_vae", task="iaf_vae", device="cuda", K=10,
                                    dim=3072, hidden=1024, dim_z=256, batch=1024, iters=200,
                                    lr=3e-4),

@@ -76,6 +76,7 @@ class FlatParams:
         self.grad = torch.zeros_like(self.master)
         self.m = torch.zeros_like(self.master)
         self.v = torch.zeros_like(self.master)
+        self.v_init = 0.0     # optimizer's second-moment start value (autograd RMSProp: 1.0)
         if compute_dtype == torch.float32:
             self.compute = self.master
         else:
@@ -93,6 +94,12 @@ class FlatParams:
     def sync_compute(self) -> None:
         if self.compute is not self.master:
             self.compute.copy_(self.master)
+
+    def reset_optimizer_state(self) -> None:
+        """Zero the first moment and start the second at ``v_init`` (0 for Adam / SGD /
+        Lasagne RMSProp+momentum, 1 for autograd's RMSProp, optimizers.AutogradRMSprop)."""
+        self.m.zero_()
+        self.v.fill_(self.v_init)
 
     def state_dict(self) -> dict:
         return {"master": self.master.detach().cpu(), "m": self.m.detach().cpu(),
