@@ -88,6 +88,17 @@ case $name in
     tag=${2:-t}
     timeout -k 10 900 python -u -m pytest $1 -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > $O/$tag.txt 2>&1 || { tail -40 $O/$tag.txt; exit 1; }
     tail -3 $O/$tag.txt ;;
+  tests_all)      # as "tests" but every test runs (failures are listed, the chain continues
+                  # unless the run hung or crashed)
+    tag=${2:-t}
+    timeout -k 10 900 python -u -m pytest $1 -m gpu -q --timeout 240 --timeout-method thread -p no:cacheprovider > $O/$tag.txt 2>&1
+    rc=$?; tail -12 $O/$tag.txt; [ $rc -le 1 ] || exit $rc ;;
+  dp_contention)  # RCCL CU-occupancy emulation on the headline step (bench/dp_contention.py)
+    timeout -k 10 600 python -m vi_normflows_amd.bench.dp_contention "$@" > $O/dpc.jsonl 2> $O/dpc.err || { tail -20 $O/dpc.err; exit 1; }
+    cat $O/dpc.jsonl ;;
+  partition)      # backward's chain and weight gradients on two CU-masked streams (bench/partition_probe.py)
+    timeout -k 10 600 python -m vi_normflows_amd.bench.partition_probe "$@" > $O/part.jsonl 2> $O/part.err || { tail -20 $O/part.err; exit 1; }
+    cat $O/part.jsonl ;;
   bench)          # headline bench on this box: args [tag] [extra bench args]
     tag=${1:-base}; shift
     timeout -k 10 240 python bench.py --steps 20 --warmup 5 "$@" > $O/$tag.json 2> $O/$tag.err || { tail -20 $O/$tag.err; exit 1; }

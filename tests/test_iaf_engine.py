@@ -167,6 +167,55 @@ def test_iaf_engine_graph_step_bitwise_gpu(gpu):
     assert not diff, f"graph replay differs from eager, first buffers: {diff[:8]}"
 
 
+def _first_diff(a_bufs, b_bufs):
+    for (n, a), (_, b) in zip(a_bufs, b_bufs):
+        if not torch.equal(a, b):
+            nan = bool(torch.isnan(a).any() or torch.isnan(b).any())
+            return n, float((a.float() - b.float()).abs().nan_to_num(1e30).max()), nan
+    return None
+
+
+@pytest.mark.gpu
+def test_iaf_engine_two_instances_bitwise_gpu(gpu):
+    """Two engines built the same way step bitwise alike, step by step (the caching allocator
+    hands the second one different memory). The first differing buffer in compute order names
+    an op whose result depends on memory it did not write."""
+    cfg = IAFVAEConfig()
+    B = 1024
+    data = synthetic_images(2 * B, cfg.image_shape, seed=1, device=gpu).reshape(2 * B, -1)
+    a = IAFEngine(cfg, B, data, device=gpu, seed=7)
+    b = IAFEngine(cfg, B, data, device=gpu, seed=7)
+    for step in range(3):
+        a.train_step()
+        b.train_step()
+        torch.cuda.synchronize()
+        d = _first_diff(_iaf_step_buffers(a), _iaf_step_buffers(b))
+        assert d is None, f"step {step}: first differing buffer {d}"
+        assert torch.equal(a.params.master, b.params.master), f"step {step}: master"
+
+
+@pytest.mark.gpu
+def test_iaf_engine_poisoned_allocator_gpu(gpu):
+    """Every byte the step reads it has written: the caching allocator's free memory is filled
+    with NaN before the engine is built (its buffers and every per-step temporary come from
+    it), and one forward + backward must leave no NaN anywhere; the first NaN buffer in compute
+    order names the op that read memory it never wrote."""
+    cfg = IAFVAEConfig()
+    B = 1024
+    data = synthetic_images(2 * B, cfg.image_shape, seed=1, device=gpu).reshape(2 * B, -1)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    junk = torch.full((3 << 28,), float("nan"), device=gpu)   # 3 GiB of NaN
+    del junk
+    e = IAFEngine(cfg, B, data, device=gpu, seed=7)
+    for step in range(2):
+        e.train_step()
+        torch.cuda.synchronize()
+        bad = [n for n, t in _iaf_step_buffers(e) if not torch.isfinite(t.float()).all()]
+        assert not bad, f"step {step}: non-finite buffers (compute order) {bad[:6]}"
+        assert torch.isfinite(e.params.master).all()
+
+
 @pytest.mark.gpu
 def test_iaf_engine_graph_replay_gpu(gpu):
     """A captured step replays the eager step bitwise: after 3 steps from the same state (1

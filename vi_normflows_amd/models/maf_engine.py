@@ -89,6 +89,7 @@ class MAFEngine:
         self.lr_warmup = float(lr_warmup)
         self.grad_scale_host = 1.0
         self.unit_ready_hook = None
+        self.wgrad_fence_hook = None  # callable() before each weight-gradient launch (DP runner)
         self.data_override = None      # fixed data [B, D] (tests)
         D, H, L = cfg.dim, cfg.hidden, cfg.n_layers
         if gpu:
@@ -507,7 +508,8 @@ class MAFEngine:
         L = cfg.n_layers
         steady8 = self.fp8_bwd and self._gscale_ready
         plan = self._wgrad_plan_f8() if steady8 and self.f8_wgrad else self._wgrad_plan()
-        sched = gemm.WgradScheduler(plan, plan.unit_ends, self._wchunk, self.unit_ready_hook)
+        sched = gemm.WgradScheduler(plan, plan.unit_ends, self._wchunk, self.unit_ready_hook,
+                                    self.wgrad_fence_hook)
         gu, gx = self.gU, self.gX
         WT = self._weights_t() if self.wt_dgrad else None
         if steady8:

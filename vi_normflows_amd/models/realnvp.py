@@ -128,6 +128,7 @@ class RealNVPVI:
         self.lr_warmup = float(lr_warmup)   # linear lr ramp over the first steps (device step)
         self.grad_scale_host = 1.0
         self.unit_ready_hook = None   # callable(unit_idx) after a unit's grads are final
+        self.wgrad_fence_hook = None  # callable() before each weight-gradient launch (DP runner)
         self.eps_override = None      # fixed base noise [B, D] (tests); None -> Philox sampler
         # DP runner: persistent GEMM grid in the forward only (parallel/runner.py)
         self.persist_forward_only = False
@@ -443,7 +444,7 @@ class RealNVPVI:
         c = -1.0 / self.B
         plan = self._wgrad_plan()
         sched = gemm.WgradScheduler(plan, [(l + 1, plan.layer_end[l]) for l in range(L - 1, -1, -1)],
-                                    self._wchunk, self.unit_ready_hook)
+                                    self._wchunk, self.unit_ready_hook, self.wgrad_fence_hook)
         fuse = self.cpl_fuse
         side = self.defer_stream
         main = torch.cuda.current_stream(self.device) if side is not None else None

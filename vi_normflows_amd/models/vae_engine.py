@@ -150,7 +150,14 @@ class PlanarVAEEngine:
 
     def _reference_forward_backward(self):
         """Autograd through the PlanarVAE composite on views of the flat buffer (CPU path and
-        the GPU tests' fp32 reference)."""
+        the GPU tests' fp32 reference: its dense layers run the explicit fp32 torch oracle,
+        ``ops.gemm.oracle()``, not the bf16 MFMA module path)."""
+        from ..ops import gemm
+
+        with gemm.oracle():
+            self._reference_fb()
+
+    def _reference_fb(self):
         model = self.to_module(PlanarVAE(self.cfg).to(self.device))
         eps = self.eps_override
         if eps is None:

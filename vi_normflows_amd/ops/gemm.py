@@ -346,16 +346,22 @@ class WgradScheduler:
     the plan's tiles below ``end_tile``. :meth:`ready` (call after a layer's input-gradient
     chain) launches every full chunk of ``chunk`` tiles now available (the CU count: one tile
     per CU per launch), with ``final=True`` the rest as well; ``hook(unit)`` fires once all of
-    a unit's tiles are issued (the DP reducer's bucket trigger)."""
+    a unit's tiles are issued (the DP reducer's bucket trigger). ``fence()`` (if given) runs
+    before every launch: the DP runner makes it wait for the all-reduces already in flight, so
+    a launch of exactly one tile per CU never starts while RCCL kernels hold CUs (a held CU
+    would push its tile into a second ~2.2 ms round)."""
 
-    def __init__(self, plan: WgradPlan, unit_ends, chunk: int, hook=None):
+    def __init__(self, plan: WgradPlan, unit_ends, chunk: int, hook=None, fence=None):
         self.plan, self.unit_ends, self.chunk, self.hook = plan, list(unit_ends), int(chunk), hook
+        self.fence = fence
         self.launched = 0
         self._next = 0
 
     def ready(self, avail_end: int, final: bool = False) -> None:
         while avail_end - self.launched >= self.chunk or (final and self.launched < avail_end):
             n = min(self.chunk, avail_end - self.launched)
+            if self.fence is not None:
+                self.fence()
             self.plan.run(self.launched, n)
             self.launched += n
             while (self._next < len(self.unit_ends)

@@ -11,6 +11,8 @@ On CPU the composite ``F.linear(x, W * mask, b)`` is used.
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 import torch.nn.functional as F
 
@@ -118,15 +120,25 @@ class MaskPlan:
                                          dtype=torch.int16).to(dev)
 
 
+# Plans cached per mask TENSOR. The key is the storage address + shape + version, and the
+# entry holds a weak reference to the tensor it was built from: a lookup hits only while that
+# very tensor is alive. (Keyed on the address alone, a mask freed by one model and a new mask
+# of the same shape allocated at the same address - a different MADE ordering - would get the
+# old tile ranges: silently wrong products that depended on the process's allocation history.
+# tests/test_iaf_engine.py::test_iaf_engine_two_instances_bitwise_gpu caught exactly that.)
 _PLANS: dict = {}
 
 
 def plan_for(mask: torch.Tensor) -> MaskPlan:
     key = (mask.data_ptr(), tuple(mask.shape), str(mask.device), mask._version)
-    p = _PLANS.get(key)
-    if p is None:
-        p = MaskPlan(mask)
-        _PLANS[key] = p
+    hit = _PLANS.get(key)
+    if hit is not None and hit[0]() is mask:
+        return hit[1]
+    p = MaskPlan(mask)
+    _PLANS[key] = (weakref.ref(mask), p)
+    if len(_PLANS) > 4096:   # drop entries whose tensor is gone
+        for k in [k for k, (r, _) in _PLANS.items() if r() is None]:
+            del _PLANS[k]
     return p
 
 

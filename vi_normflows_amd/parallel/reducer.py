@@ -67,6 +67,7 @@ class BucketedAllReduce:
         if cur:
             self._close(cur, unit_ranges)
         self.works = []
+        self._fenced = 0          # works [0, _fenced) already waited for by wait_inflight()
         self._side = None
         if compress_bf16:
             self._side = torch.empty(flat_grad.numel(), dtype=torch.bfloat16,
@@ -86,6 +87,7 @@ class BucketedAllReduce:
 
     def start_step(self) -> None:
         self.works = []
+        self._fenced = 0
         for b in self.buckets:
             b.pending = len(b.units)
 
@@ -117,6 +119,19 @@ class BucketedAllReduce:
         else:
             w = dist.all_reduce(view, group=self.group, async_op=True)
             self.works.append((w, None, None))
+
+    def wait_inflight(self) -> None:
+        """Make the compute stream wait for every all-reduce issued so far (stream-ordered, no
+        host sync on RCCL). The engines call it before each weight-gradient launch of whole
+        tiles (``WgradScheduler.fence``): the launch then never starts beside RCCL kernels
+        that hold CUs. The buckets issued right after a launch run during the input-gradient
+        chain that follows (~2.5 ms of non-persistent GEMMs, which degrade gracefully around
+        held CUs), so the wait is normally already satisfied."""
+        if not self.active:
+            return
+        for w, _, _ in self.works[self._fenced:]:
+            w.wait()
+        self._fenced = len(self.works)
 
     def finish(self) -> None:
         if not self.active:

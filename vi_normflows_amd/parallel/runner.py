@@ -110,6 +110,10 @@ class DataParallelRunner:
                                              bucket_cap_mb=bucket_cap_mb,
                                              compress_bf16=compress_bf16, force=force)
             engine.unit_ready_hook = self.reducer.mark_ready
+            # weight-gradient launches of exactly one tile per CU wait for the buckets in flight
+            # (VINF_DP_WGRAD_FENCE=0 lets them start beside the all-reduce)
+            if hasattr(engine, "wgrad_fence_hook") and os.environ.get("VINF_DP_WGRAD_FENCE", "1") != "0":
+                engine.wgrad_fence_hook = self.reducer.wait_inflight
 
     def _eager_step(self):
         kind = faults.armed(self._t, self.info.rank)
