@@ -30,6 +30,9 @@ enum Epi : int {
                          // flow layer (staged path only; see GemmArgs::cpl_*)
   EPI_CPL_FWD = 5,       // [s_hat | t] = acc + bias, then the affine-coupling forward of the same
                          // layer (gemm256 only; see GemmArgs::cf_*)
+  EPI_CPL_BWD_XB = 6,    // EPI_CPL_BWD reading x = h_{l-1} as bf16 (the conditioner operand copy
+                         // the forward wrote) instead of the fp32 state: 2 B less per element of
+                         // an HBM-bound epilogue; x only enters dS_hat, which is stored in bf16
 };
 
 struct GemmArgs {
@@ -66,7 +69,7 @@ struct GemmArgs {
   //   s = cpl_scale * tanh(s_hat)      (s_hat = aux, bf16, [M][ld_aux])
   //   dS_hat = (gy x e^s + cpl_c) (cpl_scale - s^2 / cpl_scale),  dT = gy,  gx = gy e^s
   // writing dst = [dS_hat | dT | 0-pad to cpl_pad] (bf16) and gx (fp32) for n < cpl_dh.
-  const float* cpl_x; long ld_cpl_x;   // x = h_{l-1} (fp32)
+  const float* cpl_x; long ld_cpl_x;   // x = h_{l-1} (fp32; bf16 under EPI_CPL_BWD_XB)
   float* cpl_gx; long ld_cpl_gx;       // dL/dh_{l-1} (fp32, written)
   bf16_t* cpl_dst; long ld_cpl_dst;    // conditioner output gradient of layer l-1
   int cpl_dh, cpl_pad;
@@ -134,9 +137,10 @@ inline bool staged_ok(const GemmArgs& a, int epi) {
     if (epi == EPI_BF16_RELUMASK && !a.aux_bits && (a.ld_aux % 8 || !al(a.aux))) return false;
     return true;
   }
-  if (epi == EPI_CPL_BWD) {
+  if (epi == EPI_CPL_BWD || epi == EPI_CPL_BWD_XB) {
+    const bool xok = epi == EPI_CPL_BWD ? al(a.cpl_x) : ((unsigned long)a.cpl_x & 7) == 0;
     if (a.cpl_dh % 4 || a.ld_cpl_x % 4 || a.ld_cpl_gx % 4 || a.ld_cpl_dst % 4 || a.ld_aux % 4 ||
-        !al(a.cpl_x) || !al(a.cpl_gx) || ((unsigned long)a.cpl_dst & 7) || ((unsigned long)a.aux & 7))
+        !xok || !al(a.cpl_gx) || ((unsigned long)a.cpl_dst & 7) || ((unsigned long)a.aux & 7))
       return false;
   }
   return a.N % 4 == 0 && a.ldc % 4 == 0 && a.c_split_stride % 4 == 0 && al(a.C);
@@ -486,6 +490,8 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
     // coupling-backward epilogue took 52.6 us per tile, profiles/r2_g256_stamps_b65536.jsonl.)
     // 16-row accumulator blocks per pass (e4m3 fused backward: 1 - its loop leaves fewer
     // registers for the pass's preloaded operands, 264 B/lane of scratch at 2)
+    constexpr bool CPLB = EPI == EPI_CPL_BWD || EPI == EPI_CPL_BWD_XB;
+    constexpr bool XB = EPI == EPI_CPL_BWD_XB;   // x operand in bf16
     constexpr int PJ = (F8 && EPI == EPI_CPL_BWD) ? 1 : 2;
     constexpr int PIT = PJ * 4;       // readback iterations (4 rows each) per pass
     // e4m3 operands (EPI_CPL_BWD): acc * f8_sa[0] * f8_sb[n], and with f8_cq the e4m3 copy of
@@ -515,18 +521,22 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
       const int q = lane & 15;
       float4 cv[PIT];
       float4 xp[PIT];
-      ushort4 sp[PIT];
-      if constexpr (EPI == EPI_F32_ACC || EPI == EPI_CPL_BWD) {
+      ushort4 sp[PIT], xh[PIT];
+      if constexpr (EPI == EPI_F32_ACC || CPLB) {
 #pragma unroll
         for (int it = 0; it < PIT; ++it) {
           int m = m0 + hj * 16 * PJ + it * 4 + (lane >> 4), n = n0 + q * 4 + (SPLITN && q >= 8 ? 96 : 0);
           m = m < a.M ? m : a.M - 1;
           n = n < a.N ? n : a.N - 4;
           cv[it] = *reinterpret_cast<const float4*>((const float*)a.C + (long)m * a.ldc + n);
-          if constexpr (EPI == EPI_CPL_BWD) {
+          if constexpr (CPLB) {
             const int nx = n < a.cpl_dh ? n : a.cpl_dh - 4;
             sp[it] = *reinterpret_cast<const ushort4*>(a.aux + (long)m * a.ld_aux + nx);
-            xp[it] = *reinterpret_cast<const float4*>(a.cpl_x + (long)m * a.ld_cpl_x + nx);
+            if constexpr (XB)
+              xh[it] = *reinterpret_cast<const ushort4*>(
+                  reinterpret_cast<const bf16_t*>(a.cpl_x) + (long)m * a.ld_cpl_x + nx);
+            else
+              xp[it] = *reinterpret_cast<const float4*>(a.cpl_x + (long)m * a.ld_cpl_x + nx);
           }
         }
       }
@@ -551,15 +561,21 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
         }
         const int m = m0 + hj * 16 * PJ + row, n = n0 + q * 4 + (SPLITN && q >= 8 ? 96 : 0);
         if (m < a.M && n < a.N) {
-          if constexpr (EPI == EPI_CPL_BWD) {
+          if constexpr (CPLB) {
             const float4 o = cv[it];
             const float gy[4] = {o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]};
             bf16_t* drow = a.cpl_dst + (long)m * a.ld_cpl_dst;
             if (n < a.cpl_dh) {
               const ushort4 sh = sp[it];
-              const float4 xv = xp[it];
               const float shv[4] = {bf2f(sh.x), bf2f(sh.y), bf2f(sh.z), bf2f(sh.w)};
-              const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+              float xs[4];
+              if constexpr (XB) {
+                const ushort4 xv = xh[it];
+                xs[0] = bf2f(xv.x); xs[1] = bf2f(xv.y); xs[2] = bf2f(xv.z); xs[3] = bf2f(xv.w);
+              } else {
+                const float4 xv = xp[it];
+                xs[0] = xv.x; xs[1] = xv.y; xs[2] = xv.z; xs[3] = xv.w;
+              }
               const float inv = 1.0f / a.cpl_scale;
               float gx[4], dsh[4], d1v[4];
               if (a.cpl_mode) {   // MAF: dst = [dmu | ds_raw], x = u of layer l-1

@@ -1485,7 +1485,7 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
                               const float* x, long ld_x, void* dst, long ld_dst, int dst_pad,
                               float* gx, long ld_gx, int Dh, float scale, float c,
                               hipStream_t stream, int w_kmajor, const int* krange,
-                              int krange_segs, int mode, const NfF8Operands* f8) {
+                              int krange_segs, int mode, const NfF8Operands* f8, int x_bf16) {
   if (M <= 0 || N <= 0) return;
   GemmArgs a{};
   if (f8) {   // e4m3 dy (per-tensor scale) and Wt (per-row scales); optional e4m3 copy of dst
@@ -1508,7 +1508,13 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
   a.cpl_dst = (nf::bf16_t*)dst; a.ld_cpl_dst = ld_dst;
   a.cpl_dh = Dh; a.cpl_pad = dst_pad;
   a.cpl_scale = scale; a.cpl_c = c;
-  if (Dh > N || dst_pad < 2 * Dh || dst_pad > Dh + N || !staged_ok(a, EPI_CPL_BWD) ||
+  // x_bf16: x is the bf16 copy of h_{l-1} (EPI_CPL_BWD_XB; bf16 coupling form only)
+  const int epi = x_bf16 ? EPI_CPL_BWD_XB : EPI_CPL_BWD;
+  if (x_bf16 && (f8 || mode || !w_kmajor)) {
+    fprintf(stderr, "vinf: bf16 x in the fused backward needs the bf16 coupling form with Wt\n");
+    abort();
+  }
+  if (Dh > N || dst_pad < 2 * Dh || dst_pad > Dh + N || !staged_ok(a, epi) ||
       !staged_enabled()) {
     fprintf(stderr, "vinf: fused coupling-backward GEMM needs Dh <= N, 2 Dh <= pad <= Dh + N, "
                     "4-element aligned rows and the staged epilogue\n");
@@ -1521,6 +1527,10 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
     }
     a.k_per_split = K;
     g256::launch_f8<EPI_CPL_BWD>(a, stream);
+    return;
+  }
+  if (x_bf16) {
+    g256::launch<true, true, EPI_CPL_BWD_XB>(a, 1, stream);
     return;
   }
   if (w_kmajor && mode == 0 && (nf_gemm_pp_enabled() & 2)) {

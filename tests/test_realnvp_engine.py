@@ -123,6 +123,9 @@ def test_deferred_wgrad_matches_per_layer_and_captures(gpu, monkeypatch):
     from vi_normflows_amd.parallel.runner import DataParallelRunner
 
     cfg = RealNVPConfig(dim=784, n_layers=5, hidden=512, anneal="none", init_out_std=0.1)
+    # the per-layer schedule has no fused coupling backward, so it reads x in fp32: pin the
+    # deferred engine's fused epilogue to fp32 x too (bf16 x: its own test)
+    monkeypatch.setenv("VINF_CPL_XBF16", "0")
     a = RealNVPVI(cfg, batch=1024, device=gpu, seed=3)
     monkeypatch.setenv("VINF_WGRAD_DEFER", "0")
     b = RealNVPVI(cfg, batch=1024, device=gpu, seed=3)
@@ -153,8 +156,10 @@ def test_deferred_wgrad_matches_per_layer_and_captures(gpu, monkeypatch):
 @pytest.mark.gpu
 def test_fused_coupling_backward_epilogue_matches_unfused(gpu, monkeypatch):
     """Coupling layer l-1's backward inside layer l's input-gradient GEMM epilogue
-    (EPI_CPL_BWD) gives bitwise the gradients of the separate coupling kernel."""
+    (EPI_CPL_BWD) gives bitwise the gradients of the separate coupling kernel (both reading
+    x = h_{l-1} in fp32; the bf16-x form is covered by the next test)."""
     cfg = RealNVPConfig(dim=784, n_layers=4, hidden=512, anneal="none", init_out_std=0.1)
+    monkeypatch.setenv("VINF_CPL_XBF16", "0")
     a = RealNVPVI(cfg, batch=768, device=gpu, seed=5)
     monkeypatch.setenv("VINF_CPL_FUSE", "0")
     b = RealNVPVI(cfg, batch=768, device=gpu, seed=5)
@@ -167,6 +172,33 @@ def test_fused_coupling_backward_epilogue_matches_unfused(gpu, monkeypatch):
     assert torch.isfinite(a.params.grad).all()
     assert torch.equal(a.params.grad, b.params.grad)
     assert torch.equal(a.dstL, b.dstL)
+
+
+@pytest.mark.gpu
+def test_fused_coupling_backward_bf16_x_close_to_fp32_x(gpu, monkeypatch):
+    """EPI_CPL_BWD_XB (x = h_{l-1} read from the bf16 conditioner operand) vs the fp32-x
+    epilogue on a trained-scale engine: x only enters dS_hat, whose product is stored in bf16,
+    so the parameter gradient moves by bf16 rounding of x (<= 2^-9 relative per element)."""
+    cfg = RealNVPConfig(dim=784, n_layers=6, hidden=512, anneal="none", init_out_std=0.1)
+    a = RealNVPVI(cfg, batch=1024, device=gpu, seed=5)
+    monkeypatch.setenv("VINF_CPL_XBF16", "0")
+    b = RealNVPVI(cfg, batch=1024, device=gpu, seed=5)
+    assert a.cpl_xbf16 and not b.cpl_xbf16
+    assert a._cpl_x(2, True).dtype == torch.bfloat16
+    assert b._cpl_x(2, True).dtype == torch.float32
+    for e in (a, b):
+        e._update_schedule()
+        e.forward()
+        e.backward()
+    torch.cuda.synchronize()
+    ga, gb = a.params.grad, b.params.grad
+    assert torch.isfinite(ga).all()
+    assert torch.equal(a.loss, b.loss)            # forward untouched
+    rel = ((ga - gb).norm() / gb.norm()).item()
+    assert rel <= 1e-2, rel
+    # the weight-gradient cosine stays at bf16-noise level
+    cos = torch.nn.functional.cosine_similarity(ga, gb, dim=0).item()
+    assert cos >= 0.9999, cos
 
 
 @pytest.mark.gpu
@@ -190,6 +222,20 @@ def test_gemm_nn_cpl_matches_torch(gpu):
     torch.cuda.synchronize()
     assert (out[0][:, 2 * Dh:] == 0).all()
     for o, r in zip(out, ref):
+        err = (o.float() - r.float()).abs().max().item()
+        assert err <= 2e-2 * r.float().abs().max().item(), err
+    # bf16 x (EPI_CPL_BWD_XB, needs Wt) vs the fp32 oracle of the same rounded x
+    xb = x.to(torch.bfloat16)
+    Wt = W.t().contiguous()
+    outb = [torch.full_like(out[0], 5.0), torch.full_like(out[1], 5.0)]
+    refb = [o.clone() for o in outb]
+    gemm.linear_dgrad_coupling(dy, W, G, s_hat[:, :Dh], xb, outb[0], outb[1], 1.0, -1e-3, Wt=Wt)
+    with gemm.oracle():
+        gemm.linear_dgrad_coupling(dy, W, G, s_hat[:, :Dh], xb.float(), refb[0], refb[1], 1.0,
+                                   -1e-3)
+    torch.cuda.synchronize()
+    assert (outb[0][:, 2 * Dh:] == 0).all()
+    for o, r in zip(outb, refb):
         err = (o.float() - r.float()).abs().max().item()
         assert err <= 2e-2 * r.float().abs().max().item(), err
 
@@ -319,6 +365,8 @@ def test_dgrad_nt_transposed_weights_match_nn(gpu, monkeypatch):
     """Input gradients against a per-step W^T copy (NT instantiation, VINF_DGRAD_NT=1) give
     the NN path's gradients: same operands and K order, only the LDS fragment reads differ."""
     cfg = RealNVPConfig(dim=784, n_layers=4, hidden=512, anneal="none", init_out_std=0.1)
+    # bf16 x in the fused coupling backward needs W^T (NN has none): pin fp32 x on both
+    monkeypatch.setenv("VINF_CPL_XBF16", "0")
     a = RealNVPVI(cfg, batch=768, device=gpu, seed=5)
     monkeypatch.setenv("VINF_DGRAD_NT", "0")
     b = RealNVPVI(cfg, batch=768, device=gpu, seed=5)

@@ -9,9 +9,11 @@ the backward; ``parallel/runner.py``), and the hold is placed where the collecti
 * ``nominal``: at every bucket's ready point (after the weight-gradient launch that completes
   its units, exactly where ``BucketedAllReduce`` issues the all-reduce), for the bucket's
   expected all-reduce time at ``--busbw`` GB/s bus bandwidth over ``--world`` ranks;
-* ``worst``: the hold is resident when a weight-gradient launch (exactly one 256x256 tile per
-  CU, ~2.2 ms) starts: issued right before each launch, ``--worst-us`` long (a collective that
-  outlasts the input-gradient chain between two launches, e.g. a straggling peer);
+* ``long``: at every bucket's ready point, but ``--worst-us`` long: a collective that outlasts
+  the input-gradient chain between two weight-gradient launches (a straggling peer, a slow
+  link), so it is still resident when the next launch of exactly one tile per CU starts;
+* ``worst``: a hold issued right before each weight-gradient launch, ``--worst-us`` long
+  (resident when the launch starts regardless of the chain);
 
 each without and with the runner's fence (``WgradScheduler.fence``: the launch waits for the
 collectives in flight). Prints one JSON line per setting (ms/step and overhead vs none).
@@ -39,7 +41,7 @@ def main() -> None:
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--worst-us", type=float, nargs="+", default=[500.0, 1500.0])
-    ap.add_argument("--modes", default="none,nominal,nominal_fence,worst,worst_fence")
+    ap.add_argument("--modes", default="none,nominal,nominal_fence,long,long_fence,worst,worst_fence")
     a = ap.parse_args()
 
     from ..models.realnvp import RealNVPConfig, RealNVPVI
@@ -64,6 +66,8 @@ def main() -> None:
         st["bytes"] += 4.0 * (e - s)
         if st["bytes"] >= cap or u == 0:
             usec = st["bytes"] * f / (a.busbw * 1e3)
+            if st["mode"].startswith("long"):
+                usec = max(usec, st["worst_us"])
             ev = torch.cuda.Event()
             ev.record(main_s)
             side.wait_event(ev)
@@ -85,7 +89,7 @@ def main() -> None:
 
     def run(mode, k, worst_us=0.0):
         st.update(k=k, mode=mode, fence=mode.endswith("_fence"), worst_us=worst_us, bytes=0.0)
-        eng.unit_ready_hook = hook if mode.startswith("nominal") else None
+        eng.unit_ready_hook = hook if mode.startswith(("nominal", "long")) else None
         eng.wgrad_fence_hook = fence if mode != "none" else None
 
         def step():
@@ -110,7 +114,7 @@ def main() -> None:
         for mode in modes:
             if mode == "none":
                 continue
-            for wu in (a.worst_us if mode.startswith("worst") else [0.0]):
+            for wu in (a.worst_us if mode.startswith(("worst", "long")) else [0.0]):
                 ms = run(mode, k, wu)
                 rec = {"mode": mode, "hold_blocks": k, "ms_per_step": round(ms, 3),
                        "overhead_ms": round(ms - base, 3), "busbw_GBps": a.busbw}

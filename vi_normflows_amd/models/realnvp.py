@@ -199,6 +199,8 @@ class RealNVPVI:
         # fuse coupling layer l-1's backward into the epilogue of layer l's last input-gradient
         # GEMM (gemm_tile.h EPI_CPL_BWD): dL/dh_{l+1} is finished there and consumed at once
         self.cpl_fuse = self.wgrad_defer and os.environ.get("VINF_CPL_FUSE", "1") != "0"
+        # ... reading x = h_{l-1} from its bf16 operand copy (EPI_CPL_BWD_XB, see _cpl_x)
+        self.cpl_xbf16 = os.environ.get("VINF_CPL_XBF16", "1") != "0"
         self.dstL = self.dHL = None
         # fuse each layer's coupling forward into its last conditioner GEMM (gemm256
         # EPI_CPL_FWD): s_hat / t never make an HBM round trip and t is never stored; the
@@ -255,6 +257,15 @@ class RealNVPVI:
         if i == 1:
             return self.z0[:, :Dh]
         return self.Hs[i - 2]
+
+    def _cpl_x(self, i: int, has_wt: bool) -> torch.Tensor:
+        """x operand of the fused coupling backward (input half h_i of coupling layer i): the
+        bf16 conditioner-operand copy Hbf[i-1] the forward already wrote when it exists (i >= 1,
+        bf16 compute, W^T given; VINF_CPL_XBF16=0 keeps the fp32 state). The epilogue is at the
+        HBM roof (profiles/r4/roofline_step.txt) and x only enters dS_hat, stored in bf16."""
+        if i >= 1 and self.cpl_xbf16 and has_wt and self.cdt == torch.bfloat16:
+            return self.Hbf[i - 1][:, :self.cfg.half]
+        return self.h(i)
 
     def zK_halves(self):
         """(first-half, second-half) of z_K as fp32 views."""
@@ -485,8 +496,9 @@ class RealNVPVI:
                     # coupling backward in the same epilogue (writes dstL[l-1], G[l-1])
                     gemm.linear_dgrad_coupling(d, P.c(f"l{l}.W0"), self._G[l + 1],
                                                s_hat=self.ST[l - 1][:, :cfg.half],
-                                               x=self.h(l - 1), dst=self.dstL[l - 1],
-                                               gx=self.G[l - 1], scale=cfg.scale_bound, c=c,
+                                               x=self._cpl_x(l - 1, WT is not None),
+                                               dst=self.dstL[l - 1], gx=self.G[l - 1],
+                                               scale=cfg.scale_bound, c=c,
                                                Wt=None if WT is None else WT[l][0])
                 else:
                     gemm.linear_dgrad(d, P.c(f"l{l}.W0"), self._G[l + 1], accumulate=True)

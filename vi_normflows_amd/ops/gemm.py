@@ -156,6 +156,8 @@ def linear_dgrad_coupling(dy: torch.Tensor, W: torch.Tensor, G: torch.Tensor, s_
         s = scale * tanh(s_hat);  dst = [ (gy x e^s + c)(scale - s^2/scale) | gy | 0-pad ]
         gx = gy e^s
 
+    ``x`` may be the bf16 copy of h_{l-1} (with ``Wt``: ``EPI_CPL_BWD_XB``, 2 B less read per
+    element; x only enters dS_hat, which is stored in bf16).
     Elsewhere: the two steps through torch (same math as ``ops.fused.coupling_bwd``)."""
     if _mfma_ok(dy, W):
         from ._ext import native
