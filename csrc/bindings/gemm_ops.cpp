@@ -221,7 +221,7 @@ static void gemm_tn_multi_impl(at::TensorList dy, at::TensorList x, at::TensorLi
                                const at::Tensor* f8_scales, at::IntArrayRef sa_idx,
                                at::IntArrayRef sb_idx, int layout = 0) {
   const size_t n = dy.size();
-  TORCH_CHECK(layout >= 0 && layout <= 2 && (layout == 0 || !f8_scales), "layout 0..2, bf16");
+  TORCH_CHECK(layout >= 0 && layout <= 3 && (layout == 0 || !f8_scales), "layout 0..3, bf16");
   const bool f8 = f8_scales != nullptr;
   const auto odt = f8 ? at::kFloat8_e4m3fn : at::kBFloat16;
   if (f8) {

@@ -29,6 +29,7 @@
 // on each SIMD one wave issues its LDS reads / DMA while the other runs MFMAs.
 #include "gemm_tile.h"
 #include "wgrad_pack.h"
+#include "tn_multi.h"
 
 // Diagnostic build only (csrc/build.py --variant stamps -D NF_G256_STAMPS): every block records
 // s_memrealtime (100 MHz, chip-global) at body entry, after the prologue wait, after the main
@@ -156,8 +157,20 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long
       gm = gm < rows_total ? gm : rows_total - 8;
       src = base + (long)gk * ld + gm;
     }
+#ifdef NF_G256_ASM_DMA
+    // A/B build: the DMA in asm, invisible to the compiler's wait-count pass. With the builtin
+    // it drains the DMA queue (s_waitcnt vmcnt(0)) before every ds_read_b64_tr_b16 of the
+    // mn-major operands (12 such drains in the weight-gradient kernel, none before the k-major
+    // b128 reads): it cannot tell the slot being filled from the slot being read, so the
+    // counted vmcnt ring degenerates to one phase of prefetch. Ordering is then the schedule's
+    // own counted vmcnt + barriers only.
+    const unsigned lds = (unsigned)(unsigned long)(LDS_AS char*)(dst + piece * 1024);
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(src), "s"(lds) : "memory", "m0");
+#else
     __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(dst + piece * 1024), 16, 0,
                                      0);
+#endif
   }
 }
 
@@ -975,33 +988,7 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_group_kernel(GroupArgs g) {
   gemm256_body<false, false, EPI_F32, D, true>(a, local % tiles, local / tiles, smem);
 }
 
-// Weight gradients of MANY layers per launch, no split-K. A launch covers the global tile range
-// [tile0, tile0 + ntiles) of a problem list; every block owns one whole 256x256 output tile and
-// streams the full K (= batch) range, so there are no fp32 slabs and no reduce launch, and the
-// launch size is chosen by the caller (a multiple of the CU count: 40 tiles per RealNVP layer x
-// 32 layers = 1280 = 5 x 256). The descriptors travel in the kernarg segment (scalar loads).
-struct TnDesc {
-  const bf16_t* A;
-  const bf16_t* B;
-  float* C;
-  float* db;
-  const unsigned short* tiles;   // active tile ids of a masked problem (others never launched)
-  const unsigned char* cmask;    // [M][N] 0/1 applied to dW (MADE), or null
-  int lda, ldb, ldc, M, N, K, start, staged;
-  int sidx;                      // e4m3 launches: scale-pool indices of dy (low 16 bits) and x
-};
-constexpr int TN_MULTI_MAX = 40;   // 80-B descriptors: the table stays inside the 4 KiB kernarg
-constexpr int TN_PERM_MAX = 256;   // + 512 B: 3724 B of kernarg with 40 descriptors
-struct TnMulti {
-  TnDesc d[TN_MULTI_MAX];
-  int n, tile0, ntiles, use_perm;
-  // XCD packing (VINF_WGRAD_XCD_PACK): block position -> tile offset. Positions
-  // [x * ntiles/8, (x+1) * ntiles/8) run on XCD x (xcd_remap), so the permutation keeps each
-  // problem's tiles - which share A / B panels - inside one XCD's L2 where they fit
-  unsigned short perm[TN_PERM_MAX];
-  const float* scales;   // e4m3 launches: per-tensor dequantisation scales, indexed by sidx
-};
-static_assert(sizeof(TnMulti) <= 4096, "TnMulti must fit the 4 KiB kernarg segment");
+// Weight gradients of MANY layers per launch (TnDesc / TnMulti: tn_multi.h)
 
 // F8: every problem of the launch has e4m3 operands (mn-major, K % 128 == 0, ld in bytes):
 // read through ds_read_b64_tr_b8 (read_frag_f8mn), dW = acc * s_dy * s_x, db = s_dy * row sums
@@ -1673,6 +1660,15 @@ void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int
     }
     t.use_perm = nf::wgrad_xcd_perm(t.n, seg_lo, seg_n, ntiles, t.perm) ? 1 : 0;
   }
+  // 4-wave 128x128-per-wave TN kernel (gemm_tn4w.hip): layout 3, or the default bf16 launch
+  // under VINF_WGRAD_TN4W=1
+  static const int tn4w_env = [] {
+    const char* e = getenv("VINF_WGRAD_TN4W");
+    return e ? atoi(e) : 0;
+  }();
+  if (!f8 && (layout == 3 || (layout == 0 && tn4w_env)) && nf::gemm::launch_tn4w_multi(t, stream))
+    return;
+  if (layout == 3) layout = 0;
   if (layout != 0 && f8) {
     fprintf(stderr, "vinf: gemm256_tn_multi: transposed-operand layouts are bf16 only\n");
     abort();

@@ -81,6 +81,13 @@ case $name in
     timeout -k 10 300 python -u -m pytest tests/test_iaf_engine.py -m gpu -k graph -v --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1
     rc=$?; grep -E "PASS|FAIL|assert|differs|Error" $O/pytest.txt | head -20
     [ $rc -le 1 ] || exit $rc ;;
+  tn4w)           # 4-wave TN weight-gradient kernel: bitwise vs the 8-wave launch, then the probe
+                  # (real / cache-resident operands) and the real multi-layer launch layouts 0-3
+    timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py -m gpu -x -q -k "tn4w or tn_multi" --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
+    tail -1 $O/pytest.txt
+    VINF_BENCH_TAG=${1:-cur} timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 > $O/probe.jsonl &&
+    VINF_BENCH_TAG=${1:-cur} timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --layout-probe --layers 13 --iters 3 > $O/layout.jsonl &&
+    cat $O/probe.jsonl $O/layout.jsonl ;;
   cumask)         # CU-mask stream probe: mask bit -> XCD / SE / CU, and graph replay vs the mask
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/cumask_probe.hip -o $O/cumask_probe &&
     timeout -k 10 120 $O/cumask_probe > $O/cumask.jsonl && tail -3 $O/cumask.jsonl ;;

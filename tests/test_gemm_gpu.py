@@ -248,3 +248,33 @@ def test_gemm_tn_multi(gpu, B, ranges):
         _check(dW, rW, 1e-4)
         if db is not None:
             _check(db, rb, 1e-4)
+
+
+@pytest.mark.parametrize("B", [4096, 256, 96])
+def test_gemm_tn4w_matches_tn_multi(gpu, B):
+    """The 4-wave 128x128-per-wave weight-gradient kernel (gemm_tn4w.hip, layout 3) against
+    the 8-wave multi-layer launch (layout 0) on the headline's problem shapes plus odd edges:
+    same k order per output, so dW and db must be bitwise equal; both against fp32. B = 96 is
+    not a whole number of K-tile pairs: layout 3 must fall back to the 8-wave kernel."""
+    from vi_normflows_amd.ops._ext import native
+
+    torch.manual_seed(7)
+    shapes = [(800, 1024), (1024, 1024), (1024, 416), (264, 40), (520, 1024)]
+    dys = [_bf(B, M, device=gpu) for M, _ in shapes]
+    xs = [_bf(B, N, device=gpu) for _, N in shapes]
+    total = sum(((M + 255) // 256) * ((N + 255) // 256) for M, N in shapes)
+    outs = {}
+    for layout in (0, 3):
+        dWs = [torch.full((M, N), 3.0, device=gpu) for M, N in shapes]
+        dbs = [torch.full((M,), 3.0, device=gpu) if p % 2 == 0 else None
+               for p, (M, _) in enumerate(shapes)]
+        native().gemm_tn_multi_layout(dys, xs, dWs, dbs, 0, total, layout)
+        outs[layout] = (dWs, dbs)
+    torch.cuda.synchronize()
+    for p in range(len(shapes)):
+        ref = dys[p].float().t() @ xs[p].float()
+        _check(outs[3][0][p], ref, 1e-4)
+        assert torch.equal(outs[3][0][p], outs[0][0][p]), p
+        if outs[3][1][p] is not None:
+            _check(outs[3][1][p], dys[p].float().sum(0), 1e-4)
+            assert torch.equal(outs[3][1][p], outs[0][1][p]), p

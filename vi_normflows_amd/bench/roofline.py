@@ -49,6 +49,10 @@ FAMILIES = [
     (r"gemm256_kernel<true, true, 4, 4, false, true>", "MAF bwd e4m3 EPI4 (fused)", 65536),
     (r"gemm256_kernel<true, true, 2, 4, false, true>", "dgrad e4m3 EPI2", 65536),
     (r"gemm256_kernel<true, true, 0, 4, false, true>", "fwd e4m3 EPI0", 65536),
+    (r"gemm256_kernel<true, true, 5, 4, false, false>", "MAF fwd bf16 EPI5 (fused)", 16384),
+    (r"gemm256_kernel<true, true, 4, 4, false, false>", "MAF bwd bf16 EPI4 (fused)", 16384),
+    (r"gemm256_kernel<true, true, 2, 4, false, false>", "dgrad bf16 EPI2 (masked)", 16384),
+    (r"gemm256_kernel<true, true, 0, 4, false, false>", "fwd bf16 EPI0 (masked)", 16384),
     (r"gemm256_kernel<", "gemm256 one-tile-per-block", 16384),
     (r"flat_optimizer", "Adam (flat, fused)", 0),
     (r"transpose_bf16_batched", "W^T refresh", 0),
@@ -57,7 +61,9 @@ FAMILIES = [
     (r"reparam_grad", "base backward", 0),
     (r"sumsq", "grad guard (sumsq)", 0),
     (r"coupling_bwd", "coupling bwd (top layer)", 0),
-    (r"fp8_colsum", "e4m3 bias column sums", 0),
+    (r"colsum", "e4m3 bias column sums", 0),
+    (r"quant_(rows|tensor)_kernel", "e4m3 quantisation", 0),
+    (r"maf_bwd_kernel", "MAF bwd (top layer)", 0),
 ]
 
 LEVERS = {

@@ -58,8 +58,15 @@ def probe(B: int, iters: int, tag: str, dev):
     xt = x.t().contiguous()
     dyt = dy.t().contiguous()
     out = torch.empty(n, n, device=dev, dtype=bf)
+    from ..ops._ext import native
+
+    def tn4w(a_, b_):
+        return lambda: native().gemm_tn_multi_layout([a_], [b_], [dW], [db], 0, 256, 3)
+
     cases = {
         "tn_real": lambda: gemm.WgradPlan([(dy, x, dW, db)]).run(0, 256),
+        "tn4w_real": tn4w(dy, x),
+        "tn4w_cached": tn4w(dy0, x0),
         "tn_cached": lambda: gemm.WgradPlan([(dy0, x0, dW, db)]).run(0, 256),
         "tn_a_cached": lambda: gemm.WgradPlan([(dy0, x, dW, db)]).run(0, 256),
         "tn_b_cached": lambda: gemm.WgradPlan([(dy, x0, dW, db)]).run(0, 256),
@@ -90,8 +97,9 @@ def layout_probe(B: int, layers: int, iters: int, tag: str, dev):
     """The real deferred weight-gradient launch (per layer dW3 [800 x 1024], dW2 [1024 x 1024],
     dW1 [1024 x 416], chunks of one tile per CU) with three operand layouts: 0 = dy, x both
     batch-major (TN, what the engine runs), 1 = x as a transposed [N][batch] copy (k-major B),
-    2 = dy as a transposed [M][batch] copy (k-major A). Results must agree; one JSON line per
-    layout with the median launch time."""
+    2 = dy as a transposed [M][batch] copy (k-major A), 3 = layout 0 on the 4-wave
+    128x128-per-wave kernel (gemm_tn4w.hip). Results must agree; one JSON line per layout with
+    the median launch time."""
     from ..ops._ext import native
     from ..ops.gemm import wgrad_tiles
 
@@ -110,7 +118,7 @@ def layout_probe(B: int, layers: int, iters: int, tag: str, dev):
     total = starts[-1]
     nl = total // cus
     ops = {0: (dys, xs), 1: (dys, [x.t().contiguous() for x in xs]),
-           2: ([d.t().contiguous() for d in dys], xs)}
+           2: ([d.t().contiguous() for d in dys], xs), 3: (dys, xs)}
     ref = None
     flops = 2.0 * B * cus * 256 * 256
     import bisect
