@@ -87,7 +87,17 @@ case $name in
     tail -1 $O/pytest.txt
     VINF_BENCH_TAG=${1:-cur} timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 > $O/probe.jsonl &&
     VINF_BENCH_TAG=${1:-cur} timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --layout-probe --layers 13 --iters 3 > $O/layout.jsonl &&
-    cat $O/probe.jsonl $O/layout.jsonl ;;
+    cat $O/probe.jsonl $O/layout.jsonl
+    # the 8-wave kernel built with its LDS-DMA in asm (NF_G256_ASM_DMA): correctness, then the same
+    if [ -f vi_normflows_amd/_native/libvinf_hip_asmdma.so ]; then
+      export VINF_NATIVE_LIB=vi_normflows_amd/_native/libvinf_hip_asmdma.so
+      timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py tests/test_gemm_persistent_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_asmdma.txt 2>&1 || { tail -30 $O/pytest_asmdma.txt; exit 1; }
+      tail -1 $O/pytest_asmdma.txt
+      VINF_BENCH_TAG=asmdma timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 > $O/probe_asmdma.jsonl &&
+      VINF_BENCH_TAG=asmdma timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --layout-probe --layers 13 --iters 3 > $O/layout_asmdma.jsonl &&
+      cat $O/probe_asmdma.jsonl $O/layout_asmdma.jsonl
+      unset VINF_NATIVE_LIB
+    fi ;;
   cumask)         # CU-mask stream probe: mask bit -> XCD / SE / CU, and graph replay vs the mask
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/cumask_probe.hip -o $O/cumask_probe &&
     timeout -k 10 120 $O/cumask_probe > $O/cumask.jsonl && tail -3 $O/cumask.jsonl ;;

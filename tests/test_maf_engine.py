@@ -316,3 +316,32 @@ def test_fp8_vs_bf16_nll_trajectory_500_steps(gpu):
     assert abs(tail_f - tail_b) < 0.015 * total
     for r in (b, f):
         assert (r[0] - r[-50:].mean()).item() > 0.05 * (r[0].item() - floor)
+
+
+@pytest.mark.gpu
+def test_engine_fp8_saturation_counter_spike(gpu):
+    """The delayed e4m3 scales clip values that outgrow the previous step's amax; the engine
+    counts such state-steps. Steady data: no new events after the first steps. A 16x
+    data spike for one step: the forward activations' states (x at least) record events, the
+    step stays finite, and the counter is exposed in the training log record."""
+    cfg = MAFEngineConfig(dim=256, hidden=512, n_layers=4, precision="fp8", init_out_std=0.3)
+    eng = MAFEngine(cfg, batch=1024, device=gpu, seed=4)
+    x = torch.randn(1024, 256, generator=torch.Generator().manual_seed(9)).to(gpu)
+    eng.data_override = x
+    for _ in range(4):
+        eng.train_step()
+    torch.cuda.synchronize()
+    base = eng.fp8_saturation()
+    assert set(base) == {"fp8_sat_x", "fp8_sat_h", "fp8_sat_dO", "fp8_sat_dH"}
+    for _ in range(3):   # same data again: amax repeats, nothing new clips on the inputs
+        eng.train_step()
+    torch.cuda.synchronize()
+    assert eng.fp8_saturation()["fp8_sat_x"] == base["fp8_sat_x"]
+    eng.data_override = x * 16.0
+    eng.train_step()
+    eng.data_override = x
+    eng.train_step()      # the roll at this step's start records the spike
+    torch.cuda.synchronize()
+    after = eng.fp8_saturation()
+    assert after["fp8_sat_x"] > base["fp8_sat_x"], (base, after)
+    assert torch.isfinite(eng.loss).all()

@@ -204,6 +204,10 @@ class MAFEngine:
             # scales, against e4m3 (W*M)^T with per-row scales; VINF_FP8_DGRAD=0 keeps bf16
             self.fp8_bwd = self.fuse and os.environ.get("VINF_FP8_DGRAD", "1") != "0"
             self.amax_pool = torch.zeros(4 * L, 1 + AMAX_SLOTS, dtype=f32, device=dev)
+            # per delayed-scale state: steps whose amax exceeded the scale it was quantised with
+            # (amax_cur > amax_prev > 0: values beyond 448 * scale were clipped, the e4m3 weight
+            # gradients included). Device-side, so the hipGraph step needs no host sync
+            self.f8_saturated = torch.zeros(4 * L, dtype=torch.int32, device=dev)
             # the scales the producers quantise with this step, one pool (the e4m3 weight-
             # gradient launches index it): input of l, hidden of l, dO_l, dH_l
             self.f8_scale_pool = torch.ones(4 * L, dtype=f32, device=dev)
@@ -330,6 +334,16 @@ class MAFEngine:
                                         self.s2)
         self._wq_fresh = True
 
+    def fp8_saturation(self) -> dict:
+        """Clipping record of the delayed e4m3 scales: events = state-steps whose amax
+        outgrew the previous step's scale, by operand family (x / h forward activations, dO / dH
+        input gradients; all four feed the e4m3 weight gradients). Host sync: for logging."""
+        if not self.fp8:
+            return {}
+        L = self.cfg.n_layers
+        c = self.f8_saturated.view(4, L).sum(1).tolist()
+        return {"fp8_sat_x": c[0], "fp8_sat_h": c[1], "fp8_sat_dO": c[2], "fp8_sat_dH": c[3]}
+
     def forward(self):
         cfg, P = self.cfg, self.params
         D, H, L = cfg.dim, cfg.hidden, cfg.n_layers
@@ -341,8 +355,12 @@ class MAFEngine:
 
             if not self._wq_fresh:
                 self.quantize_weights()
-            # amax_prev <- max(amax_cur slots), slots <- 0 for every state at once
-            torch.amax(self.amax_pool[:, 1:], 1, out=self.amax_pool[:, 0])
+            # saturation of the step that just ran, then amax_prev <- max(amax_cur slots),
+            # slots <- 0 for every state at once
+            cur = torch.amax(self.amax_pool[:, 1:], 1)
+            prev = self.amax_pool[:, 0]
+            self.f8_saturated += ((cur > prev) & (prev > 0)).to(torch.int32)
+            self.amax_pool[:, 0].copy_(cur)
             self.amax_pool[:, 1:].zero_()
             _, sxs = self.sx[0].quantize(self.X[0], out=self._xq(0))
         if self.fuse:

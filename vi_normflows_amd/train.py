@@ -297,7 +297,8 @@ def run_maf(cfg, out, info, logger):
                 el = time.perf_counter() - t0
                 logger.log({"step": t, "nll": float(eng.loss.item()),
                             "grad_norm": math.sqrt(max(float(eng.gnorm2.item()), 0.0)),
-                            "samples_per_s": (t + 1) * cfg.batch * info.world / el})
+                            "samples_per_s": (t + 1) * cfg.batch * info.world / el,
+                            **eng.fp8_saturation()})
         save_engine(eng, out / "ckpt.pt", info.rank)
         vdist.barrier()
         return {"nll": float(eng.loss.item()), "nll_floor_entropy": mc.entropy(),

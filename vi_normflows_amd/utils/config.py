@@ -10,6 +10,12 @@ of BASELINE.json are shipped as presets:
     config4_iaf10_vae       IAF-10 amortized VI (VAE encoder) on 3x32x32 synthetic, DP
     config5_maf64           MAF-64 density estimation on 1024-d synthetic, DP
 plus ``mnist_planar_vae`` (the reference's main workload, src/learning_mnist.py).
+
+Divergence from the reference schedule (recorded, not hidden): ``config2_realnvp8`` and
+``config3_realnvp32_dp8`` train with beta = 1 and Adam lr 1e-3 after a 100-step warm-up - the
+model ``bench.py`` times - NOT the reference's annealed objective (``normflows/optimization.py:
+71-72``, lr 1e-4). ``config3_realnvp32_annealed`` is the reference-faithful variant (annealed
+beta_t, lr 1e-4; the warm-up is the one addition, without it the first Adam step diverged).
 """
 from __future__ import annotations
 
