@@ -24,6 +24,7 @@
 // stage s before it is restaged. K-tile t+1's DMA has the compute of one K-tile to land.
 #include "tn_multi.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace nf {
@@ -38,6 +39,7 @@ constexpr int STAGE = 4 * HALF;        // 64 KiB per K-tile
 // Address = uniform row base (SGPRs: k-row k0 + 4 piece) + a per-lane 32-bit byte offset that
 // takes two values (the chunk swizzle depends on bit 1 of the piece): saddr + voffset LDS-DMA,
 // 2 VGPRs instead of 16 64-bit addresses
+template <int NPIECE = 16>
 __device__ __forceinline__ void stage(const bf16_t* __restrict__ base, long ld, int col0,
                                       int cols_total, int k0, char* dst, int lane) {
   unsigned voff[2];
@@ -51,7 +53,7 @@ __device__ __forceinline__ void stage(const bf16_t* __restrict__ base, long ld, 
   }
   const char* b = (const char*)base + (long)k0 * ld * 2;
 #pragma unroll
-  for (int piece = 0; piece < 16; ++piece) {
+  for (int piece = 0; piece < NPIECE; ++piece) {
     const char* row = b + (long)(piece * 4) * ld * 2;
     const unsigned lds = (unsigned)(unsigned long)(LDS_AS char*)(dst + piece * 1024);
     // saddr + voffset form in asm: the builtin hoisted 16 64-bit per-lane addresses out of the
@@ -219,6 +221,171 @@ __device__ __forceinline__ void tile_body(const GemmArgs& a, int m0, int n0, cha
   }
 }
 
+// Deeper variant (VINF_TN4W_STAGES=4): 32-deep K-tiles in 4 stages of 32 KiB (separate
+// __shared__ objects, compile-time stage per access), K-tile t+3 issued while t is computed, so
+// up to 96 KiB per CU are in flight instead of 64; one barrier per 64 MFMAs.
+template <bool DODB>
+__device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, char* q0, char* q1,
+                                           char* q2, char* q3) {
+  constexpr int BK4 = 32, HALF4 = 128 * BK4 * 2;   // 8 KiB half-image
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nkt = a.K / BK4;   // a multiple of 4 (launch_tn4w_multi: K % 128 == 0)
+  const bf16_t* sbase = wave < 2 ? a.A : a.B;
+  const long sld = wave < 2 ? a.lda : a.ldb;
+  const int scol0 = wave < 2 ? m0 + wave * 128 : n0 + (wave - 2) * 128;
+  const int stot = wave < 2 ? a.M : a.N;
+  auto stp = [&](auto q_c) -> char* {
+    constexpr int Q = decltype(q_c)::value;
+    return Q == 0 ? q0 : Q == 1 ? q1 : Q == 2 ? q2 : q3;
+  };
+  auto issue = [&](int t, auto q_c) {
+    stage<8>(sbase, sld, scol0, stot, t * BK4, stp(q_c) + wave * HALF4, lane);
+  };
+  v4f acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+  float dbs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dbs[j] = 0.f;
+  v8s fa[8], fb0[8], fb1[8];
+  auto rd_a = [&](auto q_c, int j) { return read_frag<false>(stp(q_c) + wr * HALF4, j * 16, 0, lane); };
+  auto rd_b = [&](auto q_c, v8s (&fb)[8]) {
+    const char* st = stp(q_c) + (2 + wc) * HALF4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fb[i] = read_frag<false>(st, i * 16, 0, lane);
+  };
+  auto kstep = [&](const v8s (&fb)[8], auto qn_c, auto rd_c) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mfma_acc(acc[i][j], fb[i], fa[j]);
+      if constexpr (DODB) {
+        typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
+        const v2bf one = {(__bf16)1.0f, (__bf16)1.0f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const unsigned w = (unsigned)(unsigned short)fa[j][2 * e] |
+                             ((unsigned)(unsigned short)fa[j][2 * e + 1] << 16);
+          dbs[j] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf, w), one, dbs[j], false);
+        }
+      }
+      if constexpr (decltype(rd_c)::value) fa[j] = rd_a(qn_c, j);
+    }
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  issue(0, std::integral_constant<int, 0>{});
+  issue(1, std::integral_constant<int, 1>{});
+  issue(2, std::integral_constant<int, 2>{});
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fa[j] = rd_a(std::integral_constant<int, 0>{}, j);
+  rd_b(std::integral_constant<int, 0>{}, fb0);
+  // K-tile t in stage Q; W2: K-tile t+2 outstanding (wait vmcnt(8), else 0); NEXT: t+1 exists;
+  // ISSUE: t+3 exists
+  auto ktile = [&](int t, auto q_c, const v8s (&fbc)[8], v8s (&fbn)[8], auto w2_c, auto next_c,
+                   auto issue_c) {
+    constexpr int Q = decltype(q_c)::value;
+    using QN = std::integral_constant<int, (Q + 1) & 3>;
+    using QI = std::integral_constant<int, (Q + 3) & 3>;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (decltype(next_c)::value) {
+      if constexpr (decltype(w2_c)::value) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (decltype(issue_c)::value) issue(t + 3, QI{});
+    if constexpr (decltype(next_c)::value) rd_b(QN{}, fbn);
+    kstep(fbc, QN{}, next_c);
+  };
+  using Q0 = std::integral_constant<int, 0>;
+  using Q1 = std::integral_constant<int, 1>;
+  using Q2 = std::integral_constant<int, 2>;
+  using Q3 = std::integral_constant<int, 3>;
+  int t = 0;
+  for (; t + 4 < nkt; t += 4) {
+    ktile(t, Q0{}, fb0, fb1, T{}, T{}, T{});
+    ktile(t + 1, Q1{}, fb1, fb0, T{}, T{}, T{});
+    ktile(t + 2, Q2{}, fb0, fb1, T{}, T{}, T{});
+    ktile(t + 3, Q3{}, fb1, fb0, T{}, T{}, T{});
+  }
+  // last four K-tiles: t+3 = nkt-1 already issued
+  ktile(t, Q0{}, fb0, fb1, T{}, T{}, F{});
+  ktile(t + 1, Q1{}, fb1, fb0, F{}, T{}, F{});
+  ktile(t + 2, Q2{}, fb0, fb1, F{}, T{}, F{});
+  ktile(t + 3, Q3{}, fb1, fb0, F{}, F{}, F{});
+
+  const int g = lane >> 4, c = lane & 15;
+  if (DODB && wc == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = dbs[j];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      const int m = m0 + wr * 128 + j * 16 + c;
+      if (g == 0 && m < a.M) a.dbias[m] = v;
+    }
+  }
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+  __syncthreads();
+  char* region = (wave == 0 ? q0 : wave == 1 ? q1 : wave == 2 ? q2 : q3);   // 32 KiB per wave
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    v4f sub[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sub[i][j] = acc[4 * h + i][j];
+    if (a.staged)
+      epi_tile_staged<EPI_F32, 8>(a, sub, m0 + wr * 128, n0 + wc * 128 + h * 64, 0,
+                                  region + h * 16384, lane);
+    else
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = m0 + wr * 128 + j * 16 + c;
+        if (m >= a.M) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = n0 + wc * 128 + h * 64 + i * 16 + g * 4;
+          if (n < a.N) epi_store<EPI_F32>(a, sub[i][j], m, n, 0);
+        }
+      }
+  }
+}
+
+__global__ void __launch_bounds__(NTHR, 1) gemm_tn4w4_kernel(g256::TnMulti t) {
+  __shared__ __attribute__((aligned(16))) char q0[32768];
+  __shared__ __attribute__((aligned(16))) char q1[32768];
+  __shared__ __attribute__((aligned(16))) char q2[32768];
+  __shared__ __attribute__((aligned(16))) char q3[32768];
+  const int pos = xcd_remap(blockIdx.x, t.ntiles);
+  const int id = t.tile0 + (t.use_perm ? (int)t.perm[pos] : pos);
+  int p = 0;
+  for (int q = 1; q < t.n; ++q)
+    if (id >= t.d[q].start) p = q;
+  const g256::TnDesc& d = t.d[p];
+  GemmArgs a{};
+  a.A = d.A; a.lda = d.lda;
+  a.B = d.B; a.ldb = d.ldb;
+  a.C = d.C; a.ldc = d.ldc;
+  a.dbias = d.db;
+  a.M = d.M; a.N = d.N; a.K = d.K;
+  a.staged = d.staged;
+  a.cmask = d.cmask;
+  const int local = d.tiles ? (int)d.tiles[id - d.start] : id - d.start;
+  const int ntn = (a.N + BN - 1) / BN;
+  const int tm = local / ntn, tn = local % ntn;
+  if (a.dbias != nullptr && tn == 0) tile_body4<true>(a, tm * BM, tn * BN, q0, q1, q2, q3);
+  else tile_body4<false>(a, tm * BM, tn * BN, q0, q1, q2, q3);
+}
+
 __global__ void __launch_bounds__(NTHR, 1) gemm_tn4w_kernel(g256::TnMulti t) {
   __shared__ __attribute__((aligned(16))) char st0[STAGE];
   __shared__ __attribute__((aligned(16))) char st1[STAGE];
@@ -253,7 +420,14 @@ bool launch_tn4w_multi(const g256::TnMulti& t, hipStream_t stream) {
         ((unsigned long)d.A & 15) || ((unsigned long)d.B & 15))
       return false;
   }
-  hipLaunchKernelGGL(tn4w::gemm_tn4w_kernel, dim3(t.ntiles), dim3(tn4w::NTHR), 0, stream, t);
+  static const int stages = [] {
+    const char* e = getenv("VINF_TN4W_STAGES");
+    return e ? atoi(e) : 2;
+  }();
+  if (stages == 4)
+    hipLaunchKernelGGL(tn4w::gemm_tn4w4_kernel, dim3(t.ntiles), dim3(tn4w::NTHR), 0, stream, t);
+  else
+    hipLaunchKernelGGL(tn4w::gemm_tn4w_kernel, dim3(t.ntiles), dim3(tn4w::NTHR), 0, stream, t);
   NF_HIP_CHECK(hipGetLastError());
   return true;
 }
