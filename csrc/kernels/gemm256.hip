@@ -157,13 +157,15 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long
       gm = gm < rows_total ? gm : rows_total - 8;
       src = base + (long)gk * ld + gm;
     }
-#ifdef NF_G256_ASM_DMA
-    // A/B build: the DMA in asm, invisible to the compiler's wait-count pass. With the builtin
-    // it drains the DMA queue (s_waitcnt vmcnt(0)) before every ds_read_b64_tr_b16 of the
+#ifndef NF_G256_BUILTIN_DMA
+    // The DMA in asm, invisible to the compiler's wait-count pass. With the builtin it drains
+    // the DMA queue (s_waitcnt vmcnt(0)) before every ds_read_b64_tr_b16 / _tr_b8 of the
     // mn-major operands (12 such drains in the weight-gradient kernel, none before the k-major
     // b128 reads): it cannot tell the slot being filled from the slot being read, so the
-    // counted vmcnt ring degenerates to one phase of prefetch. Ordering is then the schedule's
-    // own counted vmcnt + barriers only.
+    // counted vmcnt ring degenerates to one phase of prefetch. Ordering is the schedule's own
+    // counted vmcnt + barriers only (RAW / WAR distances in the header comment). Measured
+    // (profiles/r4/asmdma_probe.jsonl): NN product 1782 -> 1612 us, TN 2238 -> 2158 us, NT
+    // unchanged; -D NF_G256_BUILTIN_DMA restores the builtin for A/B.
     const unsigned lds = (unsigned)(unsigned long)(LDS_AS char*)(dst + piece * 1024);
     asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
                  :: "v"(src), "s"(lds) : "memory", "m0");
@@ -1660,11 +1662,12 @@ void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int
     }
     t.use_perm = nf::wgrad_xcd_perm(t.n, seg_lo, seg_n, ntiles, t.perm) ? 1 : 0;
   }
-  // 4-wave 128x128-per-wave TN kernel (gemm_tn4w.hip): layout 3, or the default bf16 launch
-  // under VINF_WGRAD_TN4W=1
+  // 4-wave 128x128-per-wave TN kernel (gemm_tn4w.hip): the default bf16 launch (the real
+  // multi-layer launch 2583 -> 1960 us median, profiles/r4/tn4w4_layout_probe.jsonl);
+  // VINF_WGRAD_TN4W=0 keeps the 8-wave kernel, layout 3 forces the 4-wave one
   static const int tn4w_env = [] {
     const char* e = getenv("VINF_WGRAD_TN4W");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
   }();
   if (!f8 && (layout == 3 || (layout == 0 && tn4w_env)) && nf::gemm::launch_tn4w_multi(t, stream))
     return;

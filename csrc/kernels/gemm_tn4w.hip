@@ -316,9 +316,9 @@ __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, ch
     ktile(t + 2, Q2{}, fb0, fb1, T{}, T{}, T{});
     ktile(t + 3, Q3{}, fb1, fb0, T{}, T{}, T{});
   }
-  // last four K-tiles: t+3 = nkt-1 already issued
-  ktile(t, Q0{}, fb0, fb1, T{}, T{}, F{});
-  ktile(t + 1, Q1{}, fb1, fb0, F{}, T{}, F{});
+  // last four K-tiles: the first still issues K-tile nkt-1
+  ktile(t, Q0{}, fb0, fb1, T{}, T{}, T{});
+  ktile(t + 1, Q1{}, fb1, fb0, T{}, T{}, F{});
   ktile(t + 2, Q2{}, fb0, fb1, F{}, T{}, F{});
   ktile(t + 3, Q3{}, fb1, fb0, F{}, F{}, F{});
 
@@ -422,7 +422,7 @@ bool launch_tn4w_multi(const g256::TnMulti& t, hipStream_t stream) {
   }
   static const int stages = [] {
     const char* e = getenv("VINF_TN4W_STAGES");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 4;   // 4: profiles/r4/tn4w4_layout_probe.jsonl (2: tn4w_layout_probe)
   }();
   if (stages == 4)
     hipLaunchKernelGGL(tn4w::gemm_tn4w4_kernel, dim3(t.ntiles), dim3(tn4w::NTHR), 0, stream, t);

@@ -93,7 +93,7 @@ case $name in
     VINF_TN4W_STAGES=4 VINF_BENCH_TAG=stages4 timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 > $O/probe_s4.jsonl &&
     VINF_TN4W_STAGES=4 VINF_BENCH_TAG=stages4 timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --layout-probe --layers 13 --iters 3 > $O/layout_s4.jsonl &&
     cat $O/probe_s4.jsonl $O/layout_s4.jsonl
-    # the 8-wave kernel built with its LDS-DMA in asm (NF_G256_ASM_DMA): correctness, then the same
+    # a variant build (e.g. --variant builtindma -D NF_G256_BUILTIN_DMA): correctness, then the same
     if [ -f vi_normflows_amd/_native/libvinf_hip_asmdma.so ]; then
       export VINF_NATIVE_LIB=vi_normflows_amd/_native/libvinf_hip_asmdma.so
       timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py tests/test_gemm_persistent_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_asmdma.txt 2>&1 || { tail -30 $O/pytest_asmdma.txt; exit 1; }
