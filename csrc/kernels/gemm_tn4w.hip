@@ -224,7 +224,7 @@ __device__ __forceinline__ void tile_body(const GemmArgs& a, int m0, int n0, cha
 // Deeper variant (VINF_TN4W_STAGES=4): 32-deep K-tiles in 4 stages of 32 KiB (separate
 // __shared__ objects, compile-time stage per access), K-tile t+3 issued while t is computed, so
 // up to 96 KiB per CU are in flight instead of 64; one barrier per 64 MFMAs.
-template <bool DODB>
+template <bool DODB, int PD>
 __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, char* q0, char* q1,
                                            char* q2, char* q3) {
   constexpr int BK4 = 32, HALF4 = 128 * BK4 * 2;   // 8 KiB half-image
@@ -278,10 +278,16 @@ __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, ch
   };
   using T = std::true_type;
   using F = std::false_type;
+  // PD: prefetch distance in K-tiles (K-tile t + PD issued while t is computed): 3 keeps up to
+  // 96 KiB per CU in flight, 2 keeps 64 KiB (less of the XCD's 4 MiB L2 held by data in flight)
   issue(0, std::integral_constant<int, 0>{});
   issue(1, std::integral_constant<int, 1>{});
-  issue(2, std::integral_constant<int, 2>{});
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  if constexpr (PD == 3) {
+    issue(2, std::integral_constant<int, 2>{});
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int j = 0; j < 8; ++j) fa[j] = rd_a(std::integral_constant<int, 0>{}, j);
@@ -292,16 +298,16 @@ __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, ch
                    auto issue_c) {
     constexpr int Q = decltype(q_c)::value;
     using QN = std::integral_constant<int, (Q + 1) & 3>;
-    using QI = std::integral_constant<int, (Q + 3) & 3>;
+    using QI = std::integral_constant<int, (Q + PD) & 3>;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if constexpr (decltype(next_c)::value) {
-      if constexpr (decltype(w2_c)::value) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      if constexpr (PD == 3 && decltype(w2_c)::value) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (decltype(issue_c)::value) issue(t + 3, QI{});
+    if constexpr (decltype(issue_c)::value) issue(t + PD, QI{});
     if constexpr (decltype(next_c)::value) rd_b(QN{}, fbn);
     kstep(fbc, QN{}, next_c);
   };
@@ -317,8 +323,13 @@ __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, ch
     ktile(t + 3, Q3{}, fb1, fb0, T{}, T{}, T{});
   }
   // last four K-tiles: the first still issues K-tile nkt-1
-  ktile(t, Q0{}, fb0, fb1, T{}, T{}, T{});
-  ktile(t + 1, Q1{}, fb1, fb0, T{}, T{}, F{});
+  if constexpr (PD == 3) {
+    ktile(t, Q0{}, fb0, fb1, T{}, T{}, T{});
+    ktile(t + 1, Q1{}, fb1, fb0, T{}, T{}, F{});
+  } else {   // K-tiles nkt-2, nkt-1 still to issue
+    ktile(t, Q0{}, fb0, fb1, F{}, T{}, T{});
+    ktile(t + 1, Q1{}, fb1, fb0, F{}, T{}, T{});
+  }
   ktile(t + 2, Q2{}, fb0, fb1, F{}, T{}, F{});
   ktile(t + 3, Q3{}, fb1, fb0, F{}, F{}, F{});
 
@@ -360,6 +371,7 @@ __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, ch
   }
 }
 
+template <int PD>
 __global__ void __launch_bounds__(NTHR, 1) gemm_tn4w4_kernel(g256::TnMulti t) {
   __shared__ __attribute__((aligned(16))) char q0[32768];
   __shared__ __attribute__((aligned(16))) char q1[32768];
@@ -382,8 +394,8 @@ __global__ void __launch_bounds__(NTHR, 1) gemm_tn4w4_kernel(g256::TnMulti t) {
   const int local = d.tiles ? (int)d.tiles[id - d.start] : id - d.start;
   const int ntn = (a.N + BN - 1) / BN;
   const int tm = local / ntn, tn = local % ntn;
-  if (a.dbias != nullptr && tn == 0) tile_body4<true>(a, tm * BM, tn * BN, q0, q1, q2, q3);
-  else tile_body4<false>(a, tm * BM, tn * BN, q0, q1, q2, q3);
+  if (a.dbias != nullptr && tn == 0) tile_body4<true, PD>(a, tm * BM, tn * BN, q0, q1, q2, q3);
+  else tile_body4<false, PD>(a, tm * BM, tn * BN, q0, q1, q2, q3);
 }
 
 __global__ void __launch_bounds__(NTHR, 1) gemm_tn4w_kernel(g256::TnMulti t) {
@@ -424,8 +436,14 @@ bool launch_tn4w_multi(const g256::TnMulti& t, hipStream_t stream) {
     const char* e = getenv("VINF_TN4W_STAGES");
     return e ? atoi(e) : 4;   // 4: profiles/r4/tn4w4_layout_probe.jsonl (2: tn4w_layout_probe)
   }();
-  if (stages == 4)
-    hipLaunchKernelGGL(tn4w::gemm_tn4w4_kernel, dim3(t.ntiles), dim3(tn4w::NTHR), 0, stream, t);
+  static const int pd = [] {
+    const char* e = getenv("VINF_TN4W_PD");
+    return e && atoi(e) == 2 ? 2 : 3;
+  }();
+  if (stages == 4 && pd == 2)
+    hipLaunchKernelGGL(tn4w::gemm_tn4w4_kernel<2>, dim3(t.ntiles), dim3(tn4w::NTHR), 0, stream, t);
+  else if (stages == 4)
+    hipLaunchKernelGGL(tn4w::gemm_tn4w4_kernel<3>, dim3(t.ntiles), dim3(tn4w::NTHR), 0, stream, t);
   else
     hipLaunchKernelGGL(tn4w::gemm_tn4w_kernel, dim3(t.ntiles), dim3(tn4w::NTHR), 0, stream, t);
   NF_HIP_CHECK(hipGetLastError());

@@ -103,6 +103,15 @@ case $name in
       cat $O/probe_asmdma.jsonl $O/layout_asmdma.jsonl
       unset VINF_NATIVE_LIB
     fi ;;
+  tn4w_pd)        # 4-stage TN kernel, prefetch distance 2 vs 3: layout probe + whole step
+    for r in 1 2; do
+      for pd in 3 2; do
+        VINF_TN4W_PD=$pd VINF_BENCH_TAG=pd$pd timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --layout-probe --layers 13 --iters 3 >> $O/layout.jsonl || exit 1
+        VINF_TN4W_PD=$pd timeout -k 10 240 python bench.py --steps 20 --warmup 5 > $O/b.json 2> $O/b.err || { tail -20 $O/b.err; exit 1; }
+        python -c "import json;d=json.load(open('$O/b.json'));print(json.dumps({'pd':$pd,'ms':d['ms_per_step'],'F':d['notes']['final_free_energy']}))" >> $O/ab.jsonl
+      done
+    done
+    grep '"layout": [03]' $O/layout.jsonl; cat $O/ab.jsonl ;;
   cumask)         # CU-mask stream probe: mask bit -> XCD / SE / CU, and graph replay vs the mask
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/cumask_probe.hip -o $O/cumask_probe &&
     timeout -k 10 120 $O/cumask_probe > $O/cumask.jsonl && tail -3 $O/cumask.jsonl ;;

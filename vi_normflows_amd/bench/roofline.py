@@ -38,12 +38,14 @@ N_XCD, N_SIMD = 8, 1024
 
 # kernel-name pattern -> (family label, FLOPs per MFMA instruction)
 FAMILIES = [
+    (r"gemm_tn4w4?_kernel", "wgrad TN bf16 4-wave (multi-layer, K = batch)", 16384),
     (r"gemm256_multi_kernel<4, true", "wgrad TN e4m3 (multi-layer)", 65536),
     (r"gemm256_multi_kernel<", "wgrad TN bf16 (multi-layer, K = batch)", 16384),
     (r"gemm256_persistent_kernel<true, true, 0>", "fwd NT EPI0 (bias+ReLU+bitmask)", 16384),
     (r"gemm256_persistent_kernel<true, true, 2>", "dgrad NT EPI2 (ReLU bitmask)", 16384),
     (r"gemm256_persistent_kernel<true, true, 5>", "coupling fwd NT EPI5 (fused)", 16384),
     (r"gemm256_persistent_kernel<true, true, 4>", "coupling bwd NT EPI4 (fused)", 16384),
+    (r"gemm256_persistent_kernel<true, true, 6>", "coupling bwd NT EPI6 (fused, bf16 x)", 16384),
     (r"gemm256_persistent_kernel<true, false, 3>", "layer-0 dgrad NN EPI3 (fp32 acc)", 16384),
     (r"gemm256_kernel<true, true, 5, 4, false, true>", "MAF fwd e4m3 EPI5 (fused)", 65536),
     (r"gemm256_kernel<true, true, 4, 4, false, true>", "MAF bwd e4m3 EPI4 (fused)", 65536),
@@ -71,6 +73,9 @@ LEVERS = {
         "mn-major operand stream (L2 hit capped at ~0.75 by the 4x4 panel sharing of a "
         "1024-wide problem, transposed LDS reads); next: 12.5 % padded tiles (dW3 rows "
         "768-799, dW1 cols 392-511), more MFMA per transposed byte",
+    "wgrad TN bf16 4-wave (multi-layer, K = batch)":
+        "operand delivery per CU (64 KiB per 32-deep K-tile pair at ~30 GB/s/CU, L2 hit ~0.75 "
+        "from the 4x4 panel sharing); next: the 12.5 % padded tiles, a fifth LDS stage",
     "fwd NT EPI0 (bias+ReLU+bitmask)":
         "per-CU LDS-DMA operand rate at K <= 1024 and the all-CU epilogue store burst; "
         "next: overlap the C write with the next tile's main loop",
@@ -82,6 +87,8 @@ LEVERS = {
     "coupling bwd NT EPI4 (fused)":
         "epilogue bytes (gy, s_hat, x in; gx, dst out) and a 136/256-column second tile; "
         "next: bf16 x from the saved conditioner input, skip the pad-column MFMAs",
+    "coupling bwd NT EPI6 (fused, bf16 x)":
+        "epilogue bytes (gy, s_hat, bf16 x in; gx, dst out); next: the G chain in bf16",
     "Adam (flat, fused)": "streams 2.2 GB (p, g, m, v, bf16 copy): at the HBM roof when >= 70 %",
 }
 
