@@ -111,7 +111,21 @@ case $name in
         python -c "import json;d=json.load(open('$O/b.json'));print(json.dumps({'pd':$pd,'ms':d['ms_per_step'],'F':d['notes']['final_free_energy']}))" >> $O/ab.jsonl
       done
     done
-    grep '"layout": [03]' $O/layout.jsonl; cat $O/ab.jsonl ;;
+    grep '"layout": [03]' $O/layout.jsonl; cat $O/ab.jsonl
+    # L2 hit / fabric reads of the real launch at both distances (one counter pass each)
+    export TMPDIR=/tmp
+    for pd in 3 2; do
+      VINF_TN4W_PD=$pd timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum \
+        -d $O/pmc_pd$pd -o wg --output-format csv -- python3 -m vi_normflows_amd.bench.wgrad_bench --layers 13 --iters 1 > $O/pmc_pd$pd.log 2>&1 || { tail -20 $O/pmc_pd$pd.log; exit 1; }
+    done ;;
+  wg_pitch)       # weight-gradient launch vs operand row pitch (power of two or padded), both
+                  # kernels, plus the L2 counters of the 4-wave one at each pitch
+    for r in 1 2; do
+      for pad in 0 64 32; do
+        VINF_BENCH_TAG=pad$pad timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --layout-probe --layers 13 --iters 3 --layouts 0,3 --pitch-pad $pad >> $O/layout.jsonl || exit 1
+      done
+    done
+    cat $O/layout.jsonl ;;
   cumask)         # CU-mask stream probe: mask bit -> XCD / SE / CU, and graph replay vs the mask
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/cumask_probe.hip -o $O/cumask_probe &&
     timeout -k 10 120 $O/cumask_probe > $O/cumask.jsonl && tail -3 $O/cumask.jsonl ;;

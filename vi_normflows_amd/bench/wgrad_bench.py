@@ -93,7 +93,8 @@ def probe(B: int, iters: int, tag: str, dev):
               flush=True)
 
 
-def layout_probe(B: int, layers: int, iters: int, tag: str, dev):
+def layout_probe(B: int, layers: int, iters: int, tag: str, dev, pad: int = 0,
+                 layouts=(0, 1, 2, 3)):
     """The real deferred weight-gradient launch (per layer dW3 [800 x 1024], dW2 [1024 x 1024],
     dW1 [1024 x 416], chunks of one tile per CU) with three operand layouts: 0 = dy, x both
     batch-major (TN, what the engine runs), 1 = x as a transposed [N][batch] copy (k-major B),
@@ -107,10 +108,15 @@ def layout_probe(B: int, layers: int, iters: int, tag: str, dev):
     H, Dp, Np = 1024, 416, 800
     g = torch.Generator(device=dev).manual_seed(0)
     dys, xs, outs, dbs, starts = [], [], [], [], [0]
+    def rows(n):   # [B, n] view of a [B, n + pad] buffer: row pitch off the power of two
+        t = torch.empty(B, n + pad, device=dev, dtype=bf)
+        t[:, :n].copy_(torch.randn(B, n, device=dev, generator=g).to(bf))
+        return t[:, :n]
+
     for _ in range(layers):
         for (o, i) in ((Np, H), (H, H), (H, Dp)):
-            dys.append(torch.randn(B, o, device=dev, generator=g).to(bf))
-            xs.append(torch.randn(B, i, device=dev, generator=g).to(bf))
+            dys.append(rows(o))
+            xs.append(rows(i))
             outs.append(torch.empty(o, i, device=dev))
             dbs.append(torch.empty(o, device=dev))
             starts.append(starts[-1] + wgrad_tiles(o, i))
@@ -119,6 +125,7 @@ def layout_probe(B: int, layers: int, iters: int, tag: str, dev):
     nl = total // cus
     ops = {0: (dys, xs), 1: (dys, [x.t().contiguous() for x in xs]),
            2: ([d.t().contiguous() for d in dys], xs), 3: (dys, xs)}
+    ops = {k: v for k, v in ops.items() if k in layouts}
     ref = None
     flops = 2.0 * B * cus * 256 * 256
     import bisect
@@ -148,7 +155,8 @@ def layout_probe(B: int, layers: int, iters: int, tag: str, dev):
                 ts.append(s.elapsed_time(e) * 1e3)
         ts.sort()
         med = ts[len(ts) // 2]
-        print(json.dumps({"tag": tag, "layout": layout, "launches": nl, "us_min": round(ts[0], 1),
+        print(json.dumps({"tag": tag, "layout": layout, "pitch_pad": pad, "launches": nl,
+                          "us_min": round(ts[0], 1),
                           "us_med": round(med, 1), "tflops_padded": round(flops / med / 1e6, 1),
                           "max_rel_diff_vs_layout0": err}), flush=True)
 
@@ -161,13 +169,16 @@ def main(argv=None):
     ap.add_argument("--tag", default=os.environ.get("VINF_BENCH_TAG", ""))
     ap.add_argument("--probe", action="store_true")
     ap.add_argument("--layout-probe", action="store_true")
+    ap.add_argument("--pitch-pad", type=int, default=0, help="layout probe: extra row elements")
+    ap.add_argument("--layouts", default="0,1,2,3")
     a = ap.parse_args(argv)
     dev = torch.device("cuda")
     if a.probe:
         probe(a.batch, a.iters, a.tag, dev)
         return
     if a.layout_probe:
-        layout_probe(a.batch, a.layers, a.iters, a.tag, dev)
+        layout_probe(a.batch, a.layers, a.iters, a.tag, dev, a.pitch_pad,
+                     tuple(int(v) for v in a.layouts.split(",")))
         return
     plan, _ = build(a.batch, a.layers, dev)
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
