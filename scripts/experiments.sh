@@ -126,6 +126,27 @@ case $name in
       done
     done
     cat $O/layout.jsonl ;;
+  wg_drift)       # L2 reuse of the 4-wave weight-gradient launch vs K (= batch): counters per K
+    export TMPDIR=/tmp
+    for b in 8192 32768 65536; do
+      timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum \
+        -d $O/pmc_b$b -o wg --output-format csv -- python3 -m vi_normflows_amd.bench.wgrad_bench --layers 13 --iters 1 --batch $b > $O/pmc_b$b.log 2>&1 || { tail -20 $O/pmc_b$b.log; exit 1; }
+    done
+    python3 - <<'PY'
+import csv, collections, os
+for b in (8192, 32768, 65536):
+    f = f"gpurun_out/exp_wg_drift/pmc_b{b}/wg_counter_collection.csv"
+    tot = collections.defaultdict(float); n = set()
+    for r in csv.DictReader(open(f)):
+        if "tn4w" not in r["Kernel_Name"]: continue
+        tot[r["Counter_Name"]] += float(r["Counter_Value"]); n.add(r["Dispatch_Id"])
+    h, m = tot["TCC_HIT_sum"], tot["TCC_MISS_sum"]
+    rd, r128 = tot["TCC_EA0_RDREQ_sum"], tot["TCC_EA0_RDREQ_128B_sum"]
+    eab = (128 * r128 + 64 * (rd - r128)) / max(len(n), 1)
+    req = 256 * 2 * 256 * 2 * b
+    print(b, "dispatches", len(n), "L2 hit %.3f" % (h / (h + m)), "fabric/requested %.3f" % (eab / req))
+PY
+    ;;
   cumask)         # CU-mask stream probe: mask bit -> XCD / SE / CU, and graph replay vs the mask
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/cumask_probe.hip -o $O/cumask_probe &&
     timeout -k 10 120 $O/cumask_probe > $O/cumask.jsonl && tail -3 $O/cumask.jsonl ;;

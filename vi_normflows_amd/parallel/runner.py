@@ -110,9 +110,11 @@ class DataParallelRunner:
                                              bucket_cap_mb=bucket_cap_mb,
                                              compress_bf16=compress_bf16, force=force)
             engine.unit_ready_hook = self.reducer.mark_ready
-            # weight-gradient launches of exactly one tile per CU wait for the buckets in flight
-            # (VINF_DP_WGRAD_FENCE=0 lets them start beside the all-reduce)
-            if hasattr(engine, "wgrad_fence_hook") and os.environ.get("VINF_DP_WGRAD_FENCE", "1") != "0":
+            # VINF_DP_WGRAD_FENCE=1: weight-gradient launches wait for the buckets in flight.
+            # Off by default: with the 4-wave weight-gradient kernel a collective resident at a
+            # launch's start costs nothing measurable (-0.24 / -0.03 ms at 250 / 500 us holds)
+            # while the fence waits it out (+1.0 / +2.4 ms), profiles/r4/dp_contention_tn4w.jsonl
+            if hasattr(engine, "wgrad_fence_hook") and os.environ.get("VINF_DP_WGRAD_FENCE", "0") == "1":
                 engine.wgrad_fence_hook = self.reducer.wait_inflight
 
     def _eager_step(self):
