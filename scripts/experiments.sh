@@ -147,6 +147,13 @@ for b in (8192, 32768, 65536):
     print(b, "dispatches", len(n), "L2 hit %.3f" % (h / (h + m)), "fabric/requested %.3f" % (eab / req))
 PY
     ;;
+  wg_kchunk)      # timing probe: the weight-gradient launch as 1 / 2 / 4 / 8 K-chunk launches
+    for r in 1 2; do
+      for kc in 1 2 4 8; do
+        VINF_BENCH_TAG=kc$kc timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --layout-probe --layers 13 --iters 3 --layouts 3 --kchunks $kc >> $O/layout.jsonl || exit 1
+      done
+    done
+    cat $O/layout.jsonl ;;
   cumask)         # CU-mask stream probe: mask bit -> XCD / SE / CU, and graph replay vs the mask
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/cumask_probe.hip -o $O/cumask_probe &&
     timeout -k 10 120 $O/cumask_probe > $O/cumask.jsonl && tail -3 $O/cumask.jsonl ;;

@@ -94,7 +94,7 @@ def probe(B: int, iters: int, tag: str, dev):
 
 
 def layout_probe(B: int, layers: int, iters: int, tag: str, dev, pad: int = 0,
-                 layouts=(0, 1, 2, 3)):
+                 layouts=(0, 1, 2, 3), kchunks: int = 1):
     """The real deferred weight-gradient launch (per layer dW3 [800 x 1024], dW2 [1024 x 1024],
     dW1 [1024 x 416], chunks of one tile per CU) with three operand layouts: 0 = dy, x both
     batch-major (TN, what the engine runs), 1 = x as a transposed [N][batch] copy (k-major B),
@@ -135,6 +135,14 @@ def layout_probe(B: int, layers: int, iters: int, tag: str, dev, pad: int = 0,
             t0, t1 = c * cus, (c + 1) * cus
             p0 = bisect.bisect_right(starts, t0) - 1
             p1 = bisect.bisect_left(starts, t1) - 1
+            if kchunks > 1 and layout in (0, 3):   # timing probe: K split over launches
+                kc = B // kchunks
+                for q in range(kchunks):
+                    native().gemm_tn_multi_layout([d[q * kc:(q + 1) * kc] for d in D_[p0:p1 + 1]],
+                                                  [x[q * kc:(q + 1) * kc] for x in X_[p0:p1 + 1]],
+                                                  outs[p0:p1 + 1], dbs[p0:p1 + 1],
+                                                  t0 - starts[p0], cus, layout)
+                return
             native().gemm_tn_multi_layout(D_[p0:p1 + 1], X_[p0:p1 + 1], outs[p0:p1 + 1],
                                           dbs[p0:p1 + 1], t0 - starts[p0], cus, layout)
         for c in range(nl):
@@ -155,7 +163,8 @@ def layout_probe(B: int, layers: int, iters: int, tag: str, dev, pad: int = 0,
                 ts.append(s.elapsed_time(e) * 1e3)
         ts.sort()
         med = ts[len(ts) // 2]
-        print(json.dumps({"tag": tag, "layout": layout, "pitch_pad": pad, "launches": nl,
+        print(json.dumps({"tag": tag, "layout": layout, "pitch_pad": pad, "kchunks": kchunks,
+                          "launches": nl,
                           "us_min": round(ts[0], 1),
                           "us_med": round(med, 1), "tflops_padded": round(flops / med / 1e6, 1),
                           "max_rel_diff_vs_layout0": err}), flush=True)
@@ -171,6 +180,8 @@ def main(argv=None):
     ap.add_argument("--layout-probe", action="store_true")
     ap.add_argument("--pitch-pad", type=int, default=0, help="layout probe: extra row elements")
     ap.add_argument("--layouts", default="0,1,2,3")
+    ap.add_argument("--kchunks", type=int, default=1,
+                    help="layout probe, timing only: each launch as K-chunk launches")
     a = ap.parse_args(argv)
     dev = torch.device("cuda")
     if a.probe:
@@ -178,7 +189,7 @@ def main(argv=None):
         return
     if a.layout_probe:
         layout_probe(a.batch, a.layers, a.iters, a.tag, dev, a.pitch_pad,
-                     tuple(int(v) for v in a.layouts.split(",")))
+                     tuple(int(v) for v in a.layouts.split(",")), a.kchunks)
         return
     plan, _ = build(a.batch, a.layers, dev)
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
