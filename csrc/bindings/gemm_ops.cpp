@@ -414,21 +414,25 @@ void gemm_nn_cpl(const at::Tensor& dy, const at::Tensor& W, const at::Tensor& G,
   for (const at::Tensor* t : {&G, &s_hat, &x, &dst, &gx})
     TORCH_CHECK(t->is_cuda() && t->dim() == 2 && t->stride(1) == 1 && t->size(0) == M,
                 "gemm_nn_cpl: 2-D GPU operands with unit inner stride and M rows");
-  TORCH_CHECK(G.scalar_type() == at::kFloat && G.size(1) == N, "G: fp32 [M, N]");
   const int Dh = x.size(1);
   const bool x_bf16 = x.scalar_type() == at::kBFloat16;
+  // the G chain may be bf16 (G in, gx out) on the bf16-x form
+  const bool g_bf16 = G.scalar_type() == at::kBFloat16, gx_bf16 = gx.scalar_type() == at::kBFloat16;
+  TORCH_CHECK((G.scalar_type() == at::kFloat || (g_bf16 && x_bf16)) && G.size(1) == N,
+              "G: fp32 (or bf16 with bf16 x) [M, N]");
   TORCH_CHECK((x.scalar_type() == at::kFloat || (x_bf16 && use_wt)) &&
-                  gx.scalar_type() == at::kFloat && gx.size(1) == Dh,
-              "x: fp32 (or bf16 with Wt) [M, Dh], gx: fp32 [M, Dh]");
+                  (gx.scalar_type() == at::kFloat || (gx_bf16 && x_bf16)) && gx.size(1) == Dh,
+              "x: fp32 (or bf16 with Wt) [M, Dh], gx: fp32 (or bf16 with bf16 x) [M, Dh]");
   TORCH_CHECK(s_hat.scalar_type() == at::kBFloat16 && s_hat.size(1) >= Dh, "s_hat: bf16 [M, >= Dh]");
   TORCH_CHECK(dst.scalar_type() == at::kBFloat16 && dst.size(1) >= 2 * Dh && dst.size(1) <= Dh + N,
               "dst: bf16 [M, 2 Dh .. Dh + N]");
   nf_launch_gemm256_nn_cpl(dy.data_ptr(), ld2(dy), use_wt ? Wt->data_ptr() : W.data_ptr(),
-                           use_wt ? ld2(*Wt) : ld2(W), G.data_ptr<float>(),
+                           use_wt ? ld2(*Wt) : ld2(W), (const float*)G.data_ptr(),
                            ld2(G), M, N, K, s_hat.data_ptr(), ld2(s_hat), (const float*)x.data_ptr(),
                            ld2(x), dst.data_ptr(), ld2(dst), (int)dst.size(1),
-                           gx.data_ptr<float>(), ld2(gx), Dh, (float)scale, (float)c, cur_stream(),
-                           use_wt ? 1 : 0, nullptr, 1, 0, nullptr, x_bf16 ? 1 : 0);
+                           (float*)gx.data_ptr(), ld2(gx), Dh, (float)scale, (float)c, cur_stream(),
+                           use_wt ? 1 : 0, nullptr, 1, 0, nullptr, x_bf16 ? 1 : 0, g_bf16 ? 1 : 0,
+                           gx_bf16 ? 1 : 0);
 }
 
 // MAF layer l's second MADE product with the layer's transform fused (gemm256.hip

@@ -74,6 +74,9 @@ struct GemmArgs {
   bf16_t* cpl_dst; long ld_cpl_dst;    // conditioner output gradient of layer l-1
   int cpl_dh, cpl_pad;
   float cpl_scale, cpl_c;
+  // EPI_CPL_BWD_XB only: the G chain in bf16 - C (the partial dL/dh_{l+1}) read as bf16 and / or
+  // gx written as bf16 (the engine keeps fp32 at the chain's two ends)
+  int cpl_c_bf16, cpl_gx_bf16;
   // cpl_mode 1: the backward of MAF layer l-1 instead (models/maf_engine.py, csrc/kernels/maf.hip)
   //   u = (x - mu) e^-alpha, alpha = b tanh(s_raw / b)   (b = cpl_scale, s_raw = aux, x = u_{l-1})
   //   gx = gy e^-alpha,  dst = [dmu | ds_raw] = [-gx | (cpl_c - gy u)(1 - tanh^2)]
@@ -139,11 +142,14 @@ inline bool staged_ok(const GemmArgs& a, int epi) {
   }
   if (epi == EPI_CPL_BWD || epi == EPI_CPL_BWD_XB) {
     const bool xok = epi == EPI_CPL_BWD ? al(a.cpl_x) : ((unsigned long)a.cpl_x & 7) == 0;
+    const bool gxok = a.cpl_gx_bf16 ? ((unsigned long)a.cpl_gx & 7) == 0 : al(a.cpl_gx);
     if (a.cpl_dh % 4 || a.ld_cpl_x % 4 || a.ld_cpl_gx % 4 || a.ld_cpl_dst % 4 || a.ld_aux % 4 ||
-        !xok || !al(a.cpl_gx) || ((unsigned long)a.cpl_dst & 7) || ((unsigned long)a.aux & 7))
+        !xok || !gxok || ((unsigned long)a.cpl_dst & 7) || ((unsigned long)a.aux & 7))
       return false;
   }
-  return a.N % 4 == 0 && a.ldc % 4 == 0 && a.c_split_stride % 4 == 0 && al(a.C);
+  const bool c_ok = (epi == EPI_CPL_BWD_XB && a.cpl_c_bf16) ? ((unsigned long)a.C & 7) == 0
+                                                           : al(a.C);
+  return a.N % 4 == 0 && a.ldc % 4 == 0 && a.c_split_stride % 4 == 0 && c_ok;
 }
 
 // Grouped launch: up to 4 independent problems (the weight gradients of one conditioner MLP),
@@ -528,7 +534,17 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
           int m = m0 + hj * 16 * PJ + it * 4 + (lane >> 4), n = n0 + q * 4 + (SPLITN && q >= 8 ? 96 : 0);
           m = m < a.M ? m : a.M - 1;
           n = n < a.N ? n : a.N - 4;
-          cv[it] = *reinterpret_cast<const float4*>((const float*)a.C + (long)m * a.ldc + n);
+          if constexpr (XB) {
+            if (a.cpl_c_bf16) {
+              const ushort4 h =
+                  *reinterpret_cast<const ushort4*>((const bf16_t*)a.C + (long)m * a.ldc + n);
+              cv[it] = make_float4(bf2f(h.x), bf2f(h.y), bf2f(h.z), bf2f(h.w));
+            } else {
+              cv[it] = *reinterpret_cast<const float4*>((const float*)a.C + (long)m * a.ldc + n);
+            }
+          } else {
+            cv[it] = *reinterpret_cast<const float4*>((const float*)a.C + (long)m * a.ldc + n);
+          }
           if constexpr (CPLB) {
             const int nx = n < a.cpl_dh ? n : a.cpl_dh - 4;
             sp[it] = *reinterpret_cast<const ushort4*>(a.aux + (long)m * a.ld_aux + nx);
@@ -597,8 +613,15 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
                   d1v[e] = gy[e];
                 }
               }
-              *reinterpret_cast<float4*>(a.cpl_gx + (long)m * a.ld_cpl_gx + n) =
-                  make_float4(gx[0], gx[1], gx[2], gx[3]);
+              if (XB && a.cpl_gx_bf16) {
+                ushort4 gh;
+                gh.x = f2bf(gx[0]); gh.y = f2bf(gx[1]); gh.z = f2bf(gx[2]); gh.w = f2bf(gx[3]);
+                *reinterpret_cast<ushort4*>(reinterpret_cast<bf16_t*>(a.cpl_gx) +
+                                            (long)m * a.ld_cpl_gx + n) = gh;
+              } else {
+                *reinterpret_cast<float4*>(a.cpl_gx + (long)m * a.ld_cpl_gx + n) =
+                    make_float4(gx[0], gx[1], gx[2], gx[3]);
+              }
               ushort4 d0, d1;
               d0.x = f2bf(dsh[0]); d0.y = f2bf(dsh[1]); d0.z = f2bf(dsh[2]); d0.w = f2bf(dsh[3]);
               d1.x = f2bf(d1v[0]); d1.y = f2bf(d1v[1]); d1.z = f2bf(d1v[2]); d1.w = f2bf(d1v[3]);

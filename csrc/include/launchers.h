@@ -138,7 +138,7 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
                               float* gx, long ld_gx, int Dh, float scale, float c,
                               hipStream_t stream, int w_kmajor = 0, const int* krange = nullptr,
                               int krange_segs = 1, int mode = 0, const NfF8Operands* f8 = nullptr,
-                              int x_bf16 = 0);
+                              int x_bf16 = 0, int g_in_bf16 = 0, int gx_bf16 = 0);
 void nf_launch_gemm256_fp8_dgrad(const void* dyq, long lddy, const float* sa, const void* wtq,
                                  long ldwt, const float* sb, const void* aux, long ld_aux,
                                  int aux_bits, void* dx, long lddx, int M, int N, int K,

@@ -1474,7 +1474,8 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
                               const float* x, long ld_x, void* dst, long ld_dst, int dst_pad,
                               float* gx, long ld_gx, int Dh, float scale, float c,
                               hipStream_t stream, int w_kmajor, const int* krange,
-                              int krange_segs, int mode, const NfF8Operands* f8, int x_bf16) {
+                              int krange_segs, int mode, const NfF8Operands* f8, int x_bf16,
+                              int g_in_bf16, int gx_bf16) {
   if (M <= 0 || N <= 0) return;
   GemmArgs a{};
   if (f8) {   // e4m3 dy (per-tensor scale) and Wt (per-row scales); optional e4m3 copy of dst
@@ -1497,6 +1498,11 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
   a.cpl_dst = (nf::bf16_t*)dst; a.ld_cpl_dst = ld_dst;
   a.cpl_dh = Dh; a.cpl_pad = dst_pad;
   a.cpl_scale = scale; a.cpl_c = c;
+  a.cpl_c_bf16 = g_in_bf16; a.cpl_gx_bf16 = gx_bf16;
+  if ((g_in_bf16 || gx_bf16) && !x_bf16) {
+    fprintf(stderr, "vinf: bf16 G chain in the fused backward needs the bf16-x form\n");
+    abort();
+  }
   // x_bf16: x is the bf16 copy of h_{l-1} (EPI_CPL_BWD_XB; bf16 coupling form only)
   const int epi = x_bf16 ? EPI_CPL_BWD_XB : EPI_CPL_BWD;
   if (x_bf16 && (f8 || mode || !w_kmajor)) {

@@ -176,26 +176,35 @@ def test_fused_coupling_backward_epilogue_matches_unfused(gpu, monkeypatch):
 
 @pytest.mark.gpu
 def test_fused_coupling_backward_bf16_x_close_to_fp32_x(gpu, monkeypatch):
-    """EPI_CPL_BWD_XB (x = h_{l-1} read from the bf16 conditioner operand) vs the fp32-x
-    epilogue on a trained-scale engine: x only enters dS_hat, whose product is stored in bf16,
-    so the parameter gradient moves by bf16 rounding of x (<= 2^-9 relative per element)."""
+    """EPI_CPL_BWD_XB (x = h_{l-1} read from the bf16 conditioner operand, and the middle of
+    the dL/dh chain kept in bf16) vs the fp32-x / fp32-G epilogue: x only enters dS_hat, whose
+    product is stored in bf16, and dL/dh only reaches the weight gradients through dst, which is
+    stored in bf16, so the parameter gradient moves by bf16 roundings (<= 2^-9 relative per
+    element, compounding over the layers for G)."""
     cfg = RealNVPConfig(dim=784, n_layers=6, hidden=512, anneal="none", init_out_std=0.1)
     a = RealNVPVI(cfg, batch=1024, device=gpu, seed=5)
     monkeypatch.setenv("VINF_CPL_XBF16", "0")
     b = RealNVPVI(cfg, batch=1024, device=gpu, seed=5)
-    assert a.cpl_xbf16 and not b.cpl_xbf16
+    monkeypatch.setenv("VINF_CPL_XBF16", "1")
+    monkeypatch.setenv("VINF_CPL_GBF16", "0")
+    c = RealNVPVI(cfg, batch=1024, device=gpu, seed=5)   # bf16 x, fp32 G chain
+    assert a.cpl_xbf16 and not b.cpl_xbf16 and a.g_bf16 and not b.g_bf16 and not c.g_bf16
     assert a._cpl_x(2, True).dtype == torch.bfloat16
     assert b._cpl_x(2, True).dtype == torch.float32
-    for e in (a, b):
+    for e in (a, b, c):
         e._update_schedule()
         e.forward()
         e.backward()
     torch.cuda.synchronize()
-    ga, gb = a.params.grad, b.params.grad
+    ga, gb, gc = a.params.grad, b.params.grad, c.params.grad
     assert torch.isfinite(ga).all()
     assert torch.equal(a.loss, b.loss)            # forward untouched
     rel = ((ga - gb).norm() / gb.norm()).item()
     assert rel <= 1e-2, rel
+    # the bf16 middle of the G chain alone (x bf16 in both): one more bf16 rounding of
+    # dL/dh per layer, compounding over the 6 layers
+    rel_g = ((ga - gc).norm() / gc.norm()).item()
+    assert rel_g <= 1e-2, rel_g
     # the weight-gradient cosine stays at bf16-noise level
     cos = torch.nn.functional.cosine_similarity(ga, gb, dim=0).item()
     assert cos >= 0.9999, cos

@@ -234,6 +234,14 @@ class RealNVPVI:
             self.wgrad_stream = torch.cuda.Stream(device=dev)
         self._G = torch.zeros(L + 2, B, Dp, dtype=f32, device=dev)   # dL/dh_i, 0-padded rows
         self.G = self._G[:, :, :Dh]
+        # the middle of the G chain in bf16 (VINF_CPL_GBF16=0: fp32): the fused coupling backward
+        # of layer l-1 (EPI_CPL_BWD_XB) reads G[l+1] / writes G[l-1] in bf16 where both sides are
+        # bf16-x fused epilogues (reads 2 <= l <= L-3, writes 4 <= l <= L-1); the chain's ends
+        # (target gradient, top coupling backward, layers 0-1, base backward) stay fp32
+        self.g_bf16 = (self.cpl_fuse and self.cpl_xbf16 and self.cdt == torch.bfloat16
+                       and os.environ.get("VINF_CPL_GBF16", "1") != "0")
+        self._G16 = (torch.zeros(L + 2, B, Dp, dtype=torch.bfloat16, device=dev)
+                     if self.g_bf16 else None)
         # per-slab column sums of the base backward (HIP path: float4 columns, <= 1024 wide)
         self._rg_partial = None
         if (dev.type == "cuda" and D % 4 == 0 and Dh % 4 == 0 and Dp % 4 == 0 and D <= 1024
@@ -494,10 +502,15 @@ class RealNVPVI:
                 elif fuse and l > 0:
                     # dL/dh_{l+1} = G[l+1] + d W0 is finished and consumed by layer l-1's
                     # coupling backward in the same epilogue (writes dstL[l-1], G[l-1])
-                    gemm.linear_dgrad_coupling(d, P.c(f"l{l}.W0"), self._G[l + 1],
+                    xb = self._cpl_x(l - 1, WT is not None)
+                    # bf16 G is read by layers 2 <= l <= L-3 (bf16-x form, written by a fused
+                    # epilogue) and written by layers 4 <= l <= L-1 (their readers l-2)
+                    g16 = self.g_bf16 and xb.dtype == torch.bfloat16
+                    gin = self._G16[l + 1] if g16 and 2 <= l <= L - 3 else self._G[l + 1]
+                    gout = (self._G16[l - 1] if g16 and l >= 4 else self._G[l - 1])[:, :cfg.half]
+                    gemm.linear_dgrad_coupling(d, P.c(f"l{l}.W0"), gin,
                                                s_hat=self.ST[l - 1][:, :cfg.half],
-                                               x=self._cpl_x(l - 1, WT is not None),
-                                               dst=self.dstL[l - 1], gx=self.G[l - 1],
+                                               x=xb, dst=self.dstL[l - 1], gx=gout,
                                                scale=cfg.scale_bound, c=c,
                                                Wt=None if WT is None else WT[l][0])
                 else:
