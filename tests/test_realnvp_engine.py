@@ -182,6 +182,7 @@ def test_fused_coupling_backward_bf16_x_close_to_fp32_x(gpu, monkeypatch):
     stored in bf16, so the parameter gradient moves by bf16 roundings (<= 2^-9 relative per
     element, compounding over the layers for G)."""
     cfg = RealNVPConfig(dim=784, n_layers=6, hidden=512, anneal="none", init_out_std=0.1)
+    monkeypatch.setenv("VINF_CPL_GBF16", "1")   # the opt-in bf16 G chain
     a = RealNVPVI(cfg, batch=1024, device=gpu, seed=5)
     monkeypatch.setenv("VINF_CPL_XBF16", "0")
     b = RealNVPVI(cfg, batch=1024, device=gpu, seed=5)

@@ -234,12 +234,14 @@ class RealNVPVI:
             self.wgrad_stream = torch.cuda.Stream(device=dev)
         self._G = torch.zeros(L + 2, B, Dp, dtype=f32, device=dev)   # dL/dh_i, 0-padded rows
         self.G = self._G[:, :, :Dh]
-        # the middle of the G chain in bf16 (VINF_CPL_GBF16=0: fp32): the fused coupling backward
+        # opt-in (VINF_CPL_GBF16=1; measured slower: 34.90-35.09 vs 34.70-34.81 ms/step on one
+        # box, profiles/r4/cpl_gbf16_step_ab.jsonl - the 8-B loads / stores cost more than the
+        # 110 MB per call they save): the middle of the G chain in bf16. The fused coupling backward
         # of layer l-1 (EPI_CPL_BWD_XB) reads G[l+1] / writes G[l-1] in bf16 where both sides are
         # bf16-x fused epilogues (reads 2 <= l <= L-3, writes 4 <= l <= L-1); the chain's ends
         # (target gradient, top coupling backward, layers 0-1, base backward) stay fp32
         self.g_bf16 = (self.cpl_fuse and self.cpl_xbf16 and self.cdt == torch.bfloat16
-                       and os.environ.get("VINF_CPL_GBF16", "1") != "0")
+                       and os.environ.get("VINF_CPL_GBF16", "0") == "1")
         self._G16 = (torch.zeros(L + 2, B, Dp, dtype=torch.bfloat16, device=dev)
                      if self.g_bf16 else None)
         # per-slab column sums of the base backward (HIP path: float4 columns, <= 1024 wide)
