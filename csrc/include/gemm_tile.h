@@ -315,7 +315,11 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) bv[i][r] = 0.f;
+#ifdef NF_EPI_NOLOAD   // diagnostic build (timing only, wrong results): no epilogue operand loads
+    if (false) {
+#else
     if (EPI == EPI_BF16 && a.bias) {
+#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int n = n0 + i * 16 + g * 4;
@@ -377,7 +381,11 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
           int m = m0 + it * 8 + (lane >> 3), n = n0 + q * 8;
           m = m < a.M ? m : a.M - 1;
           n = n < a.N ? n : a.N - 8;
+#ifdef NF_EPI_NOLOAD
+          hb[it] = 0xffu ^ (unsigned)(m & 1);
+#else
           hb[it] = ((const unsigned char*)a.aux)[(long)m * a.ld_aux + (n >> 3)];
+#endif
         }
       } else {
 #pragma unroll

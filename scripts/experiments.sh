@@ -154,6 +154,14 @@ PY
       done
     done
     cat $O/layout.jsonl ;;
+  epi_noload)     # diagnostic: the persistent products without their epilogue operand loads (bias,
+                  # ReLU bits; timing only) vs the default library, per product
+    L=vi_normflows_amd/_native/libvinf_hip_noload.so
+    for r in 1 2; do
+      VINF_BENCH_TAG=default timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,dgrad_l2 >> $O/sg.jsonl || exit 1
+      VINF_NATIVE_LIB=$L VINF_BENCH_TAG=noload timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,dgrad_l2 >> $O/sg.jsonl || exit 1
+    done
+    cat $O/sg.jsonl ;;
   cumask)         # CU-mask stream probe: mask bit -> XCD / SE / CU, and graph replay vs the mask
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/cumask_probe.hip -o $O/cumask_probe &&
     timeout -k 10 120 $O/cumask_probe > $O/cumask.jsonl && tail -3 $O/cumask.jsonl ;;
