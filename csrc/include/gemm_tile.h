@@ -304,10 +304,19 @@ __device__ __forceinline__ v4u bf_stage_fix(v4u v, bool swapped) {
 // origin of block J0), so a caller short of LDS can stage a sub-tile in several calls.
 // SPLITN (fp32 outputs only): the wave's 64 columns are two 32-column groups, n0 + [0, 32) and
 // n0 + 128 + [0, 32) (contiguous-B-half weight-gradient tiles, gemm256.hip stage_half BCONTIG)
-template <int EPI, int NJ, bool F8 = false, int J0 = 0, int NJA = NJ, bool SPLITN = false>
+// Epilogue operands loaded ahead of time (A/B build NF_EPI_PRELOAD, persistent NT products): the
+// bias of the tile's columns and the ReLU bits of its rows, issued before the next tile's LDS-DMA
+// burst so the epilogue does not wait behind those DMAs (vmcnt retires in issue order)
+struct EpiPre {
+  float bv[4][4];
+  unsigned hb4[4];   // 16 bitmask bytes, 4 per register
+};
+
+template <int EPI, int NJ, bool F8 = false, int J0 = 0, int NJA = NJ, bool SPLITN = false,
+          bool PRE = false>
 __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&acc)[4][NJA],
                                                 int m0, int n0, int split, char* region,
-                                                int lane) {
+                                                int lane, const EpiPre* pre = nullptr) {
   const int g = lane >> 4, c = lane & 15;
   if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK) {
     float bv[4][4];
@@ -315,10 +324,16 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) bv[i][r] = 0.f;
+    if constexpr (PRE) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[i][r] = pre->bv[i][r];
+    }
 #ifdef NF_EPI_NOLOAD   // diagnostic build (timing only, wrong results): no epilogue operand loads
     if (false) {
 #else
-    if (EPI == EPI_BF16 && a.bias) {
+    if (!PRE && EPI == EPI_BF16 && a.bias) {
 #endif
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -384,7 +399,8 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
 #ifdef NF_EPI_NOLOAD
           hb[it] = 0xffu ^ (unsigned)(m & 1);
 #else
-          hb[it] = ((const unsigned char*)a.aux)[(long)m * a.ld_aux + (n >> 3)];
+          if constexpr (PRE) hb[it] = (pre->hb4[(J0 * 2 + it) >> 2] >> (8 * ((J0 * 2 + it) & 3))) & 0xffu;
+          else hb[it] = ((const unsigned char*)a.aux)[(long)m * a.ld_aux + (n >> 3)];
 #endif
         }
       } else {

@@ -118,7 +118,7 @@ __device__ __forceinline__ v8i cat16(v8s lo, v8s hi) {
 // of a half is 256 contiguous bytes - whole 128-B lines - where the split halves fetched each
 // line in two 64-B pieces at different times. Wave wc then owns tile columns
 // {wc*32 + 0..31} (N0-1) and {128 + wc*32 + 0..31} (N2-3); the epilogue maps them back.
-template <bool KMAJOR, int EB = 2, bool BCONTIG = false>
+template <bool KMAJOR, int EB = 2, bool BCONTIG = false, bool ASMDMA = true>
 __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long ld, int row0,
                                            int rows_total, int k0, int K, bool is_a, bool hi,
                                            char* dst, int wave, int lane, int pair_dh = 0) {
@@ -158,6 +158,11 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long
       src = base + (long)gk * ld + gm;
     }
 #ifndef NF_G256_BUILTIN_DMA
+    if constexpr (!ASMDMA) {   // the preload build's NT kernels: DMA visible to the compiler
+      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(dst + piece * 1024), 16,
+                                       0, 0);
+      continue;
+    }
     // The DMA in asm, invisible to the compiler's wait-count pass. With the builtin it drains
     // the DMA queue (s_waitcnt vmcnt(0)) before every ds_read_b64_tr_b16 / _tr_b8 of the
     // mn-major operands (12 such drains in the weight-gradient kernel, none before the k-major
@@ -710,6 +715,14 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
 template <bool A_KMAJOR, bool B_KMAJOR, int EPI>
 __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char* smem) {
   constexpr int D = 4, NSLOT = 8;
+#ifdef NF_EPI_PRELOAD
+  // NT products: the compiler sees the DMA (no transposed reads, so it never drains before the
+  // b128 reads) and can then wait for the preloaded epilogue operands without the DMAs behind them
+  constexpr bool PRE = A_KMAJOR && B_KMAJOR && (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK);
+#else
+  constexpr bool PRE = false;
+#endif
+  constexpr bool ASMDMA = !PRE;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -737,12 +750,14 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
     char* dst = smem + ((4 * Tg + j) & (NSLOT - 1)) * HALF_BYTES;
     const int k0 = tk * BK;
     if (j == H_ALO || j == H_AHI)
-      stage_half<A_KMAJOR>(a.A, a.lda, tm0, a.M, k0, a.K, true, j == H_AHI, dst, wave, lane);
+      stage_half<A_KMAJOR, 2, false, ASMDMA>(a.A, a.lda, tm0, a.M, k0, a.K, true, j == H_AHI, dst,
+                                             wave, lane);
     else if constexpr (EPI == EPI_CPL_FWD)
-      stage_half<B_KMAJOR>(a.B, a.ldb, tn0, a.cf_b_rows, k0, a.K, false, j == H_BHI, dst, wave,
-                           lane, a.cf_pair);
+      stage_half<B_KMAJOR, 2, false, ASMDMA>(a.B, a.ldb, tn0, a.cf_b_rows, k0, a.K, false,
+                                             j == H_BHI, dst, wave, lane, a.cf_pair);
     else
-      stage_half<B_KMAJOR>(a.B, a.ldb, tn0, a.N, k0, a.K, false, j == H_BHI, dst, wave, lane);
+      stage_half<B_KMAJOR, 2, false, ASMDMA>(a.B, a.ldb, tn0, a.N, k0, a.K, false, j == H_BHI, dst,
+                                             wave, lane);
   };
 
   v4f acc[4][8];
@@ -879,6 +894,37 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
     // slots of K-tiles T-2 (all four, read long ago) and T-1's A-lo / B-lo (read in its phase
     // r1) - not the free pair the epilogue stages through
     int m0n = 0, n0n = 0;
+    EpiPre pre;
+    if constexpr (PRE) {   // this tile's bias / ReLU bits, ahead of the DMA burst
+      const int g = lane >> 4, q = lane & 7;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pre.bv[i][r] = 0.f;
+      if (EPI == EPI_BF16 && a.bias) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = n0 + wc * 64 + i * 16 + g * 4;
+          if (n < a.N) {
+            const ushort4 bb = *reinterpret_cast<const ushort4*>(a.bias + n);
+            pre.bv[i][0] = bf2f(bb.x); pre.bv[i][1] = bf2f(bb.y);
+            pre.bv[i][2] = bf2f(bb.z); pre.bv[i][3] = bf2f(bb.w);
+          }
+        }
+      }
+#pragma unroll
+      for (int w = 0; w < 4; ++w) pre.hb4[w] = 0u;
+      if (EPI == EPI_BF16_RELUMASK && a.aux_bits) {
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+          int m = m0 + wr * 128 + it * 8 + (lane >> 3), n = n0 + wc * 64 + q * 8;
+          m = m < a.M ? m : a.M - 1;
+          n = n < a.N ? n : a.N - 8;
+          pre.hb4[it >> 2] |= (unsigned)((const unsigned char*)a.aux)[(long)m * a.ld_aux + (n >> 3)]
+                              << (8 * (it & 3));
+        }
+      }
+    }
     if (has_next) {
       tile_org(s + 1, m0n, n0n);
 #pragma unroll
@@ -902,10 +948,11 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
                           },
                           lane_e, tid_e);
     } else if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK) {
-      epi_tile_staged<EPI, 4, false, 0, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, 0, region, lane);
+      epi_tile_staged<EPI, 4, false, 0, 8, false, PRE>(a, acc, m0 + wr * 128, n0 + wc * 64, 0,
+                                                       region, lane, &pre);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own readback done before re-staging
-      epi_tile_staged<EPI, 4, false, 4, 8>(a, acc, m0 + wr * 128 + 64, n0 + wc * 64, 0, region,
-                                           lane);
+      epi_tile_staged<EPI, 4, false, 4, 8, false, PRE>(a, acc, m0 + wr * 128 + 64, n0 + wc * 64, 0,
+                                                       region, lane, &pre);
     } else {
       epi_tile_staged<EPI, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, 0, region, lane_e);
     }
