@@ -153,8 +153,11 @@ def realnvp_useful_gflop(batch=65536, dim=784, hidden=1024, layers=32):
         "coupling fwd NT EPI5 (fused)": L * g(B, 2 * Dh, H),
         "dgrad NT EPI2 (ReLU bitmask)": L * (g(B, H, 2 * Dh) + g(B, H, H)),
         "coupling bwd NT EPI4 (fused)": (L - 1) * g(B, Dh, H),
+        "coupling bwd NT EPI6 (fused, bf16 x)": (L - 1) * g(B, Dh, H),
         "layer-0 dgrad NN EPI3 (fp32 acc)": g(B, Dh, H),
         "wgrad TN bf16 (multi-layer, K = batch)": L * (g(2 * Dh, H, B) + g(H, H, B) + g(H, Dh, B)),
+        "wgrad TN bf16 4-wave (multi-layer, K = batch)":
+            L * (g(2 * Dh, H, B) + g(H, H, B) + g(H, Dh, B)),
     }
 
 
