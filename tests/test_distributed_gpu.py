@@ -91,9 +91,13 @@ def _rccl_worker(rank, port, out_dir):
     cfg = RealNVPConfig(dim=64, n_layers=4, hidden=256, target="banana", anneal="none",
                         init_out_std=0.2)
     out = {}
-    for name in ("plain", "rccl_eager", "rccl_graph"):
+    for name in ("plain", "rccl_eager", "rccl_graph", "rccl_fence"):
+        # rccl_fence: the opt-in weight-gradient fence (each launch waits for the collectives
+        # in flight, VINF_DP_WGRAD_FENCE=1) must not change a bit either
+        os.environ["VINF_DP_WGRAD_FENCE"] = "1" if name == "rccl_fence" else "0"
         eng = RealNVPVI(cfg, batch=512, device=dev, seed=7, lr=1e-3)
         run = DataParallelRunner(eng, info, bucket_cap_mb=0.05, force_reduce=(name != "plain"))
+        assert (eng.wgrad_fence_hook is not None) == (name == "rccl_fence")
         if name == "plain":
             assert run.reducer is None
         else:
@@ -117,10 +121,11 @@ def _rccl_worker(rank, port, out_dir):
 def test_rccl_reducer_eager_and_captured_bitwise(tmp_path):
     mp.spawn(_rccl_worker, args=(_port(), str(tmp_path)), nprocs=1, join=True)
     r = torch.load(tmp_path / "rccl.pt", weights_only=True)
-    for k in ("plain", "rccl_eager", "rccl_graph"):
+    for k in ("plain", "rccl_eager", "rccl_graph", "rccl_fence"):
         assert r[k + "_step"] == 3.0
     assert torch.equal(r["plain"], r["rccl_eager"])
     assert torch.equal(r["plain"], r["rccl_graph"])
+    assert torch.equal(r["plain"], r["rccl_fence"])
     assert r["plain_loss"] == r["rccl_graph_loss"]
 
 
