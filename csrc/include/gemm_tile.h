@@ -308,8 +308,8 @@ __device__ __forceinline__ v4u bf_stage_fix(v4u v, bool swapped) {
 // bias of the tile's columns and the ReLU bits of its rows, issued before the next tile's LDS-DMA
 // burst so the epilogue does not wait behind those DMAs (vmcnt retires in issue order)
 struct EpiPre {
-  float bv[4][4];
-  unsigned hb4[4];   // 16 bitmask bytes, 4 per register
+  ushort4 bb[4];     // bias of the wave's 4 column groups, raw bf16 (8 registers)
+  unsigned hb4[2];   // the first pass's 8 bitmask bytes, 4 per register
 };
 
 template <int EPI, int NJ, bool F8 = false, int J0 = 0, int NJA = NJ, bool SPLITN = false,
@@ -326,9 +326,10 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
       for (int r = 0; r < 4; ++r) bv[i][r] = 0.f;
     if constexpr (PRE) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bv[i][r] = pre->bv[i][r];
+      for (int i = 0; i < 4; ++i) {
+        const ushort4 bb = pre->bb[i];
+        bv[i][0] = bf2f(bb.x); bv[i][1] = bf2f(bb.y); bv[i][2] = bf2f(bb.z); bv[i][3] = bf2f(bb.w);
+      }
     }
 #ifdef NF_EPI_NOLOAD   // diagnostic build (timing only, wrong results): no epilogue operand loads
     if (false) {
@@ -399,7 +400,9 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
 #ifdef NF_EPI_NOLOAD
           hb[it] = 0xffu ^ (unsigned)(m & 1);
 #else
-          if constexpr (PRE) hb[it] = (pre->hb4[(J0 * 2 + it) >> 2] >> (8 * ((J0 * 2 + it) & 3))) & 0xffu;
+          // preloaded: the first pass's rows (the second pass runs after the next tile's DMA
+          // burst has landed)
+          if constexpr (PRE && J0 == 0) hb[it] = (pre->hb4[it >> 2] >> (8 * (it & 3))) & 0xffu;
           else hb[it] = ((const unsigned char*)a.aux)[(long)m * a.ld_aux + (n >> 3)];
 #endif
         }

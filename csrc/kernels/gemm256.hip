@@ -716,13 +716,15 @@ template <bool A_KMAJOR, bool B_KMAJOR, int EPI>
 __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char* smem) {
   constexpr int D = 4, NSLOT = 8;
 #ifdef NF_EPI_PRELOAD
-  // NT products: the compiler sees the DMA (no transposed reads, so it never drains before the
-  // b128 reads) and can then wait for the preloaded epilogue operands without the DMAs behind them
-  constexpr bool PRE = A_KMAJOR && B_KMAJOR && (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK);
+  // the epilogue's own global operands (bias / ReLU bits) are loaded at the start of a tile's
+  // last K-tile and consumed (waited for) before the next tile's DMA burst: otherwise the
+  // epilogue's vmcnt wait for them also waits out that burst (vmcnt retires in issue order),
+  // the whole difference of a no-load diagnostic build (dgrad 141 -> 127 us)
+  constexpr bool PRE = EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK;
 #else
   constexpr bool PRE = false;
 #endif
-  constexpr bool ASMDMA = !PRE;
+  constexpr bool ASMDMA = true;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -875,11 +877,37 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
   for (int s = 0; s < ns; ++s) {
     const bool has_next = s + 1 < ns;
     if (wr == 1) barrier();
+    EpiPre pre;
+    auto preload = [&]() {   // this tile's bias / ReLU bits (NF_EPI_PRELOAD)
+      const int g = lane >> 4, q = lane & 7;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pre.bb[i] = make_ushort4(0, 0, 0, 0);
+#pragma unroll
+      for (int w = 0; w < 2; ++w) pre.hb4[w] = 0u;
+      if (EPI == EPI_BF16 && a.bias) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = n0 + wc * 64 + i * 16 + g * 4;
+          if (n < a.N) pre.bb[i] = *reinterpret_cast<const ushort4*>(a.bias + n);
+        }
+      }
+      if (EPI == EPI_BF16_RELUMASK && a.aux_bits) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          int m = m0 + wr * 128 + it * 8 + (lane >> 3), n = n0 + wc * 64 + q * 8;
+          m = m < a.M ? m : a.M - 1;
+          n = n < a.N ? n : a.N - 8;
+          pre.hb4[it >> 2] |= (unsigned)((const unsigned char*)a.aux)[(long)m * a.ld_aux + (n >> 3)]
+                              << (8 * (it & 3));
+        }
+      }
+    };
     auto tile_loop = [&](auto edge_c) {
       for (int t = 0; t < nkt - 2; ++t, ++T)
         ktile(T, t, m0, n0, true, std::integral_constant<int, 0>{}, std::true_type{}, edge_c);
       ktile(T, nkt - 2, m0, n0, true, std::integral_constant<int, 1>{}, std::true_type{}, edge_c);
       ++T;
+      if constexpr (PRE) preload();
       ktile(T, nkt - 1, m0, n0, !tail_half, std::integral_constant<int, 2>{}, std::false_type{},
             edge_c);
       ++T;
@@ -894,36 +922,13 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
     // slots of K-tiles T-2 (all four, read long ago) and T-1's A-lo / B-lo (read in its phase
     // r1) - not the free pair the epilogue stages through
     int m0n = 0, n0n = 0;
-    EpiPre pre;
-    if constexpr (PRE) {   // this tile's bias / ReLU bits, ahead of the DMA burst
-      const int g = lane >> 4, q = lane & 7;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pre.bv[i][r] = 0.f;
-      if (EPI == EPI_BF16 && a.bias) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int n = n0 + wc * 64 + i * 16 + g * 4;
-          if (n < a.N) {
-            const ushort4 bb = *reinterpret_cast<const ushort4*>(a.bias + n);
-            pre.bv[i][0] = bf2f(bb.x); pre.bv[i][1] = bf2f(bb.y);
-            pre.bv[i][2] = bf2f(bb.z); pre.bv[i][3] = bf2f(bb.w);
-          }
-        }
-      }
-#pragma unroll
-      for (int w = 0; w < 4; ++w) pre.hb4[w] = 0u;
-      if (EPI == EPI_BF16_RELUMASK && a.aux_bits) {
-#pragma unroll
-        for (int it = 0; it < 16; ++it) {
-          int m = m0 + wr * 128 + it * 8 + (lane >> 3), n = n0 + wc * 64 + q * 8;
-          m = m < a.M ? m : a.M - 1;
-          n = n < a.N ? n : a.N - 8;
-          pre.hb4[it >> 2] |= (unsigned)((const unsigned char*)a.aux)[(long)m * a.ld_aux + (n >> 3)]
-                              << (8 * (it & 3));
-        }
-      }
+    if constexpr (PRE) {
+      // consume the preloads here: the compiler's wait for them lands before the burst below
+      if constexpr (EPI == EPI_BF16_RELUMASK)
+        asm volatile("" ::"v"(pre.hb4[0]), "v"(pre.hb4[1]));
+      else
+        asm volatile("" ::"v"(pre.bb[0].x), "v"(pre.bb[1].x), "v"(pre.bb[2].x), "v"(pre.bb[3].x),
+                     "v"(pre.bb[0].w), "v"(pre.bb[1].w), "v"(pre.bb[2].w), "v"(pre.bb[3].w));
     }
     if (has_next) {
       tile_org(s + 1, m0n, n0n);
