@@ -304,19 +304,10 @@ __device__ __forceinline__ v4u bf_stage_fix(v4u v, bool swapped) {
 // origin of block J0), so a caller short of LDS can stage a sub-tile in several calls.
 // SPLITN (fp32 outputs only): the wave's 64 columns are two 32-column groups, n0 + [0, 32) and
 // n0 + 128 + [0, 32) (contiguous-B-half weight-gradient tiles, gemm256.hip stage_half BCONTIG)
-// Epilogue operands loaded ahead of time (A/B build NF_EPI_PRELOAD, persistent NT products): the
-// bias of the tile's columns and the ReLU bits of its rows, issued before the next tile's LDS-DMA
-// burst so the epilogue does not wait behind those DMAs (vmcnt retires in issue order)
-struct EpiPre {
-  ushort4 bb[4];     // bias of the wave's 4 column groups, raw bf16 (8 registers)
-  unsigned hb4[2];   // the first pass's 8 bitmask bytes, 4 per register
-};
-
-template <int EPI, int NJ, bool F8 = false, int J0 = 0, int NJA = NJ, bool SPLITN = false,
-          bool PRE = false>
+template <int EPI, int NJ, bool F8 = false, int J0 = 0, int NJA = NJ, bool SPLITN = false>
 __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&acc)[4][NJA],
                                                 int m0, int n0, int split, char* region,
-                                                int lane, const EpiPre* pre = nullptr) {
+                                                int lane) {
   const int g = lane >> 4, c = lane & 15;
   if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK) {
     float bv[4][4];
@@ -324,18 +315,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) bv[i][r] = 0.f;
-    if constexpr (PRE) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const ushort4 bb = pre->bb[i];
-        bv[i][0] = bf2f(bb.x); bv[i][1] = bf2f(bb.y); bv[i][2] = bf2f(bb.z); bv[i][3] = bf2f(bb.w);
-      }
-    }
-#ifdef NF_EPI_NOLOAD   // diagnostic build (timing only, wrong results): no epilogue operand loads
-    if (false) {
-#else
-    if (!PRE && EPI == EPI_BF16 && a.bias) {
-#endif
+    if (EPI == EPI_BF16 && a.bias) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int n = n0 + i * 16 + g * 4;
@@ -397,14 +377,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
           int m = m0 + it * 8 + (lane >> 3), n = n0 + q * 8;
           m = m < a.M ? m : a.M - 1;
           n = n < a.N ? n : a.N - 8;
-#ifdef NF_EPI_NOLOAD
-          hb[it] = 0xffu ^ (unsigned)(m & 1);
-#else
-          // preloaded: the first pass's rows (the second pass runs after the next tile's DMA
-          // burst has landed)
-          if constexpr (PRE && J0 == 0) hb[it] = (pre->hb4[it >> 2] >> (8 * (it & 3))) & 0xffu;
-          else hb[it] = ((const unsigned char*)a.aux)[(long)m * a.ld_aux + (n >> 3)];
-#endif
+          hb[it] = ((const unsigned char*)a.aux)[(long)m * a.ld_aux + (n >> 3)];
         }
       } else {
 #pragma unroll

@@ -118,7 +118,7 @@ __device__ __forceinline__ v8i cat16(v8s lo, v8s hi) {
 // of a half is 256 contiguous bytes - whole 128-B lines - where the split halves fetched each
 // line in two 64-B pieces at different times. Wave wc then owns tile columns
 // {wc*32 + 0..31} (N0-1) and {128 + wc*32 + 0..31} (N2-3); the epilogue maps them back.
-template <bool KMAJOR, int EB = 2, bool BCONTIG = false, bool ASMDMA = true>
+template <bool KMAJOR, int EB = 2, bool BCONTIG = false>
 __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long ld, int row0,
                                            int rows_total, int k0, int K, bool is_a, bool hi,
                                            char* dst, int wave, int lane, int pair_dh = 0) {
@@ -158,11 +158,6 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long
       src = base + (long)gk * ld + gm;
     }
 #ifndef NF_G256_BUILTIN_DMA
-    if constexpr (!ASMDMA) {   // the preload build's NT kernels: DMA visible to the compiler
-      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(dst + piece * 1024), 16,
-                                       0, 0);
-      continue;
-    }
     // The DMA in asm, invisible to the compiler's wait-count pass. With the builtin it drains
     // the DMA queue (s_waitcnt vmcnt(0)) before every ds_read_b64_tr_b16 / _tr_b8 of the
     // mn-major operands (12 such drains in the weight-gradient kernel, none before the k-major
@@ -715,16 +710,6 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
 template <bool A_KMAJOR, bool B_KMAJOR, int EPI>
 __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char* smem) {
   constexpr int D = 4, NSLOT = 8;
-#ifdef NF_EPI_PRELOAD
-  // the epilogue's own global operands (bias / ReLU bits) are loaded at the start of a tile's
-  // last K-tile and consumed (waited for) before the next tile's DMA burst: otherwise the
-  // epilogue's vmcnt wait for them also waits out that burst (vmcnt retires in issue order),
-  // the whole difference of a no-load diagnostic build (dgrad 141 -> 127 us)
-  constexpr bool PRE = EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK;
-#else
-  constexpr bool PRE = false;
-#endif
-  constexpr bool ASMDMA = true;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -752,14 +737,12 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
     char* dst = smem + ((4 * Tg + j) & (NSLOT - 1)) * HALF_BYTES;
     const int k0 = tk * BK;
     if (j == H_ALO || j == H_AHI)
-      stage_half<A_KMAJOR, 2, false, ASMDMA>(a.A, a.lda, tm0, a.M, k0, a.K, true, j == H_AHI, dst,
-                                             wave, lane);
+      stage_half<A_KMAJOR>(a.A, a.lda, tm0, a.M, k0, a.K, true, j == H_AHI, dst, wave, lane);
     else if constexpr (EPI == EPI_CPL_FWD)
-      stage_half<B_KMAJOR, 2, false, ASMDMA>(a.B, a.ldb, tn0, a.cf_b_rows, k0, a.K, false,
-                                             j == H_BHI, dst, wave, lane, a.cf_pair);
+      stage_half<B_KMAJOR>(a.B, a.ldb, tn0, a.cf_b_rows, k0, a.K, false, j == H_BHI, dst, wave,
+                           lane, a.cf_pair);
     else
-      stage_half<B_KMAJOR, 2, false, ASMDMA>(a.B, a.ldb, tn0, a.N, k0, a.K, false, j == H_BHI, dst,
-                                             wave, lane);
+      stage_half<B_KMAJOR>(a.B, a.ldb, tn0, a.N, k0, a.K, false, j == H_BHI, dst, wave, lane);
   };
 
   v4f acc[4][8];
@@ -877,37 +860,11 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
   for (int s = 0; s < ns; ++s) {
     const bool has_next = s + 1 < ns;
     if (wr == 1) barrier();
-    EpiPre pre;
-    auto preload = [&]() {   // this tile's bias / ReLU bits (NF_EPI_PRELOAD)
-      const int g = lane >> 4, q = lane & 7;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) pre.bb[i] = make_ushort4(0, 0, 0, 0);
-#pragma unroll
-      for (int w = 0; w < 2; ++w) pre.hb4[w] = 0u;
-      if (EPI == EPI_BF16 && a.bias) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int n = n0 + wc * 64 + i * 16 + g * 4;
-          if (n < a.N) pre.bb[i] = *reinterpret_cast<const ushort4*>(a.bias + n);
-        }
-      }
-      if (EPI == EPI_BF16_RELUMASK && a.aux_bits) {
-#pragma unroll
-        for (int it = 0; it < 8; ++it) {
-          int m = m0 + wr * 128 + it * 8 + (lane >> 3), n = n0 + wc * 64 + q * 8;
-          m = m < a.M ? m : a.M - 1;
-          n = n < a.N ? n : a.N - 8;
-          pre.hb4[it >> 2] |= (unsigned)((const unsigned char*)a.aux)[(long)m * a.ld_aux + (n >> 3)]
-                              << (8 * (it & 3));
-        }
-      }
-    };
     auto tile_loop = [&](auto edge_c) {
       for (int t = 0; t < nkt - 2; ++t, ++T)
         ktile(T, t, m0, n0, true, std::integral_constant<int, 0>{}, std::true_type{}, edge_c);
       ktile(T, nkt - 2, m0, n0, true, std::integral_constant<int, 1>{}, std::true_type{}, edge_c);
       ++T;
-      if constexpr (PRE) preload();
       ktile(T, nkt - 1, m0, n0, !tail_half, std::integral_constant<int, 2>{}, std::false_type{},
             edge_c);
       ++T;
@@ -922,19 +879,21 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
     // slots of K-tiles T-2 (all four, read long ago) and T-1's A-lo / B-lo (read in its phase
     // r1) - not the free pair the epilogue stages through
     int m0n = 0, n0n = 0;
-    if constexpr (PRE) {
-      // consume the preloads here: the compiler's wait for them lands before the burst below
-      if constexpr (EPI == EPI_BF16_RELUMASK)
-        asm volatile("" ::"v"(pre.hb4[0]), "v"(pre.hb4[1]));
-      else
-        asm volatile("" ::"v"(pre.bb[0].x), "v"(pre.bb[1].x), "v"(pre.bb[2].x), "v"(pre.bb[3].x),
-                     "v"(pre.bb[0].w), "v"(pre.bb[1].w), "v"(pre.bb[2].w), "v"(pre.bb[3].w));
-    }
-    if (has_next) {
-      tile_org(s + 1, m0n, n0n);
+    // A/B build NF_G256_BURST_MID: the bf16 epilogues issue the burst after their first 64-row
+    // pass, so that pass's global operands (bias / ReLU bits) do not wait behind it
+#ifdef NF_G256_BURST_MID
+    constexpr bool MID = EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK;
+#else
+    constexpr bool MID = false;
+#endif
+    auto burst = [&]() {
+      if (has_next) {
+        tile_org(s + 1, m0n, n0n);
 #pragma unroll
-      for (int h = 0; h < 6; ++h) issue_to(T + (h >> 2), m0n, n0n, h >> 2, h & 3);
-    }
+        for (int h = 0; h < 6; ++h) issue_to(T + (h >> 2), m0n, n0n, h >> 2, h & 3);
+      }
+    };
+    if constexpr (!MID) burst();
     if (wr == 0) barrier();
     // ---- epilogue of tile s through the free LDS (see above)
     const int fs = (4 * (T - 1) + 2) & (NSLOT - 1);   // free slot pair of the last K-tile
@@ -953,11 +912,11 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
                           },
                           lane_e, tid_e);
     } else if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK) {
-      epi_tile_staged<EPI, 4, false, 0, 8, false, PRE>(a, acc, m0 + wr * 128, n0 + wc * 64, 0,
-                                                       region, lane, &pre);
+      epi_tile_staged<EPI, 4, false, 0, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, 0, region, lane);
+      if constexpr (MID) burst();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own readback done before re-staging
-      epi_tile_staged<EPI, 4, false, 4, 8, false, PRE>(a, acc, m0 + wr * 128 + 64, n0 + wc * 64, 0,
-                                                       region, lane, &pre);
+      epi_tile_staged<EPI, 4, false, 4, 8>(a, acc, m0 + wr * 128 + 64, n0 + wc * 64, 0, region,
+                                           lane);
     } else {
       epi_tile_staged<EPI, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, 0, region, lane_e);
     }

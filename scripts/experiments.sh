@@ -154,48 +154,24 @@ PY
       done
     done
     cat $O/layout.jsonl ;;
-  epi_noload)     # diagnostic: the persistent products without their epilogue operand loads (bias,
-                  # ReLU bits; timing only) vs the default library, per product
-    L=vi_normflows_amd/_native/libvinf_hip_noload.so
+  var_ab)         # a variant library (arg: name) vs default: its GEMM / engine tests, the bf16
+                  # products, and 3 alternating whole-step runs
+    v=$1; P=vi_normflows_amd/_native/libvinf_hip_$v.so
+    VINF_NATIVE_LIB=$P timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py tests/test_gemm_persistent_gpu.py tests/test_realnvp_engine.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_$v.txt 2>&1 || { tail -30 $O/pytest_$v.txt; exit 1; }
+    tail -1 $O/pytest_$v.txt
     for r in 1 2; do
       VINF_BENCH_TAG=default timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,dgrad_l2 >> $O/sg.jsonl || exit 1
-      VINF_NATIVE_LIB=$L VINF_BENCH_TAG=noload timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,dgrad_l2 >> $O/sg.jsonl || exit 1
-      if [ -f vi_normflows_amd/_native/libvinf_hip_pre.so ]; then
-        VINF_NATIVE_LIB=vi_normflows_amd/_native/libvinf_hip_pre.so VINF_BENCH_TAG=preload timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,dgrad_l2 >> $O/sg.jsonl || exit 1
-      fi
+      VINF_NATIVE_LIB=$P VINF_BENCH_TAG=$v timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,dgrad_l2 >> $O/sg.jsonl || exit 1
     done
-    cat $O/sg.jsonl
-    if [ -f vi_normflows_amd/_native/libvinf_hip_pre.so ]; then
-      VINF_NATIVE_LIB=vi_normflows_amd/_native/libvinf_hip_pre.so timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py tests/test_gemm_persistent_gpu.py tests/test_realnvp_engine.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_pre.txt 2>&1 || { tail -30 $O/pytest_pre.txt; exit 1; }
-      tail -1 $O/pytest_pre.txt
-      for r in 1 2; do
-        for lib in default pre; do
-          if [ $lib = default ]; then unset VINF_NATIVE_LIB; else export VINF_NATIVE_LIB=vi_normflows_amd/_native/libvinf_hip_pre.so; fi
-          timeout -k 10 240 python bench.py --steps 20 --warmup 5 > $O/b.json 2> $O/b.err || { tail -20 $O/b.err; exit 1; }
-          python -c "import json;d=json.load(open('$O/b.json'));print(json.dumps({'lib':'$lib','ms':d['ms_per_step'],'F':d['notes']['final_free_energy']}))" >> $O/bench.jsonl
-        done
-      done
-      unset VINF_NATIVE_LIB
-      cat $O/bench.jsonl
-    fi ;;
-  epi_pre)        # NF_EPI_PRELOAD variant vs default: products, correctness, whole step
-    P=vi_normflows_amd/_native/libvinf_hip_pre.so
-    VINF_NATIVE_LIB=$P timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py tests/test_gemm_persistent_gpu.py tests/test_realnvp_engine.py tests/test_bf16_fidelity_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_pre.txt 2>&1 || { tail -30 $O/pytest_pre.txt; exit 1; }
-    tail -1 $O/pytest_pre.txt
-    for r in 1 2; do
-      VINF_BENCH_TAG=default timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,dgrad_l2 >> $O/sg.jsonl || exit 1
-      VINF_NATIVE_LIB=$P VINF_BENCH_TAG=preload timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,dgrad_l2 >> $O/sg.jsonl || exit 1
-    done
-    grep sum $O/sg.jsonl
     for r in 1 2 3; do
-      for lib in default pre; do
+      for lib in default $v; do
         if [ $lib = default ]; then unset VINF_NATIVE_LIB; else export VINF_NATIVE_LIB=$P; fi
         timeout -k 10 240 python bench.py --steps 20 --warmup 5 > $O/b.json 2> $O/b.err || { tail -20 $O/b.err; exit 1; }
         python -c "import json;d=json.load(open('$O/b.json'));print(json.dumps({'lib':'$lib','ms':d['ms_per_step'],'F':d['notes']['final_free_energy']}))" >> $O/bench.jsonl
       done
     done
     unset VINF_NATIVE_LIB
-    cat $O/bench.jsonl ;;
+    grep -v sum $O/sg.jsonl; cat $O/bench.jsonl ;;
   cumask)         # CU-mask stream probe: mask bit -> XCD / SE / CU, and graph replay vs the mask
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/cumask_probe.hip -o $O/cumask_probe &&
     timeout -k 10 120 $O/cumask_probe > $O/cumask.jsonl && tail -3 $O/cumask.jsonl ;;
