@@ -879,21 +879,11 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
     // slots of K-tiles T-2 (all four, read long ago) and T-1's A-lo / B-lo (read in its phase
     // r1) - not the free pair the epilogue stages through
     int m0n = 0, n0n = 0;
-    // A/B build NF_G256_BURST_MID: the bf16 epilogues issue the burst after their first 64-row
-    // pass, so that pass's global operands (bias / ReLU bits) do not wait behind it
-#ifdef NF_G256_BURST_MID
-    constexpr bool MID = EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK;
-#else
-    constexpr bool MID = false;
-#endif
-    auto burst = [&]() {
-      if (has_next) {
-        tile_org(s + 1, m0n, n0n);
+    if (has_next) {
+      tile_org(s + 1, m0n, n0n);
 #pragma unroll
-        for (int h = 0; h < 6; ++h) issue_to(T + (h >> 2), m0n, n0n, h >> 2, h & 3);
-      }
-    };
-    if constexpr (!MID) burst();
+      for (int h = 0; h < 6; ++h) issue_to(T + (h >> 2), m0n, n0n, h >> 2, h & 3);
+    }
     if (wr == 0) barrier();
     // ---- epilogue of tile s through the free LDS (see above)
     const int fs = (4 * (T - 1) + 2) & (NSLOT - 1);   // free slot pair of the last K-tile
@@ -913,7 +903,6 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
                           lane_e, tid_e);
     } else if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK) {
       epi_tile_staged<EPI, 4, false, 0, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, 0, region, lane);
-      if constexpr (MID) burst();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own readback done before re-staging
       epi_tile_staged<EPI, 4, false, 4, 8>(a, acc, m0 + wr * 128 + 64, n0 + wc * 64, 0, region,
                                            lane);
