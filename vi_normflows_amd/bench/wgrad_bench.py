@@ -170,6 +170,47 @@ def layout_probe(B: int, layers: int, iters: int, tag: str, dev, pad: int = 0,
                           "max_rel_diff_vs_layout0": err}), flush=True)
 
 
+def nt_probe(B: int, iters: int, tag: str, dev):
+    """The forward products of the headline step (x [B, K] bf16 times W [N, K]^T, persistent
+    256x256 kernel, bias + ReLU + bitmask or plain) with the activation operand real vs stride-0
+    (every row the same K-vector, so its LDS-DMA stream always hits L2; W is 2 MiB and always
+    does). Same epilogue bytes in both: the difference is what the activation's HBM / MALL
+    fetch costs the main loop."""
+    from ..ops import gemm
+
+    bf = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(0)
+    for K, N, relu in ((1024, 1024, True), (416, 1024, True), (1024, 1024, False)):
+        x = torch.randn(B, K, device=dev, generator=g).to(bf)
+        row = torch.randn(1, K, device=dev, generator=g).to(bf)
+        x0 = row.expand(B, K)
+        W = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(bf)
+        bias = torch.zeros(N, device=dev, dtype=bf)
+        out = torch.empty(B, N, device=dev, dtype=bf)
+        bits = torch.empty(B, N // 8, device=dev, dtype=torch.uint8) if relu else None
+        flops = 2.0 * B * N * K
+        for name, xin in (("a_real", x), ("a_cached", x0)):
+            def fn():
+                gemm.linear_fwd(xin, W, bias, out, relu=relu, mask_out=bits)
+            for _ in range(2):
+                fn()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(iters):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                fn()
+                e.record()
+                e.synchronize()
+                ts.append(s.elapsed_time(e) * 1e3)
+            ts.sort()
+            med = ts[len(ts) // 2]
+            print(json.dumps({"tag": tag, "probe": f"nt_K{K}_N{N}_{'relu' if relu else 'plain'}"
+                              f"_{name}", "us_min": round(ts[0], 1), "us_med": round(med, 1),
+                              "tflops": round(flops / med / 1e6, 1)}), flush=True)
+        del x, out, bits
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536)
@@ -178,6 +219,7 @@ def main(argv=None):
     ap.add_argument("--tag", default=os.environ.get("VINF_BENCH_TAG", ""))
     ap.add_argument("--probe", action="store_true")
     ap.add_argument("--layout-probe", action="store_true")
+    ap.add_argument("--nt-probe", action="store_true")
     ap.add_argument("--pitch-pad", type=int, default=0, help="layout probe: extra row elements")
     ap.add_argument("--layouts", default="0,1,2,3")
     ap.add_argument("--kchunks", type=int, default=1,
@@ -186,6 +228,9 @@ def main(argv=None):
     dev = torch.device("cuda")
     if a.probe:
         probe(a.batch, a.iters, a.tag, dev)
+        return
+    if a.nt_probe:
+        nt_probe(a.batch, a.iters, a.tag, dev)
         return
     if a.layout_probe:
         layout_probe(a.batch, a.layers, a.iters, a.tag, dev, a.pitch_pad,
