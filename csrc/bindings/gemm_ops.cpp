@@ -998,6 +998,8 @@ int64_t gemm_pp(int64_t on) {   // on < 0: query only; returns the previous sett
   if (on >= 0) nf_gemm_pp_set((int)on);
   return prev;
 }
+int nf_gemm_nt4w_set(int on);
+int64_t gemm_nt4w(int64_t on) { return nf_gemm_nt4w_set((int)on); }   // on < 0: query only
 int64_t gemm_cpl_edge(int64_t on) {   // on < 0: query only; returns the previous setting
   const int prev = nf_gemm256_get_cpl_edge();
   if (on >= 0) nf_gemm256_set_cpl_edge((int)on);
@@ -1017,6 +1019,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("gemm_persist(int on) -> int", &gemm_persist);
   m.def("gemm_cpl_edge(int on) -> int", &gemm_cpl_edge);
   m.def("gemm_pp(int on) -> int", &gemm_pp);
+  m.def("gemm_nt4w(int on) -> int", &gemm_nt4w);
   m.def("gemm_grid_reserve(int cus) -> int", &gemm_grid_reserve);
   m.def("gemm_wgrad_xcd_pack(int on) -> int", &gemm_wgrad_xcd_pack);
   m.def("fp8_quant_rows(Tensor x, Tensor(a!) q, Tensor(b!) scale) -> ()");

@@ -37,6 +37,10 @@ static_assert(sizeof(TnMulti) <= 4096, "TnMulti must fit the 4 KiB kernarg segme
 
 }  // namespace g256
 
+// 4-wave NT kernel for the plain bf16 batch-side products (gemm_nt4w.hip, opt-in
+// VINF_GEMM_NT4W=1); false: off or shape not supported (caller runs the 8-wave kernel)
+bool launch_nt4w(GemmArgs a, int epi, hipStream_t stream);
+
 // 4-wave 128x128-per-wave TN kernel (gemm_tn4w.hip); false: shape not supported (caller falls
 // back to gemm256_multi_kernel)
 bool launch_tn4w_multi(const g256::TnMulti& t, hipStream_t stream);

@@ -1072,6 +1072,9 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
     fprintf(stderr, "vinf: ReLU bitmask output needs the staged epilogue (N %% 8, 16-B rows)\n");
     abort();
   }
+  // opt-in 4-wave NT kernel (gemm_nt4w.hip, VINF_GEMM_NT4W=1) for the plain bf16 NT products
+  if constexpr (AK && BK_ && !DB && (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK))
+    if (splits == 1 && launch_nt4w(a, EPI, stream)) return;
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   // pair the column tiles of MADE-masked products (see gemm256_kernel) when that still gives
   // every CU a block; VINF_GEMM_PAIR=0 disables, =2 forces (tests)

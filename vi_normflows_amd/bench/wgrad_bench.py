@@ -171,15 +171,39 @@ def layout_probe(B: int, layers: int, iters: int, tag: str, dev, pad: int = 0,
 
 
 def nt_probe(B: int, iters: int, tag: str, dev):
-    """The forward products of the headline step (x [B, K] bf16 times W [N, K]^T, persistent
-    256x256 kernel, bias + ReLU + bitmask or plain) with the activation operand real vs stride-0
-    (every row the same K-vector, so its LDS-DMA stream always hits L2; W is 2 MiB and always
-    does). Same epilogue bytes in both: the difference is what the activation's HBM / MALL
-    fetch costs the main loop."""
+    """The forward products of the headline step (x [B, K] bf16 times W [N, K]^T, bias + ReLU +
+    bitmask or plain) and the bitmask input gradient (dy [B, 1024] times Wt^T): the 8-wave
+    persistent 256x256 kernel with the activation operand real vs stride-0 (every row the same
+    K-vector, so its LDS-DMA stream always hits L2; W is 2 MiB and always does), and the 4-wave
+    kernel (gemm_nt4w.hip) on the real operands with its outputs checked bitwise against the
+    8-wave ones."""
     from ..ops import gemm
+    from ..ops._ext import native
 
     bf = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
+
+    def timeit(fn):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(iters):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            fn()
+            e.record()
+            e.synchronize()
+            ts.append(s.elapsed_time(e) * 1e3)
+        ts.sort()
+        return ts[0], ts[len(ts) // 2]
+
+    def emit(name, flops, t, extra=None):
+        d = {"tag": tag, "probe": name, "us_min": round(t[0], 1), "us_med": round(t[1], 1),
+             "tflops": round(flops / t[1] / 1e6, 1)}
+        d.update(extra or {})
+        print(json.dumps(d), flush=True)
+
     for K, N, relu in ((1024, 1024, True), (416, 1024, True), (1024, 1024, False)):
         x = torch.randn(B, K, device=dev, generator=g).to(bf)
         row = torch.randn(1, K, device=dev, generator=g).to(bf)
@@ -189,26 +213,43 @@ def nt_probe(B: int, iters: int, tag: str, dev):
         out = torch.empty(B, N, device=dev, dtype=bf)
         bits = torch.empty(B, N // 8, device=dev, dtype=torch.uint8) if relu else None
         flops = 2.0 * B * N * K
-        for name, xin in (("a_real", x), ("a_cached", x0)):
-            def fn():
-                gemm.linear_fwd(xin, W, bias, out, relu=relu, mask_out=bits)
-            for _ in range(2):
-                fn()
-            torch.cuda.synchronize()
-            ts = []
-            for _ in range(iters):
-                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                s.record()
-                fn()
-                e.record()
-                e.synchronize()
-                ts.append(s.elapsed_time(e) * 1e3)
-            ts.sort()
-            med = ts[len(ts) // 2]
-            print(json.dumps({"tag": tag, "probe": f"nt_K{K}_N{N}_{'relu' if relu else 'plain'}"
-                              f"_{name}", "us_min": round(ts[0], 1), "us_med": round(med, 1),
-                              "tflops": round(flops / med / 1e6, 1)}), flush=True)
-        del x, out, bits
+        name = f"nt_K{K}_N{N}_{'relu' if relu else 'plain'}"
+        ref = None
+        for arm, xin, w4 in (("a_real", x, 0), ("a_cached", x0, 0), ("nt4w", x, 1)):
+            prev = native().gemm_nt4w(w4)
+            try:
+                t = timeit(lambda: gemm.linear_fwd(xin, W, bias, out, relu=relu, mask_out=bits))
+                extra = {}
+                if arm == "a_real":
+                    ref = (out.clone(), bits.clone() if bits is not None else None)
+                elif arm == "nt4w":
+                    extra["bitwise_vs_8wave"] = bool(torch.equal(out, ref[0]) and (
+                        bits is None or torch.equal(bits, ref[1])))
+            finally:
+                native().gemm_nt4w(prev)
+            emit(f"{name}_{arm}", flops, t, extra)
+        del x, out, bits, ref
+
+    # bitmask input gradient dh = (dy Wt^T) * 1(bits), K = N = 1024 (NT through Wt)
+    K = N = 1024
+    dy = torch.randn(B, K, device=dev, generator=g).to(bf)
+    W = (torch.randn(K, N, device=dev, generator=g) * K ** -0.5).to(bf)
+    Wt = W.t().contiguous()
+    rb = torch.randint(0, 256, (B, N // 8), device=dev, generator=g, dtype=torch.int32).to(torch.uint8)
+    dh = torch.empty(B, N, device=dev, dtype=bf)
+    ref = None
+    for arm, w4 in (("8wave", 0), ("nt4w", 1)):
+        prev = native().gemm_nt4w(w4)
+        try:
+            t = timeit(lambda: gemm.linear_dgrad(dy, W, dh, relu_bits=rb, Wt=Wt))
+            extra = {}
+            if ref is None:
+                ref = dh.clone()
+            else:
+                extra["bitwise_vs_8wave"] = bool(torch.equal(dh, ref))
+        finally:
+            native().gemm_nt4w(prev)
+        emit(f"dgrad_bits_K{K}_N{N}_{arm}", 2.0 * B * N * K, t, extra)
 
 
 def main(argv=None):
