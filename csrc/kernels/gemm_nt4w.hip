@@ -4,9 +4,10 @@
 //
 // Opt-in A/B of the 4-wave design on the NT products (VINF_GEMM_NT4W=1; gemm256.hip's launch()
 // keeps the 8-wave persistent kernel otherwise). The 4-wave TN kernel (gemm_tn4w.hip) beat the
-// 8-wave schedule by 5 % with cache-resident operands and 25 % on real ones; the NT products'
-// main loop was measured pipeline-bound, not fetch-bound (profiles/r4/nt_probe_a_resident.jsonl),
-// which is the case a different schedule can move.
+// 8-wave schedule by 5 % with cache-resident operands and 25 % on real ones; an L2-resident
+// activation did not speed the NT products up (profiles/r4/nt_probe_a_resident.jsonl), so their
+// schedule was the candidate. Measured slower at the headline shapes (docs/PERF_NOTES.md
+// "A 4-wave NT kernel", profiles/r4/nt4w_probe.jsonl): off by default.
 //
 // Geometry: 256 threads = 4 waves, wave w = (wr, wc) = (w >> 1, w & 1) owns tile rows
 // [128 wr, +128) x cols [128 wc, +128) (256 fp32 accumulators per lane in AGPRs). BK = 64.
