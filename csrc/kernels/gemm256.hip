@@ -166,7 +166,12 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long
     // counted vmcnt + barriers only (RAW / WAR distances in the header comment). Measured
     // (profiles/r4/asmdma_probe.jsonl): NN product 1782 -> 1612 us, TN 2238 -> 2158 us, NT
     // unchanged; -D NF_G256_BUILTIN_DMA restores the builtin for A/B.
+#ifdef NF_G256_STAMPS   // the stamps build's extra code leaves it in a VGPR otherwise
+    const unsigned lds = __builtin_amdgcn_readfirstlane(
+        (unsigned)(unsigned long)(LDS_AS char*)(dst + piece * 1024));
+#else
     const unsigned lds = (unsigned)(unsigned long)(LDS_AS char*)(dst + piece * 1024);
+#endif
     asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
                  :: "v"(src), "s"(lds) : "memory", "m0");
 #else
@@ -925,7 +930,9 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
 template <bool A_KMAJOR, bool B_KMAJOR, int EPI>
 __global__ void __launch_bounds__(NTHR, 1) gemm256_persistent_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[8 * HALF_BYTES + 8 * 4096];
+  NF_STAMP(5);   // stamps build: block start / end (the body ends on vmcnt(0) + barrier)
   gemm256_persistent_body<A_KMAJOR, B_KMAJOR, EPI>(a, smem);
+  NF_STAMP(6);
 }
 
 // Streamed K-tiles of column tile tn under a MADE K-range plan (one or two ranges).

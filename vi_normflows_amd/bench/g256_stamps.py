@@ -92,6 +92,22 @@ def main(argv=None):
         fn()
         torch.cuda.synchronize()
         ops.g256_set_stamps(torch.empty(0, dtype=torch.int64, device=dev))
+        # persistent launches (one block per CU, several tiles each): block start / end in
+        # slots 5 / 6 - how long CUs sit idle while the launch waits for its last block
+        pst = buf[: tiles * 8].view(tiles, 8)[:, 5:7].double().cpu()
+        pok = pst[:, 0] > 0
+        if bool(pok.any()):
+            pu = (pst[pok] - pst[pok][:, 0].min()) / 100.0
+            span = float(pu[:, 1].max())
+            idle = float((pu[:, 1].max() - pu[:, 1]).mean() + pu[:, 0].mean())
+            prec = dict(name=name, persistent_blocks=int(pok.sum()), launch_us=round(span, 2),
+                        start_skew_p90_us=round(float(pu[:, 0].quantile(0.9)), 2),
+                        end_min_us=round(float(pu[:, 1].min()), 2),
+                        end_median_us=round(float(pu[:, 1].median()), 2),
+                        idle_share=round(idle / span, 4))
+            recs.append(prec)
+            print(json.dumps(prec), flush=True)
+            continue
         st_ = buf[: tiles * 8].view(tiles, 8)[:, :5].double().cpu()
         ok = (st_[:, 0] > 0)
         st_ = st_[ok]
