@@ -304,6 +304,18 @@ __device__ __forceinline__ v4u bf_stage_fix(v4u v, bool swapped) {
 // origin of block J0), so a caller short of LDS can stage a sub-tile in several calls.
 // SPLITN (fp32 outputs only): the wave's 64 columns are two 32-column groups, n0 + [0, 32) and
 // n0 + 128 + [0, 32) (contiguous-B-half weight-gradient tiles, gemm256.hip stage_half BCONTIG)
+// max(v, 0) in one VALU op: fmaxf (and fmed3(v, 0, inf), which the compiler folds back into
+// it) compiles to v_max_f32 v, v, v (IEEE-mode NaN canonicalisation) + v_max_f32 v, 0, v
+__device__ __forceinline__ float relu_f(float v) {
+#ifdef NF_RELU_FMAXF   // A/B build: the compiler's form
+  return fmaxf(v, 0.f);
+#else
+  float r;
+  asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(v));
+  return r;
+#endif
+}
+
 template <int EPI, int NJ, bool F8 = false, int J0 = 0, int NJA = NJ, bool SPLITN = false>
 __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&acc)[4][NJA],
                                                 int m0, int n0, int split, char* region,
@@ -359,7 +371,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
         float v1 = fmaf(acc[i][J0 + j][1], smj[j] * sn[i][1], bv[i][1]);
         float v2 = fmaf(acc[i][J0 + j][2], smj[j] * sn[i][2], bv[i][2]);
         float v3 = fmaf(acc[i][J0 + j][3], smj[j] * sn[i][3], bv[i][3]);
-        if (relu) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
+        if (relu) { v0 = relu_f(v0); v1 = relu_f(v1); v2 = relu_f(v2); v3 = relu_f(v3); }
         const unsigned lo = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
         const unsigned hi = (unsigned)f2bf(v2) | ((unsigned)f2bf(v3) << 16);
         const int slot = i * 4 + g;  // 8-B slot of the 128-B row

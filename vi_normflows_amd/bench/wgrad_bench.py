@@ -204,6 +204,18 @@ def nt_probe(B: int, iters: int, tag: str, dev):
         d.update(extra or {})
         print(json.dumps(d), flush=True)
 
+    only = os.environ.get("VINF_NT_PROBE_MASKS")   # "1": the ReLU-mask split only
+    if only:
+        K = N = 1024
+        x = torch.randn(B, K, device=dev, generator=g).to(bf)
+        W = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(bf)
+        bias = torch.zeros(N, device=dev, dtype=bf)
+        out = torch.empty(B, N, device=dev, dtype=bf)
+        bits = torch.empty(B, N // 8, device=dev, dtype=torch.uint8)
+        for arm, relu, m in (("plain", False, None), ("relu", True, None), ("relu_mask", True, bits)):
+            t = timeit(lambda: gemm.linear_fwd(x, W, bias, out, relu=relu, mask_out=m))
+            emit(f"mask_split_K{K}_N{N}_{arm}", 2.0 * B * N * K, t)
+        return
     for K, N, relu in ((1024, 1024, True), (416, 1024, True), (1024, 1024, False)):
         x = torch.randn(B, K, device=dev, generator=g).to(bf)
         row = torch.randn(1, K, device=dev, generator=g).to(bf)
