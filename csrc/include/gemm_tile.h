@@ -228,6 +228,18 @@ __device__ __forceinline__ v8s read_frag_any(const char* lds_tile, int r0, int k
   else return read_frag<KMAJOR>(lds_tile, r0, ks, lane);
 }
 
+// max(v, 0) in one VALU op: fmaxf (and fmed3(v, 0, inf), which the compiler folds back into
+// it) compiles to v_max_f32 v, v, v (IEEE-mode NaN canonicalisation) + v_max_f32 v, 0, v
+__device__ __forceinline__ float relu_f(float v) {
+#ifdef NF_RELU_FMAXF   // A/B build: the compiler's form
+  return fmaxf(v, 0.f);
+#else
+  float r;
+  asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(v));
+  return r;
+#endif
+}
+
 // Epilogue for one accumulator fragment: 4 consecutive n of output row m.
 template <int EPI>
 __device__ __forceinline__ void epi_store(const GemmArgs& a, v4f v, int m, int n, int split) {
@@ -238,7 +250,7 @@ __device__ __forceinline__ void epi_store(const GemmArgs& a, v4f v, int m, int n
     }
     if (a.relu) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      for (int r = 0; r < 4; ++r) v[r] = relu_f(v[r]);
     }
     ushort4 o;
     o.x = f2bf(v[0]); o.y = f2bf(v[1]); o.z = f2bf(v[2]); o.w = f2bf(v[3]);
@@ -304,18 +316,6 @@ __device__ __forceinline__ v4u bf_stage_fix(v4u v, bool swapped) {
 // origin of block J0), so a caller short of LDS can stage a sub-tile in several calls.
 // SPLITN (fp32 outputs only): the wave's 64 columns are two 32-column groups, n0 + [0, 32) and
 // n0 + 128 + [0, 32) (contiguous-B-half weight-gradient tiles, gemm256.hip stage_half BCONTIG)
-// max(v, 0) in one VALU op: fmaxf (and fmed3(v, 0, inf), which the compiler folds back into
-// it) compiles to v_max_f32 v, v, v (IEEE-mode NaN canonicalisation) + v_max_f32 v, 0, v
-__device__ __forceinline__ float relu_f(float v) {
-#ifdef NF_RELU_FMAXF   // A/B build: the compiler's form
-  return fmaxf(v, 0.f);
-#else
-  float r;
-  asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(v));
-  return r;
-#endif
-}
-
 template <int EPI, int NJ, bool F8 = false, int J0 = 0, int NJA = NJ, bool SPLITN = false>
 __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&acc)[4][NJA],
                                                 int m0, int n0, int split, char* region,
