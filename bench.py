@@ -49,7 +49,7 @@ def _args(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     # 65536 MC samples per GPU per step: ~30 GB of the 288 GB HBM; the weight-gradient tiles get
     # K = 65536 and the 289 MB gradient all-reduce is ~1 % of a 40 ms step
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("VINF_BENCH_BATCH", 65536)),
+    ap.add_argument("--batch", type=int, default=65536,
                     help="per-GPU ELBO samples per step")
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--dim", type=int, default=784)

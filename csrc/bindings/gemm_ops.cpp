@@ -73,6 +73,56 @@ void gemm_nt(const at::Tensor& x, const at::Tensor& W, const c10::optional<at::T
                     (int)relu, cur_stream(), mp, ldm);
 }
 
+// y = x W^T: x [M,K], W [N,K] bf16, y [M,N] fp32 (the accumulator, unrounded)
+void gemm_nt_f32out(const at::Tensor& x, const at::Tensor& W, const at::Tensor& y) {
+  chk_mat(x, "x", at::kBFloat16);
+  chk_mat(W, "W", at::kBFloat16);
+  chk_mat(y, "y", at::kFloat);
+  const int M = x.size(0), K = x.size(1), N = W.size(0);
+  TORCH_CHECK(W.size(1) == K, "W inner dim");
+  TORCH_CHECK(y.size(0) == M && y.size(1) == N, "y shape");
+  TORCH_CHECK(K % 32 == 0 && K > 0, "K must be a positive multiple of 32 (pad the operands)");
+  TORCH_CHECK(N % 8 == 0, "N must be a multiple of 8");
+  nf_launch_gemm_nt_f32out(x.data_ptr(), ld2(x), W.data_ptr(), ld2(W), y.data_ptr<float>(), ld2(y),
+                           M, N, K, cur_stream());
+}
+
+// Exact fp32 / fp64 product C (+)= Aop Bop^T (+ bias), dbias = row sums of Aop (gemm_fp.hip).
+// A: [M,K] (a_kmajor) or [K,M]; B: [N,K] (b_kmajor) or [K,N]; C [M,N]; bias [N]; dbias [M]; one
+// dtype (fp32 or fp64) throughout, unit inner strides, any shape.
+void gemm_fp(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kmajor,
+             const c10::optional<at::Tensor>& bias, const at::Tensor& C, bool accumulate,
+             const c10::optional<at::Tensor>& dbias) {
+  const auto dt = C.scalar_type();
+  TORCH_CHECK(dt == at::kFloat || dt == at::kDouble, "gemm_fp: fp32 or fp64 output");
+  auto chk = [&](const at::Tensor& t, const char* n) {
+    TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.scalar_type() == dt, n,
+                " must be a 2-D GPU tensor of the output's dtype");
+    TORCH_CHECK(t.size(1) <= 1 || t.stride(1) == 1, n, " needs unit inner stride");
+  };
+  chk(A, "A"); chk(B, "B"); chk(C, "C");
+  const int M = C.size(0), N = C.size(1);
+  const int K = a_kmajor ? A.size(1) : A.size(0);
+  TORCH_CHECK((a_kmajor ? A.size(0) : A.size(1)) == M, "A rows must match C rows");
+  TORCH_CHECK((b_kmajor ? B.size(0) : B.size(1)) == N, "B rows must match C cols");
+  TORCH_CHECK((b_kmajor ? B.size(1) : B.size(0)) == K, "A / B inner dims differ");
+  const void* bp = nullptr;
+  if (bias && bias->defined()) {
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == dt && bias->is_contiguous() &&
+                    bias->numel() == N, "bias: contiguous [N] of the output's dtype");
+    bp = bias->data_ptr();
+  }
+  void* dbp = nullptr;
+  if (dbias && dbias->defined()) {
+    TORCH_CHECK(dbias->is_cuda() && dbias->scalar_type() == dt && dbias->is_contiguous() &&
+                    dbias->numel() == M, "dbias: contiguous [M] of the output's dtype");
+    dbp = dbias->data_ptr();
+  }
+  auto ld = [](const at::Tensor& t) { return t.size(0) <= 1 ? t.size(1) : t.stride(0); };
+  nf_launch_gemm_fp(dt == at::kDouble, A.data_ptr(), ld(A), a_kmajor, B.data_ptr(), ld(B),
+                    b_kmajor, bp, C.data_ptr(), ld(C), dbp, M, N, K, accumulate, cur_stream());
+}
+
 // dx = dy W  [* 1(h > 0)]: dy [M,K], W [K,N] bf16; dx bf16 (mask) or fp32 (+= when accumulate)
 void gemm_nn(const at::Tensor& dy, const at::Tensor& W, const c10::optional<at::Tensor>& h,
              const at::Tensor& dx, bool accumulate, const c10::optional<at::Tensor>& hbits,
@@ -221,7 +271,7 @@ static void gemm_tn_multi_impl(at::TensorList dy, at::TensorList x, at::TensorLi
                                const at::Tensor* f8_scales, at::IntArrayRef sa_idx,
                                at::IntArrayRef sb_idx, int layout = 0) {
   const size_t n = dy.size();
-  TORCH_CHECK(layout >= 0 && layout <= 3 && (layout == 0 || !f8_scales), "layout 0..3, bf16");
+  TORCH_CHECK(layout >= 0 && layout <= 4 && (layout == 0 || !f8_scales), "layout 0..4, bf16");
   const bool f8 = f8_scales != nullptr;
   const auto odt = f8 ? at::kFloat8_e4m3fn : at::kBFloat16;
   if (f8) {
@@ -982,7 +1032,8 @@ void gemm_fp8_nt(const at::Tensor& xq, const at::Tensor& sx, const at::Tensor& w
                         qp, ldq, qap, qs, qac, cur_stream());
 }
 
-void gemm_set_mode(int64_t mode, int64_t depth) { nf_gemm_set_mode((int)mode, (int)depth); }
+int64_t gemm_set_mode(int64_t mode) { return nf_gemm_set_mode((int)mode); }   // < 0: query
+int64_t gemm_pair(int64_t mode) { return nf_gemm256_set_pair((int)mode); }   // < 0: query
 int nf_gemm256_xcd_pack(int on);
 int64_t gemm_wgrad_xcd_pack(int64_t on) { return nf_gemm256_xcd_pack((int)on); }
 int64_t gemm_persist(int64_t on) {   // on < 0: query only; returns the previous setting
@@ -993,19 +1044,6 @@ int64_t gemm_persist(int64_t on) {   // on < 0: query only; returns the previous
 int64_t gemm_grid_reserve(int64_t cus) {   // cus < 0: query only; returns the previous value
   return nf_gemm256_set_reserve((int)cus);
 }
-int64_t gemm_pp(int64_t on) {   // on < 0: query only; returns the previous setting
-  const int prev = nf_gemm_pp_enabled();
-  if (on >= 0) nf_gemm_pp_set((int)on);
-  return prev;
-}
-int nf_gemm_nt4w_set(int on);
-int64_t gemm_nt4w(int64_t on) { return nf_gemm_nt4w_set((int)on); }   // on < 0: query only
-int64_t gemm_cpl_edge(int64_t on) {   // on < 0: query only; returns the previous setting
-  const int prev = nf_gemm256_get_cpl_edge();
-  if (on >= 0) nf_gemm256_set_cpl_edge((int)on);
-  return prev;
-}
-
 #ifdef NF_G256_STAMPS
 void nf_g256_set_stamps(void* p);
 void g256_set_stamps(const at::Tensor& buf) { nf_g256_set_stamps(buf.numel() ? buf.data_ptr() : nullptr); }
@@ -1015,11 +1053,9 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
 #ifdef NF_G256_STAMPS
   m.def("g256_set_stamps(Tensor buf) -> ()", &g256_set_stamps);
 #endif
-  m.def("gemm_set_mode(int mode, int depth) -> ()", &gemm_set_mode);
+  m.def("gemm_set_mode(int mode) -> int", &gemm_set_mode);
+  m.def("gemm_pair(int mode) -> int", &gemm_pair);
   m.def("gemm_persist(int on) -> int", &gemm_persist);
-  m.def("gemm_cpl_edge(int on) -> int", &gemm_cpl_edge);
-  m.def("gemm_pp(int on) -> int", &gemm_pp);
-  m.def("gemm_nt4w(int on) -> int", &gemm_nt4w);
   m.def("gemm_grid_reserve(int cus) -> int", &gemm_grid_reserve);
   m.def("gemm_wgrad_xcd_pack(int on) -> int", &gemm_wgrad_xcd_pack);
   m.def("fp8_quant_rows(Tensor x, Tensor(a!) q, Tensor(b!) scale) -> ()");
@@ -1029,6 +1065,8 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("masked_gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, Tensor krange, bool accumulate=False, Tensor? krange256=None, Tensor? Wt=None) -> ()");
   m.def("masked_gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db, Tensor skip) -> ()");
   m.def("gemm_nt(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, int relu, Tensor(b!)? mask=None) -> ()");
+  m.def("gemm_nt_f32out(Tensor x, Tensor W, Tensor(a!) y) -> ()");
+  m.def("gemm_fp(Tensor A, bool a_kmajor, Tensor B, bool b_kmajor, Tensor? bias, Tensor(a!) C, bool accumulate, Tensor(b!)? dbias=None) -> ()");
   m.def("gemm_nn(Tensor dy, Tensor W, Tensor? h, Tensor(a!) dx, bool accumulate, Tensor? hbits=None, Tensor? Wt=None) -> ()");
   m.def("transpose_bf16_batched(Tensor desc, int n, int tiles) -> ()");
   m.def("gemm_tn(Tensor dy, Tensor x, Tensor(a!) dW, Tensor(b!)? db) -> ()");
@@ -1055,6 +1093,8 @@ TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
   m.impl("masked_gemm_nn", &masked_gemm_nn);
   m.impl("masked_gemm_tn", &masked_gemm_tn);
   m.impl("gemm_nt", &gemm_nt);
+  m.impl("gemm_nt_f32out", &gemm_nt_f32out);
+  m.impl("gemm_fp", &gemm_fp);
   m.impl("gemm_nn", &gemm_nn);
   m.impl("transpose_bf16_batched", &transpose_bf16_batched);
   m.impl("gemm_tn", &gemm_tn);

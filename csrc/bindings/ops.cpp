@@ -298,24 +298,6 @@ void sumsq_guard(const at::Tensor& x, const at::Tensor& partial,
 
 void cu_hold(int64_t blocks, double usec) { nf_launch_cu_hold((int)blocks, (float)usec, cur_stream()); }
 
-// A HIP stream restricted to a CU set (hipExtStreamCreateWithCUMask): bits [first, first + n) of
-// the device's CU mask (measured on MI355X, tools/cumask_probe.hip: the first 128 bits select 128
-// CUs spread over all 8 XCDs; graphs replayed on the masked stream keep the mask). Returns the
-// raw stream handle for torch.cuda.ExternalStream; the stream lives as long as the process.
-int64_t cu_masked_stream(int64_t first, int64_t n) {
-  int dev = 0, ncu = 0;
-  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
-  TORCH_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess,
-              "CU count");
-  TORCH_CHECK(first >= 0 && n > 0 && first + n <= ncu, "CU range outside the device's ", ncu, " CUs");
-  std::vector<uint32_t> m((ncu + 31) / 32, 0u);
-  for (int64_t b = first; b < first + n; ++b) m[b / 32] |= 1u << (b % 32);
-  hipStream_t s = nullptr;
-  TORCH_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)m.size(), m.data()) == hipSuccess,
-              "hipExtStreamCreateWithCUMask failed");
-  return reinterpret_cast<int64_t>(s);
-}
-
 TORCH_LIBRARY(vinf, m) {
   m.def("coupling_fwd(Tensor st, Tensor x, Tensor(a!) y, Tensor(b!)? ybf, Tensor(c!)? ssav, "
         "Tensor(d!) ldj, float scale, bool inverse, bool ldj_init) -> ()");
@@ -337,7 +319,6 @@ TORCH_LIBRARY(vinf, m) {
         "Tensor(d!)? pbf, float lr, float b1, float b2, float eps, float wd, Tensor? step, "
         "float step_host, Tensor? gscale, float gscale_host, Tensor? skip, float warmup=0.0) -> ()");
   m.def("cu_hold(int blocks, float usec) -> ()", &cu_hold);
-  m.def("cu_masked_stream(int first, int n) -> int", &cu_masked_stream);
   m.def("sumsq_guard(Tensor x, Tensor(a!) partial, Tensor(b!)? out_sumsq, Tensor(c!)? skip, "
         "Tensor(d!)? scale, float max_norm, float base_scale) -> ()");
 }

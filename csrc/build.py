@@ -26,7 +26,7 @@ CSRC = ROOT / "csrc"
 OUT_DIR = ROOT / "vi_normflows_amd" / "_native"
 OUT_LIB = OUT_DIR / "libvinf_hip.so"
 OBJ_DIR = ROOT / "build" / "obj"
-ARCH = os.environ.get("VINF_OFFLOAD_ARCH", "gfx950")
+ARCH = "gfx950"   # MI355X (CDNA4) only
 
 
 def _hipcc() -> str:

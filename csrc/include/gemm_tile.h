@@ -117,23 +117,11 @@ struct GemmArgs {
   // ldj share is -sum alpha, C = s_raw; with f8_cq also the e4m3 copy of u (delayed scale)
   int cf_pair;
   int cf_mode;
-  int desync;                  // persistent gemm256: s_sleep(127) rounds the delayed blocks wait up front
-  int desync_bit;              // block b is delayed iff (b >> desync_bit) & 1 (0: parity = XCD parity)
-  int no_rot;                  // persistent gemm256: keep each block on one column (A/B knob)
-  int no_edge;                 // persistent EPI_CPL_FWD: run edge tiles as full tiles (A/B knob)
 };
 
-// LDS-staged epilogue switch (VINF_GEMM_STAGED_EPI=0 restores the fragment-layout stores) and
-// the alignment its 16-B row accesses need (host side).
-inline bool staged_enabled() {
-  static const int v = [] {
-    const char* e = getenv("VINF_GEMM_STAGED_EPI");
-    return e ? atoi(e) != 0 : 1;
-  }();
-  return v != 0;
-}
+// The alignment the LDS-staged epilogue's 16-B row accesses need (host side); shapes that miss
+// it take the fragment-layout stores.
 inline bool staged_ok(const GemmArgs& a, int epi) {
-  if (!staged_enabled() && !a.mask_out) return false;
   auto al = [](const void* p) { return ((unsigned long)p & 15) == 0; };
   if (epi == EPI_BF16 || epi == EPI_BF16_RELUMASK) {
     if (a.N % 8 || a.ldc % 8 || !al(a.C)) return false;
@@ -230,14 +218,11 @@ __device__ __forceinline__ v8s read_frag_any(const char* lds_tile, int r0, int k
 
 // max(v, 0) in one VALU op: fmaxf (and fmed3(v, 0, inf), which the compiler folds back into
 // it) compiles to v_max_f32 v, v, v (IEEE-mode NaN canonicalisation) + v_max_f32 v, 0, v
+// (profiles/r4/relu_asm_step_ab.jsonl: -0.1 to -0.45 ms per headline step)
 __device__ __forceinline__ float relu_f(float v) {
-#ifdef NF_RELU_FMAXF   // A/B build: the compiler's form
-  return fmaxf(v, 0.f);
-#else
   float r;
   asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(v));
   return r;
-#endif
 }
 
 // Epilogue for one accumulator fragment: 4 consecutive n of output row m.
@@ -314,9 +299,7 @@ __device__ __forceinline__ v4u bf_stage_fix(v4u v, bool swapped) {
 // ldc % 4 == 0 (fp32) and a 16-B aligned C (checked by the launchers).
 // J0 / NJA: the rows handled are accumulator blocks [J0, J0 + NJ) of a [4][NJA] array (m0 is the
 // origin of block J0), so a caller short of LDS can stage a sub-tile in several calls.
-// SPLITN (fp32 outputs only): the wave's 64 columns are two 32-column groups, n0 + [0, 32) and
-// n0 + 128 + [0, 32) (contiguous-B-half weight-gradient tiles, gemm256.hip stage_half BCONTIG)
-template <int EPI, int NJ, bool F8 = false, int J0 = 0, int NJA = NJ, bool SPLITN = false>
+template <int EPI, int NJ, bool F8 = false, int J0 = 0, int NJA = NJ>
 __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&acc)[4][NJA],
                                                 int m0, int n0, int split, char* region,
                                                 int lane) {
@@ -421,13 +404,6 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
         uint4 o = make_uint4(v[0], v[1], v[2], v[3]);
         if constexpr (EPI == EPI_BF16_RELUMASK) {
           // keep element e iff aux_e > 0 (bf16: sign clear and not +0), per 16-bit half
-#ifdef NF_MASK_OLD   // A/B build: per-half compares and selects
-          auto keep = [](unsigned hw) {
-            const unsigned lo = (hw & 0xffffu) != 0 && !(hw & 0x8000u) ? 0xffffu : 0u;
-            const unsigned hi = (hw >> 16) != 0 && !(hw & 0x80000000u) ? 0xffff0000u : 0u;
-            return lo | hi;
-          };
-#else
           // branch-free, both halves at once: bit 15 / 31 of p is set iff that bf16 half is in
           // [1, 0x7fff] (> 0; see the bitmask epilogue below), and (p << 1) - (p >> 15)
           // widens each marked bit to its whole half (mod 2^32: bit 31's shifted-out carry is
@@ -436,7 +412,6 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
             const unsigned p = ((hw & 0x7fff7fffu) + 0x7fff7fffu) & ~hw & 0x80008000u;
             return (p << 1) - (p >> 15);
           };
-#endif
           if (a.aux_bits) {
             const unsigned b = hb[it];
             auto kb = [b](int e) {
@@ -449,25 +424,13 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
           }
         }
         if (EPI == EPI_BF16 && a.mask_out) {  // 1(y > 0) of the stored bf16, 8 bits per lane
-#ifdef NF_MASK_OLD   // A/B build: per-half compares and selects
-          auto pos2 = [](unsigned w) {
-            return (((w & 0xffffu) != 0 && !(w & 0x8000u)) ? 1u : 0u) |
-                   (((w >> 16) != 0 && !(w & 0x80000000u)) ? 2u : 0u);
-          };
-          const unsigned bits = pos2(o.x) | (pos2(o.y) << 2) | (pos2(o.z) << 4) | (pos2(o.w) << 6);
-#else
           // branch-free: half h > 0 (bf16) <=> h in [1, 0x7fff] <=> bit 15 of
           // ((h & 0x7fff) + 0x7fff) & ~h; both halves at once (no carry: each sum <= 0xfffe),
           // then bits 15 / 31 of the 4 words gathered to bits 2e / 2e + 1 of one byte
           auto pos = [](unsigned w) { return ((w & 0x7fff7fffu) + 0x7fff7fffu) & ~w & 0x80008000u; };
           const unsigned t = (pos(o.x) >> 15) | (pos(o.y) >> 13) | (pos(o.z) >> 11) | (pos(o.w) >> 9);
           const unsigned bits = (t | (t >> 15)) & 0xffu;
-#endif
-#ifdef NF_MASK_NOSTORE   // diagnostic build: the bits are computed but not stored
-          asm volatile("" ::"v"(bits));
-#else
           a.mask_out[(long)m * a.ld_mask + (n >> 3)] = (unsigned char)bits;
-#endif
         }
         // (C may be null on the e4m3 paths that only need the e4m3 copy: MAF engine, e4m3
         // weight gradients)
@@ -543,7 +506,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
       if constexpr (EPI == EPI_F32_ACC || CPLB) {
 #pragma unroll
         for (int it = 0; it < PIT; ++it) {
-          int m = m0 + hj * 16 * PJ + it * 4 + (lane >> 4), n = n0 + q * 4 + (SPLITN && q >= 8 ? 96 : 0);
+          int m = m0 + hj * 16 * PJ + it * 4 + (lane >> 4), n = n0 + q * 4;
           m = m < a.M ? m : a.M - 1;
           n = n < a.N ? n : a.N - 4;
           if constexpr (XB) {
@@ -587,7 +550,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
         if constexpr (F8 && EPI == EPI_F32) {
           v[0] *= w8; v[1] *= w8; v[2] *= w8; v[3] *= w8;
         }
-        const int m = m0 + hj * 16 * PJ + row, n = n0 + q * 4 + (SPLITN && q >= 8 ? 96 : 0);
+        const int m = m0 + hj * 16 * PJ + row, n = n0 + q * 4;
         if (m < a.M && n < a.N) {
           if constexpr (CPLB) {
             const float4 o = cv[it];

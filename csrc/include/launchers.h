@@ -62,6 +62,14 @@ void nf_launch_gemm_nt(const void* x, long ldx, const void* W, long ldw, const v
 void nf_launch_gemm_nn(const void* dy, long lddy, const void* W, long ldw, const void* aux,
                        long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
                        int N, int K, hipStream_t stream, int aux_is_bits = 0);
+// y[M][N] = x W^T with bf16 operands and an fp32 output (no rounding of the accumulator)
+void nf_launch_gemm_nt_f32out(const void* x, long ldx, const void* W, long ldw, float* y, long ldy,
+                              int M, int N, int K, hipStream_t stream);
+// gemm_fp.hip: exact fp32 / fp64 GEMM on the f32 / f64 MFMA, C (+)= Aop Bop^T (+ bias),
+// dbias = row sums of Aop (see the kernel header for the operand layouts)
+void nf_launch_gemm_fp(int is_f64, const void* A, long lda, int a_kmajor, const void* B, long ldb,
+                       int b_kmajor, const void* bias, void* C, long ldc, void* dbias, int M, int N,
+                       int K, int accumulate, hipStream_t stream);
 void nf_launch_gemm_tn(const void* dy, long lddy, const void* x, long ldx, float* dW, long lddw,
                        float* db, int M, int N, int K, int splits, float* work,
                        hipStream_t stream);
@@ -95,17 +103,10 @@ void nf_launch_gemm256_nn(const void* dy, long lddy, const void* W, long ldw, co
                           long ld_aux, void* dx, long lddx, int dx_is_f32, int accumulate, int M,
                           int N, int K, hipStream_t stream, int aux_is_bits = 0,
                           const int* krange = nullptr, int krange_segs = 1, int w_kmajor = 0);
-void nf_gemm256_set_depth(int d);
 void nf_gemm256_set_persist(int on);
 int nf_gemm256_get_persist();
 int nf_gemm256_set_reserve(int cus);   // cus < 0: query; returns the previous value
-void nf_gemm256_set_cpl_edge(int on);
-int nf_launch_gemm_pp_nt(const void* x, long ldx, const void* W, long ldw, const void* bias,
-                         void* y, long ldy, int M, int N, int K, int relu, void* mask_out,
-                         long ld_mask, hipStream_t stream);
-int nf_gemm_pp_enabled();
-void nf_gemm_pp_set(int mask);
-int nf_gemm256_get_cpl_edge();
+int nf_gemm256_set_pair(int mode);     // MADE tile pairing 0 off / 1 auto / 2 always; < 0: query
 // input gradient with W given transposed (Wt [N][K]): NT instantiation, bf16 (ReLU-mask) epilogue
 void nf_launch_gemm256_nt_dgrad(const void* dy, long lddy, const void* Wt, long ldwt,
                                 const void* aux, long ld_aux, int aux_is_bits, void* dx,
@@ -164,7 +165,7 @@ void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int
 // layout: 0 = dy [K][M], x [K][N] (batch-major, TN); 1 = x given transposed [N][K] (k-major);
 // 2 = dy given transposed [M][K] - the operand-layout A/B (bench/wgrad_bench.py --probe)
 // mode: 0 auto, 1 force 128x128, 2 force 256x256; depth: half-tiles in flight (3 or 4)
-void nf_gemm_set_mode(int mode, int depth);
+int nf_gemm_set_mode(int mode);
 // fp8.hip (OCP e4m3): per-row quantisation and the MX-scaled K=128 MFMA GEMM
 void nf_launch_fp8_quant_rows(const void* x, int x_is_bf16, long ldx, int R, int C, void* q,
                               long ldq, int Cq, float* scale, hipStream_t stream);
@@ -183,7 +184,7 @@ void nf_launch_gemm_fp8_nt(const void* xq, long ldx, const float* sx, int sx_per
                            void* yq, long ldyq, const float* q_amax_prev, float* q_scale_out,
                            float* q_amax_cur, hipStream_t stream);
 int nf_gemm_tn_splits(int M, int N, int K);
-// the 256x256 kernels' auto rule (a tile per CU, K >= 256; VINF_GEMM_TILE / gemm_set_mode)
+// the 256x256 kernels' auto rule (a tile per CU, K >= 256; gemm_set_mode)
 bool nf_gemm_prefer_256(int M, int N, int K);
 // gemm256.hip F8 instantiation: same contract as nf_launch_gemm_fp8_nt on 256x256 tiles
 // (krange per 256-column tile)

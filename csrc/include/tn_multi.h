@@ -27,7 +27,7 @@ constexpr int TN_PERM_MAX = 256;   // + 512 B: 3724 B of kernarg with 40 descrip
 struct TnMulti {
   TnDesc d[TN_MULTI_MAX];
   int n, tile0, ntiles, use_perm;
-  // XCD packing (VINF_WGRAD_XCD_PACK): block position -> tile offset. Positions
+  // XCD packing (gemm_wgrad_xcd_pack): block position -> tile offset. Positions
   // [x * ntiles/8, (x+1) * ntiles/8) run on XCD x (xcd_remap), so the permutation keeps each
   // problem's tiles - which share A / B panels - inside one XCD's L2 where they fit
   unsigned short perm[TN_PERM_MAX];
@@ -37,9 +37,6 @@ static_assert(sizeof(TnMulti) <= 4096, "TnMulti must fit the 4 KiB kernarg segme
 
 }  // namespace g256
 
-// 4-wave NT kernel for the plain bf16 batch-side products (gemm_nt4w.hip, opt-in
-// VINF_GEMM_NT4W=1); false: off or shape not supported (caller runs the 8-wave kernel)
-bool launch_nt4w(GemmArgs a, int epi, hipStream_t stream);
 
 // 4-wave 128x128-per-wave TN kernel (gemm_tn4w.hip); false: shape not supported (caller falls
 // back to gemm256_multi_kernel)

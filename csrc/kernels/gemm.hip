@@ -371,22 +371,18 @@ static int device_cus() {
   return cus;
 }
 
-// Kernel choice: 0 auto, 1 the 128x128 kernel here, 2 the 256x256 8-phase kernel (gemm256.hip)
-// for the M = batch products (forward / input-gradient), 3 also for the split-K weight
-// gradients. VINF_GEMM_TILE=128|256|257 selects 1|2|3.
-static int g_tile_mode = -1;
+// Kernel choice (nf_gemm_set_mode): 0 auto, 1 the 128x128 kernel here, 2 the 256x256 8-phase
+// kernel (gemm256.hip) for the M = batch products (forward / input-gradient), 3 also for the
+// split-K weight gradients.
+static int g_tile_mode = 0;
 
-void nf_gemm_set_mode(int mode, int depth) {
-  g_tile_mode = mode;
-  nf_gemm256_set_depth(depth);
+int nf_gemm_set_mode(int mode) {   // mode < 0: query; returns the previous mode
+  const int prev = g_tile_mode;
+  if (mode >= 0) g_tile_mode = mode > 3 ? 3 : mode;
+  return prev;
 }
 
 static bool use_256(int M, int N, int K) {
-  if (g_tile_mode < 0) {
-    g_tile_mode = 0;
-    if (const char* e = getenv("VINF_GEMM_TILE"))
-      g_tile_mode = atoi(e) == 256 ? 2 : (atoi(e) == 128 ? 1 : (atoi(e) == 257 ? 3 : 0));
-  }
   if (g_tile_mode == 1) return false;
   if (g_tile_mode >= 2) return true;
   // auto: enough 256x256 tiles to cover every CU once
@@ -396,10 +392,7 @@ static bool use_256(int M, int N, int K) {
 
 bool nf_gemm_prefer_256(int M, int N, int K) { return use_256(M, N, K); }
 
-static bool use_256_tn() {
-  if (g_tile_mode < 0) use_256(1, 1, 1);  // resolve the env default
-  return g_tile_mode == 3;
-}
+static bool use_256_tn() { return g_tile_mode == 3; }
 
 // y[M][N] = act(x[M][K] W[N][K]^T + bias)   -> bf16
 void nf_launch_gemm_nt(const void* x, long ldx, const void* W, long ldw, const void* bias, void* y,
@@ -407,9 +400,6 @@ void nf_launch_gemm_nt(const void* x, long ldx, const void* W, long ldw, const v
                        void* mask_out, long ld_mask) {
   if (M <= 0 || N <= 0) return;
   if (use_256(M, N, K)) {
-    if ((nf_gemm_pp_enabled() & 1) &&
-        nf_launch_gemm_pp_nt(x, ldx, W, ldw, bias, y, ldy, M, N, K, relu, mask_out, ld_mask, stream))
-      return;
     nf_launch_gemm256_nt(x, ldx, W, ldw, bias, y, ldy, M, N, K, relu, stream, mask_out, ld_mask);
     return;
   }
@@ -421,6 +411,19 @@ void nf_launch_gemm_nt(const void* x, long ldx, const void* W, long ldw, const v
   a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + BK - 1) / BK) * BK; a.relu = relu;
   a.mask_out = (unsigned char*)mask_out; a.ld_mask = ld_mask;
   launch<true, true, EPI_BF16>(a, 1, stream);
+}
+
+// y[M][N] = x[M][K] W[N][K]^T -> fp32 (the module layers' bf16 precision path: bf16 operands,
+// the fp32 accumulator stored as is)
+void nf_launch_gemm_nt_f32out(const void* x, long ldx, const void* W, long ldw, float* y, long ldy,
+                              int M, int N, int K, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  GemmArgs a{};
+  a.A = (const bf16_t*)x; a.lda = ldx;
+  a.B = (const bf16_t*)W; a.ldb = ldw;
+  a.C = y; a.ldc = ldy;
+  a.M = M; a.N = N; a.K = K; a.k_per_split = ((K + BK - 1) / BK) * BK;
+  launch<true, true, EPI_F32>(a, 1, stream);
 }
 
 // dx[M][N] = dy[M][K] W[K][N]  (* 1(aux>0) -> bf16)  or  (fp32 dx (+)= ...)
@@ -465,8 +468,7 @@ int nf_gemm_tn_splits(int M, int N, int K) {
     return sp < 1 ? 1 : sp;
   }
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  int target = 2 * device_cus();
-  if (const char* e = getenv("VINF_TN_TARGET_BLOCKS")) target = atoi(e);
+  const int target = 2 * device_cus();
   int splits = target / tiles;
   const int nkt = (K + BK - 1) / BK;
   if (splits > nkt / 4) splits = nkt / 4;
@@ -629,10 +631,8 @@ static int tn_group_splits(int nprob, const NfTnProblem* pr) {
     const int c = ((pr[p].K + BK - 1) / BK) / 4;
     cap = c < cap ? c : cap;
   }
-  int target = (t256 ? 1 : 2) * device_cus();
-  if (const char* e = getenv("VINF_TN_TARGET_BLOCKS")) target = atoi(e);
+  const int target = (t256 ? 1 : 2) * device_cus();
   int S = (int)(target / (tiles > 0 ? tiles : 1));
-  if (const char* e = getenv("VINF_TN_GROUP_SPLITS")) S = atoi(e);   // experiments
   if (S > cap) S = cap;
   return S < 1 ? 1 : S;
 }

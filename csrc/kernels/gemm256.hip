@@ -113,12 +113,7 @@ __device__ __forceinline__ v8i cat16(v8s lo, v8s hi) {
 // 128 bytes either way (64 bf16 or 128 e4m3 k-values per row).
 // pair_dh > 0 (EPI_CPL_FWD, B operand): tile row c < 128 -> weight row row0/2 + c, c >= 128 ->
 // pair_dh + row0/2 + c - 128 (the s_hat and t rows of the same 128 features)
-// BCONTIG (mn-major B of the weight-gradient products): B-lo / B-hi are the tile's column
-// halves [0, 128) / [128, 256) instead of {wc*64 + 0..31} / {wc*64 + 32..63}, so every k-row
-// of a half is 256 contiguous bytes - whole 128-B lines - where the split halves fetched each
-// line in two 64-B pieces at different times. Wave wc then owns tile columns
-// {wc*32 + 0..31} (N0-1) and {128 + wc*32 + 0..31} (N2-3); the epilogue maps them back.
-template <bool KMAJOR, int EB = 2, bool BCONTIG = false>
+template <bool KMAJOR, int EB = 2>
 __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long ld, int row0,
                                            int rows_total, int k0, int K, bool is_a, bool hi,
                                            char* dst, int wave, int lane, int pair_dh = 0) {
@@ -153,11 +148,10 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long
       const int lc = (lane & 15) ^ mn_swz(kr);
       int gk = k0 + kr;
       gk = gk < K ? gk : K - 1;
-      int gm = row0 + ((BCONTIG && !is_a) ? lc * 8 + (hi ? 128 : 0) : half_row(is_a, hi, lc * 8));
+      int gm = row0 + half_row(is_a, hi, lc * 8);
       gm = gm < rows_total ? gm : rows_total - 8;
       src = base + (long)gk * ld + gm;
     }
-#ifndef NF_G256_BUILTIN_DMA
     // The DMA in asm, invisible to the compiler's wait-count pass. With the builtin it drains
     // the DMA queue (s_waitcnt vmcnt(0)) before every ds_read_b64_tr_b16 / _tr_b8 of the
     // mn-major operands (12 such drains in the weight-gradient kernel, none before the k-major
@@ -165,7 +159,7 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long
     // counted vmcnt ring degenerates to one phase of prefetch. Ordering is the schedule's own
     // counted vmcnt + barriers only (RAW / WAR distances in the header comment). Measured
     // (profiles/r4/asmdma_probe.jsonl): NN product 1782 -> 1612 us, TN 2238 -> 2158 us, NT
-    // unchanged; -D NF_G256_BUILTIN_DMA restores the builtin for A/B.
+    // unchanged.
 #ifdef NF_G256_STAMPS   // the stamps build's extra code leaves it in a VGPR otherwise
     const unsigned lds = __builtin_amdgcn_readfirstlane(
         (unsigned)(unsigned long)(LDS_AS char*)(dst + piece * 1024));
@@ -174,10 +168,6 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ base, long
 #endif
     asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
                  :: "v"(src), "s"(lds) : "memory", "m0");
-#else
-    __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(dst + piece * 1024), 16, 0,
-                                     0);
-#endif
   }
 }
 
@@ -234,11 +224,7 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
   // bias (and e4m3 dequantisation scale) of the 4 columns of fragment i. AT_USE: read where
   // they are used (cached; 32 more live registers across the parking loop spilled the e4m3 and
   // one-pass builds); otherwise (the persistent bf16 form) read once up front.
-#ifdef NF_CPLF_AT_USE
-  constexpr bool AT_USE = true;
-#else
   constexpr bool AT_USE = F8 || NP == 1;
-#endif
   auto col_params = [&](int i, float (&bv)[4], float (&sv)[4]) {
     const int tc = wc * 64 + i * 16 + g * 4;                     // tile column (4 consecutive)
     const int f = j0 + (tc & 127);                               // feature
@@ -415,15 +401,6 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
   constexpr int BKE = F8 ? 2 * BK : BK;  // K-tile in elements
   constexpr int EB = F8 ? 1 : 2;
   constexpr int X = ring_extra(D), NSLOT = 8 + X;
-  // weight-gradient products (both operands mn-major): contiguous B halves (stage_half)
-  // contiguous B halves for the weight-gradient products (stage_half BCONTIG): measured 4.5 %
-  // slower on the grouped weight-gradient launch (428 -> 447 us, profiles/r2_bcontig_ab.txt),
-  // kept as an opt-in A/B build (-D NF_G256_BCONTIG)
-#ifdef NF_G256_BCONTIG
-  constexpr bool BSPLIT = !A_KMAJOR && !B_KMAJOR && !F8;
-#else
-  constexpr bool BSPLIT = false;
-#endif
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -515,8 +492,7 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
       stage_half<B_KMAJOR, EB>(a.B, a.ldb, n0, a.cf_b_rows, k0, ke, false, j == H_BHI, dst, wave,
                                lane, a.cf_pair);
     else
-      stage_half<B_KMAJOR, EB, BSPLIT>(a.B, a.ldb, n0, a.N, k0, ke, false, j == H_BHI, dst, wave,
-                                       lane);
+      stage_half<B_KMAJOR, EB>(a.B, a.ldb, n0, a.N, k0, ke, false, j == H_BHI, dst, wave, lane);
   };
   auto issue_h = [&](int h) { issue(h >> 2, h & 3); };
   // valid halves issued at global phases (P - D, P]; half (t, j) is issued at 4t - 5 - X + j
@@ -613,9 +589,6 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
     // whose second 32-deep step may be absent
     int nsteady = nkt - 2;
     if (n2 > 0 && nsteady > n1 - 1) nsteady = n1 - 1;
-#ifdef NF_G256_NO_STEADY   // A/B build (csrc/build.py --variant nosteady -D NF_G256_NO_STEADY)
-    nsteady = 0;
-#endif
     int t = 0;
     for (; t < nsteady; ++t) ktile(t, std::true_type{});
     for (; t < nkt; ++t) ktile(t, std::false_type{});
@@ -656,12 +629,8 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
   }
   if (a.staged) {
     barrier();  // every wave is past its last operand read; each wave reuses 16 KiB of LDS
-    if constexpr (BSPLIT)
-      epi_tile_staged<EPI, 8, F8, 0, 8, true>(a, acc, m0 + wr * 128, n0 + wc * 32, split,
-                                              smem + wave * 16384, lane_e);
-    else
-      epi_tile_staged<EPI, 8, F8>(a, acc, m0 + wr * 128, n0 + wc * 64, split,
-                                  smem + wave * 16384, lane_e);
+    epi_tile_staged<EPI, 8, F8>(a, acc, m0 + wr * 128, n0 + wc * 64, split, smem + wave * 16384,
+                                lane_e);
 #ifdef NF_G256_STAMPS
     NF_STAMP(3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -675,8 +644,7 @@ __device__ __forceinline__ void gemm256_body_impl(const GemmArgs& a, int wg, int
     if (m >= a.M) continue;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int n = BSPLIT ? n0 + wc * 32 + (i & 1) * 16 + (i >> 1) * 128 + g * 4
-                           : n0 + wc * 64 + i * 16 + g * 4;
+      const int n = n0 + wc * 64 + i * 16 + g * 4;
       if (n >= a.N) continue;
       epi_store<EPI>(a, acc[i][j], m, n, split);
     }
@@ -729,7 +697,7 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
   // each column tile once. Without it the blocks whose ids sit on the last column get ALL of
   // its cheap edge tiles (the coupling products' 8-feature / 136-column remainders) and the
   // others all of the full ones, and the launch lasts as long as the full-tile blocks.
-  const bool rot = !a.no_rot && (G & 7) == 0 && ntiles % G == 0 && ((ntiles >> 3) % ntn) == 0 &&
+  const bool rot = (G & 7) == 0 && ntiles % G == 0 && ((ntiles >> 3) % ntn) == 0 &&
                    ((G >> 3) % ntn) == 0;
   auto tile_org = [&](int s, int& m0, int& n0) {
     const int id = xcd_remap(b + s * G, ntiles);
@@ -851,8 +819,6 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
   };
 
   if (ns <= 0) return;
-  if (a.desync && ((b >> a.desync_bit) & 1))
-    for (int i = 0; i < a.desync; ++i) __builtin_amdgcn_s_sleep(127);
   int m0, n0;
   tile_org(0, m0, n0);
   // prologue: the stream's first six halves (K-tile 0, and K-tile 1's A-lo / B-lo; nkt >= 2)
@@ -875,7 +841,7 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
       ++T;
     };
     if constexpr (EPI == EPI_CPL_FWD) {
-      if (!a.no_edge && a.cf_dh - (n0 >> 1) <= 16) tile_loop(std::true_type{});
+      if (a.cf_dh - (n0 >> 1) <= 16) tile_loop(std::true_type{});
       else tile_loop(std::false_type{});
     } else {
       tile_loop(std::false_type{});
@@ -1029,28 +995,22 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
   gemm256_body<A_KM, B_KM, EPI_F32, D, true, F8>(a, local, 0, smem);
 }
 
-// persistent plain products: VINF_G256_PERSIST at load, or nf_gemm256_set_persist (the DP
-// runner turns it off for multi-rank jobs: RCCL kernels take CUs while a grid of exactly one
-// block per CU runs, and a persistent block that cannot start delays its whole tile list)
-static int g_persist = [] {
-  const char* e = getenv("VINF_G256_PERSIST");
-  return e ? atoi(e) : 1;
-}();
+// persistent plain products (on by default), nf_gemm256_set_persist: the DP runner turns it off
+// for multi-rank backwards (RCCL kernels take CUs while a grid of exactly one block per CU runs,
+// and a persistent block that cannot start delays its whole tile list)
+static int g_persist = 1;
 
 // CUs the persistent grid leaves free (nf_gemm256_set_reserve): a multi-rank backward runs
 // RCCL kernels beside the GEMMs, and a persistent block queued behind one would hold back its
 // whole tile list; grid = min(tiles, CUs - reserve) keeps every block startable
 static int g_reserve = 0;
 
-static int g_xcd_pack = [] {
-  const char* e = getenv("VINF_WGRAD_XCD_PACK");
-  return e ? atoi(e) : 1;
-}();
+// weight-gradient tile -> block packing by XCD (nf_gemm256_xcd_pack, on by default)
+static int g_xcd_pack = 1;
 
-static int g_depth = [] {
-  const char* e = getenv("VINF_G256_DEPTH");
-  return e && atoi(e) == 6 ? 6 : 4;
-}();
+// MADE column-tile pairing (nf_gemm256_set_pair): 0 off, 1 auto (when the paired grid still
+// gives every CU a block), 2 always (tests)
+static int g_pair = 1;
 
 int device_cus_256() {
   static const int n = [] {
@@ -1062,14 +1022,14 @@ int device_cus_256() {
   return n;
 }
 
-// VINF_PAIR_ALT (read per launch; default 1): odd blocks of a paired launch run their short tile
-// first, so half the CUs are in a main loop while the other half store their epilogue. The
-// fused MAF epilogues move ~420 KB per tile and run at the chip's HBM rate when every CU stores
-// at once; alternating took fwd2 172 -> 164 us (bf16) / 191 -> 178 (e4m3) and the fused
-// backward 183 -> 166 / 178 -> 167 per layer (profiles/r2_maf_kernels.json)
-inline int pair_alt_env() {
-  const char* e = getenv("VINF_PAIR_ALT");
-  return e ? atoi(e) : 1;
+// Paired MADE launches alternate: odd blocks run their short tile first, so half the CUs are in
+// a main loop while the other half store their epilogue. The fused MAF epilogues move ~420 KB
+// per tile and run at the chip's HBM rate when every CU stores at once; alternating took fwd2
+// 172 -> 164 us (bf16) / 191 -> 178 (e4m3) and the fused backward 183 -> 166 / 178 -> 167 per
+// layer (profiles/r2_maf_kernels.json)
+inline bool pair_ok(const GemmArgs& a, int ntm, int ntn, int splits) {
+  return g_pair && a.krange && splits == 1 && ntn % 2 == 0 &&
+         (g_pair == 2 || (long)ntm * (ntn / 2) >= device_cus_256());
 }
 
 template <bool AK, bool BK_, int EPI, bool DB = false>
@@ -1079,46 +1039,16 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
     fprintf(stderr, "vinf: ReLU bitmask output needs the staged epilogue (N %% 8, 16-B rows)\n");
     abort();
   }
-  // opt-in 4-wave NT kernel (gemm_nt4w.hip, VINF_GEMM_NT4W=1) for the plain bf16 NT products
-  if constexpr (AK && BK_ && !DB && (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK))
-    if (splits == 1 && launch_nt4w(a, EPI, stream)) return;
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
-  // pair the column tiles of MADE-masked products (see gemm256_kernel) when that still gives
-  // every CU a block; VINF_GEMM_PAIR=0 disables, =2 forces (tests)
-  static const int pair_env = [] {
-    const char* e = getenv("VINF_GEMM_PAIR");
-    return e ? atoi(e) : 1;
-  }();
-  a.pair_tiles = pair_env && a.krange && splits == 1 && ntn % 2 == 0 &&
-                 (pair_env == 2 || (long)ntm * (ntn / 2) >= device_cus_256());
-  a.pair_alt = pair_alt_env();
+  // pair the column tiles of MADE-masked products (see gemm256_kernel)
+  a.pair_tiles = pair_ok(a, ntm, ntn, splits);
+  a.pair_alt = 1;
   // plain products run persistent (one continuous LDS-DMA stream per block, see
-  // gemm256_persistent_body); VINF_G256_PERSIST=0 restores one tile per block
-  const int persist_env = g_persist;
+  // gemm256_persistent_body); nf_gemm256_set_persist(0) restores one tile per block
   const bool staged_epi = EPI == EPI_CPL_FWD || a.staged;
   if constexpr (!DB && AK) {
-  if (persist_env && splits == 1 && !a.krange && !a.skip && !a.pair_tiles && staged_epi &&
-      g_depth != 6 && a.K > BK) {
-    static const int desync_env = [] {
-      const char* e = getenv("VINF_G256_DESYNC");
-      return e ? atoi(e) : 0;
-    }();
-    static const int rot_env = [] {
-      const char* e = getenv("VINF_G256_ROT");
-      return e ? atoi(e) : 1;
-    }();
-    static const int desync_bit_env = [] {
-      const char* e = getenv("VINF_G256_DESYNC_BIT");
-      return e ? atoi(e) : 0;
-    }();
-    a.desync = desync_env;
-    a.desync_bit = desync_bit_env;
-    a.no_rot = rot_env ? 0 : 1;
-    static const int edge_env = [] {
-      const char* e = getenv("VINF_G256_EDGE");
-      return e ? atoi(e) : 1;
-    }();
-    a.no_edge = edge_env ? 0 : 1;
+  if (g_persist && splits == 1 && !a.krange && !a.skip && !a.pair_tiles && staged_epi &&
+      a.K > BK) {
     const int ntiles = ntm * ntn;
     int cus = (device_cus_256() - g_reserve) & ~7;   // whole XCD rounds: xcd_remap's b & 7
     cus = cus > 8 ? cus : 8;
@@ -1130,127 +1060,23 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
   }
   }
   dim3 grid(a.pair_tiles ? ntm * (ntn / 2) : ntm * ntn, splits), block(NTHR);
-  if (g_depth != 6)
-    hipLaunchKernelGGL((gemm256_kernel<AK, BK_, EPI, 4, DB>), grid, block, 0, stream, a);
-  else
-    hipLaunchKernelGGL((gemm256_kernel<AK, BK_, EPI, 6, DB>), grid, block, 0, stream, a);
+  hipLaunchKernelGGL((gemm256_kernel<AK, BK_, EPI, 4, DB>), grid, block, 0, stream, a);
   NF_HIP_CHECK(hipGetLastError());
 }
 
 // e4m3 operands (both k-major) on the one-tile-per-block kernel, MADE column tiles paired as in
-// launch() (VINF_GEMM_PAIR read per call: 0 off, 1 auto, 2 always)
+// launch()
 template <int EPI>
 void launch_f8(GemmArgs a, hipStream_t stream) {
   a.staged = EPI == EPI_CPL_FWD ? 0 : staged_ok(a, EPI);
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
-  const char* pe = getenv("VINF_GEMM_PAIR");
-  const int pv = pe ? atoi(pe) : 1;
-  a.pair_tiles = pv && a.krange && ntn % 2 == 0 &&
-                 (pv == 2 || (long)ntm * (ntn / 2) >= device_cus_256());
-  a.pair_alt = pair_alt_env();
+  a.pair_tiles = pair_ok(a, ntm, ntn, 1);
+  a.pair_alt = 1;
   const int nblk = a.pair_tiles ? ntm * (ntn / 2) : ntm * ntn;
   hipLaunchKernelGGL((gemm256_kernel<true, true, EPI, 4, false, true>), dim3(nblk), dim3(NTHR), 0,
                      stream, a);
   NF_HIP_CHECK(hipGetLastError());
 }
-
-// Coupling forward of the last r = Dh % 128 (<= 8) features of a layer, for the launches whose
-// 256-column GEMM tiles cover only the first Dh - r features. Fused, those 8 features were a
-// whole extra column tile (n0 = 3 * 256 at Dh = 392): a full 256 x 256 main loop, 97% of it on
-// zero weight rows, plus an epilogue pass - ~40 us of a 195 us launch at the headline shape
-// (bench/step_gemms.py cpl_fwd vs cpl_fwd_384). Here one wave owns 16 rows: the 16 x 16 MFMA
-// output holds the r s-columns (weight rows j0 + f, MFMA rows 0..7) and r t-columns (rows
-// Dh + j0 + f, MFMA rows 8..15) over the same v_mfma_f32_16x16x32_bf16 k-sequence the tile
-// kernel runs, so s_hat / t are bitwise the fused path's; the lanes holding t hand them to the
-// s lanes with one shuffle, the upper half of the wave zeroes the next operand's pad columns.
-// ldjp row Dh / 128 gets this slice's sum of s (written, or added under !ldj_init).
-struct CplEdgeArgs {
-  const bf16_t* h; long ldh;
-  const bf16_t* W; long ldw;
-  const bf16_t* bias;
-  int M, K, Dh, j0, r;
-  const float* x; long ldx;
-  float* y; long ldy;
-  bf16_t* yb; long ldyb; int yb_width;
-  bf16_t* st; long ldst;
-  float* ldjp; int ldj_init;
-  float scale;
-};
-
-__global__ void __launch_bounds__(256) cpl_edge_fwd_kernel(CplEdgeArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int m0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
-  if (m0 >= a.M) return;
-  const int e = lane & 15, g = lane >> 4, f = e & 7;
-  const bool wok = f < a.r;
-  const long wrow = (e < 8 ? 0 : a.Dh) + a.j0 + (wok ? f : 0);
-  const bf16_t* wp = a.W + wrow * a.ldw + 8 * g;
-  const int mr = min(m0 + e, a.M - 1);
-  const bf16_t* hp = a.h + (long)mr * a.ldh + 8 * g;
-  v4f acc = {0.f, 0.f, 0.f, 0.f};
-  const v8s zero = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int k0 = 0; k0 < a.K; k0 += 256) {   // K % 256 == 0 (launcher): 8 k-steps per chunk,
-    v8s wv[8], hv[8];                          // all 16 loads issued before the first MFMA
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      wv[s] = wok ? *reinterpret_cast<const v8s*>(wp + k0 + 32 * s) : zero;
-      hv[s] = *reinterpret_cast<const v8s*>(hp + k0 + 32 * s);
-    }
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[s], hv[s], acc, 0, 0, 0);
-  }
-  // acc[i] of lane l: MFMA row 4 (l >> 4) + i, sample m0 + (l & 15). Lanes 0..31 hold s_hat of
-  // features 4 (l >> 4) + i, lanes 32..63 the matching t rows.
-  float tv[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) tv[i] = __shfl(acc[i], (lane + 32) & 63);
-  const int m = m0 + e;
-  if (lane < 32) {
-    float part = 0.f, lold = 0.f;
-    const int jf = a.j0 + 4 * g;
-    if (m < a.M && 4 * g < a.r) {
-      if (!a.ldj_init && g == 0) lold = a.ldjp[m];
-      const float4 xv = *reinterpret_cast<const float4*>(a.x + (long)m * a.ldx + jf);
-      const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
-      float yv[4];
-      unsigned short sh[4], ybv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float bs = a.bias ? bf2f(a.bias[jf + i]) : 0.f;
-        const float bt = a.bias ? bf2f(a.bias[a.Dh + jf + i]) : 0.f;
-        sh[i] = f2bf(fmaf(acc[i], 1.f, bs));
-        const float tt = bf2f(f2bf(fmaf(tv[i], 1.f, bt)));
-        const float sv = a.scale * fast_tanhf(bf2f(sh[i]));
-        yv[i] = fmaf(xs[i], __expf(sv), tt);
-        ybv[i] = f2bf(yv[i]);
-        part += sv;
-      }
-      *reinterpret_cast<float4*>(a.y + (long)m * a.ldy + jf) = make_float4(yv[0], yv[1], yv[2], yv[3]);
-      if (a.yb)
-        *reinterpret_cast<ushort4*>(a.yb + (long)m * a.ldyb + jf) =
-            make_ushort4(ybv[0], ybv[1], ybv[2], ybv[3]);
-      *reinterpret_cast<ushort4*>(a.st + (long)m * a.ldst + jf) =
-          make_ushort4(sh[0], sh[1], sh[2], sh[3]);
-    }
-    part += __shfl_xor(part, 16);
-    if (g == 0 && m < a.M) a.ldjp[m] = part + lold;
-  } else if (a.yb && m < a.M) {   // zero the next operand's pad columns [Dh, yb_width)
-    bf16_t* yr = a.yb + (long)m * a.ldyb;
-    for (int c = a.Dh + 8 * (g - 2); c < a.yb_width; c += 16)
-      *reinterpret_cast<uint4*>(yr + c) = make_uint4(0, 0, 0, 0);
-  }
-}
-
-// VINF_CPL_EDGE (read at load; default 0): 1 routes a layer's last Dh % 128 <= 8 features
-// through cpl_edge_fwd_kernel instead of the fused edge column tile. Measured SLOWER at the
-// headline shape (cpl_fwd 208.7 vs 190.4 us, profiles/r3/cpl_edge_ab.jsonl): its 16-row x 64-B
-// operand loads re-read the 134 MB activation at ~2.4 TB/s, while the fused edge tile only adds
-// its DMA stream (~37 us). Kept as an A/B switch with its bitwise test.
-static int g_cpl_edge = [] {
-  const char* e = getenv("VINF_CPL_EDGE");
-  return e ? atoi(e) : 0;
-}();
 
 }  // namespace g256
 }  // namespace gemm
@@ -1258,14 +1084,11 @@ static int g_cpl_edge = [] {
 
 using namespace nf::gemm;
 
-int nf_launch_gemm_pp_cpl_bwd(const GemmArgs& a, hipStream_t stream);   // gemm_pp.hip
-
-void nf_gemm256_set_cpl_edge(int on) { g256::g_cpl_edge = on ? 1 : 0; }
-int nf_gemm256_get_cpl_edge() { return g256::g_cpl_edge; }
-
-// 4 (default): 8-slot LDS ring, 128 KiB; 6: 10-slot ring, 160 KiB, half-tiles issued 2 phases
-// earlier (VINF_G256_DEPTH at load, or set_mode's depth argument)
-void nf_gemm256_set_depth(int d) { g256::g_depth = d == 6 ? 6 : 4; }
+int nf_gemm256_set_pair(int mode) {   // mode < 0: query; returns the previous setting
+  const int prev = g256::g_pair;
+  if (mode >= 0) g256::g_pair = mode > 2 ? 2 : mode;
+  return prev;
+}
 void nf_gemm256_set_persist(int on) { g256::g_persist = on ? 1 : 0; }
 int nf_gemm256_set_reserve(int cus) {
   const int prev = g256::g_reserve;
@@ -1363,14 +1186,7 @@ void nf_launch_gemm256_nt_cpl(const void* h, long ldh, const void* W, long ldw, 
   a.B = (const nf::bf16_t*)W; a.ldb = ldw;
   a.C = st; a.ldc = ld_st;
   a.bias = (const nf::bf16_t*)bias;
-  // the last r = Dh % 128 <= 8 features go to cpl_edge_fwd_kernel (bf16 operands, K % 256 == 0):
-  // the GEMM covers Dh - r features and never reaches the pad columns, which the edge kernel zeroes
-  const int r = Dh % 128;
-  const bool edge = g256::g_cpl_edge && r > 0 && r <= 8 && Dh > 128 && K % 256 == 0 &&
-                    ldh % 8 == 0 && ldw % 8 == 0 && ((unsigned long)h & 15) == 0 &&
-                    ((unsigned long)W & 15) == 0;
-  const int dmain = edge ? Dh - r : Dh;
-  const int ntn = (dmain + 127) / 128;
+  const int ntn = (Dh + 127) / 128;
   a.M = M; a.N = ntn * 256; a.K = K; a.k_per_split = ((K + 63) / 64) * 64;
   a.cf_x = x; a.ld_cf_x = ld_x;
   a.cf_y = y; a.ld_cf_y = ld_y;
@@ -1386,20 +1202,6 @@ void nf_launch_gemm256_nt_cpl(const void* h, long ldh, const void* W, long ldw, 
     abort();
   }
   g256::launch<true, true, EPI_CPL_FWD>(a, 1, stream);
-  if (edge) {
-    g256::CplEdgeArgs e{};
-    e.h = (const nf::bf16_t*)h; e.ldh = ldh;
-    e.W = (const nf::bf16_t*)W; e.ldw = ldw;
-    e.bias = (const nf::bf16_t*)bias;
-    e.M = M; e.K = K; e.Dh = Dh; e.j0 = dmain; e.r = r;
-    e.x = x; e.ldx = ld_x; e.y = y; e.ldy = ld_y;
-    e.yb = (nf::bf16_t*)yb; e.ldyb = ld_yb; e.yb_width = yb_width;
-    e.st = (nf::bf16_t*)st; e.ldst = ld_st;
-    e.ldjp = ldjp + (long)ntn * ld_ldjp; e.ldj_init = ldj_init;
-    e.scale = scale;
-    hipLaunchKernelGGL(g256::cpl_edge_fwd_kernel, dim3((M + 63) / 64), dim3(256), 0, stream, e);
-    NF_HIP_CHECK(hipGetLastError());
-  }
 }
 
 // Second MADE product of MAF layer l with the layer's transform fused (EPI_CPL_FWD, cf_mode 1):
@@ -1519,8 +1321,7 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
     fprintf(stderr, "vinf: bf16 x in the fused backward needs the bf16 coupling form with Wt\n");
     abort();
   }
-  if (Dh > N || dst_pad < 2 * Dh || dst_pad > Dh + N || !staged_ok(a, epi) ||
-      !staged_enabled()) {
+  if (Dh > N || dst_pad < 2 * Dh || dst_pad > Dh + N || !staged_ok(a, epi)) {
     fprintf(stderr, "vinf: fused coupling-backward GEMM needs Dh <= N, 2 Dh <= pad <= Dh + N, "
                     "4-element aligned rows and the staged epilogue\n");
     abort();
@@ -1537,10 +1338,6 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
   if (x_bf16) {
     g256::launch<true, true, EPI_CPL_BWD_XB>(a, 1, stream);
     return;
-  }
-  if (w_kmajor && mode == 0 && (nf_gemm_pp_enabled() & 2)) {
-    a.staged = 1;
-    if (nf_launch_gemm_pp_cpl_bwd(a, stream)) return;
   }
   if (w_kmajor) g256::launch<true, true, EPI_CPL_BWD>(a, 1, stream);   // W given as Wt [N][K]
   else g256::launch<true, false, EPI_CPL_BWD>(a, 1, stream);
@@ -1593,18 +1390,11 @@ void nf_launch_gemm256_fp8_nt(const void* xq, long ldx, const float* sx, int sx_
     abort();
   }
   const int ntm = (M + g256::BM - 1) / g256::BM, ntn = (N + g256::BN - 1) / g256::BN;
-  const char* pe = getenv("VINF_GEMM_PAIR");
-  const int pv = pe ? atoi(pe) : 1;   // 0 off, 1 auto, 2 always (tests)
-  a.pair_tiles = pv && krange && ntn % 2 == 0 &&
-                 (pv == 2 || (long)ntm * (ntn / 2) >= g256::device_cus_256());
-  a.pair_alt = g256::pair_alt_env();
+  a.pair_tiles = g256::pair_ok(a, ntm, ntn, 1);
+  a.pair_alt = 1;
   const int nblk = a.pair_tiles ? ntm * (ntn / 2) : ntm * ntn;
-  if (g256::g_depth == 6)
-    hipLaunchKernelGGL((g256::gemm256_kernel<true, true, EPI_BF16, 6, false, true>),
-                       dim3(nblk), dim3(g256::NTHR), 0, stream, a);
-  else
-    hipLaunchKernelGGL((g256::gemm256_kernel<true, true, EPI_BF16, 4, false, true>),
-                       dim3(nblk), dim3(g256::NTHR), 0, stream, a);
+  hipLaunchKernelGGL((g256::gemm256_kernel<true, true, EPI_BF16, 4, false, true>), dim3(nblk),
+                     dim3(g256::NTHR), 0, stream, a);
   NF_HIP_CHECK(hipGetLastError());
 }
 
@@ -1679,15 +1469,10 @@ void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int
     t.use_perm = nf::wgrad_xcd_perm(t.n, seg_lo, seg_n, ntiles, t.perm) ? 1 : 0;
   }
   // 4-wave 128x128-per-wave TN kernel (gemm_tn4w.hip): the default bf16 launch (the real
-  // multi-layer launch 2583 -> 1960 us median, profiles/r4/tn4w4_layout_probe.jsonl);
-  // VINF_WGRAD_TN4W=0 keeps the 8-wave kernel, layout 3 forces the 4-wave one
-  static const int tn4w_env = [] {
-    const char* e = getenv("VINF_WGRAD_TN4W");
-    return e ? atoi(e) : 1;
-  }();
-  if (!f8 && (layout == 3 || (layout == 0 && tn4w_env)) && nf::gemm::launch_tn4w_multi(t, stream))
-    return;
-  if (layout == 3) layout = 0;
+  // multi-layer launch 2583 -> 1960 us median, profiles/r4/tn4w4_layout_probe.jsonl); layout 4
+  // keeps the 8-wave kernel (A/B and bitwise tests), 3 forces the 4-wave one
+  if (!f8 && (layout == 3 || layout == 0) && nf::gemm::launch_tn4w_multi(t, stream)) return;
+  if (layout == 3 || layout == 4) layout = 0;
   if (layout != 0 && f8) {
     fprintf(stderr, "vinf: gemm256_tn_multi: transposed-operand layouts are bf16 only\n");
     abort();
@@ -1701,20 +1486,14 @@ void nf_launch_gemm256_tn_multi(int nprob, const NfTnProblem* pr, int tile0, int
   else if (f8)
     hipLaunchKernelGGL((g256::gemm256_multi_kernel<4, true>), dim3(ntiles), dim3(g256::NTHR), 0,
                        stream, t);
-  else if (g256::g_depth == 6)
-    hipLaunchKernelGGL(g256::gemm256_multi_kernel<6>, dim3(ntiles), dim3(g256::NTHR), 0, stream, t);
   else
     hipLaunchKernelGGL(g256::gemm256_multi_kernel<4>, dim3(ntiles), dim3(g256::NTHR), 0, stream, t);
   NF_HIP_CHECK(hipGetLastError());
 }
 
 void nf_launch_gemm256_tn_group(const GroupArgs& g, hipStream_t stream) {
-  if (g256::g_depth == 6)
-    hipLaunchKernelGGL(g256::gemm256_group_kernel<6>, dim3(g.start[g.nprob]), dim3(g256::NTHR), 0,
-                       stream, g);
-  else
-    hipLaunchKernelGGL(g256::gemm256_group_kernel<4>, dim3(g.start[g.nprob]), dim3(g256::NTHR), 0,
-                       stream, g);
+  hipLaunchKernelGGL(g256::gemm256_group_kernel<4>, dim3(g.start[g.nprob]), dim3(g256::NTHR), 0,
+                     stream, g);
   NF_HIP_CHECK(hipGetLastError());
 }
 

@@ -10,18 +10,13 @@
 // (32 fragments per 128 MFMAs per K-tile instead of 24 per 64).
 //
 // Geometry: 256 threads = 4 waves, wave w = (wr, wc) = (w >> 1, w & 1) owns tile rows
-// [128 wr, +128) x cols [128 wc, +128). BK = 64. LDS: 2 stages x 4 half-images x 16 KiB =
-// 128 KiB; half-image h of a stage = mn-major [64 k][128 mn] (gemm_tile.h layout, 16-B chunk c of
-// k-row k at c ^ mn_swz(k)): h = 0 / 1: dy rows m0 + [0, 128) / [128, 256); h = 2 / 3: x cols
-// n0 + [0, 128) / [128, 256). Wave w stages half-image w of every K-tile (16 LDS-DMA
-// instructions of 4 k-rows x 256 contiguous bytes: whole 128-B lines) and reads A half wr and
-// B half wc only.
-//
-// Schedule per K-tile t (stage s = t & 1; F0 / F1 = fragments of k-steps 0 / 1, 64 VGPRs each):
-//   reads F1(t)  |  MFMA F0(t) x 64  |  lgkmcnt(0), vmcnt(0) [K-tile t+1 landed], barrier  |
-//   DMA K-tile t+2 -> stage s  |  reads F0(t+1)  |  MFMA F1(t) x 64
-// one barrier per K-tile; the barrier both publishes K-tile t+1 and retires every wave's reads of
-// stage s before it is restaged. K-tile t+1's DMA has the compute of one K-tile to land.
+// [128 wr, +128) x cols [128 wc, +128). K-tiles of 32 k in 4 LDS stages of 32 KiB; a stage holds
+// four mn-major half-images [32 k][128 mn] (gemm_tile.h layout, 16-B chunk c of k-row k at
+// c ^ mn_swz(k)): h = 0 / 1: dy rows m0 + [0, 128) / [128, 256); h = 2 / 3: x cols n0 + [0, 128)
+// / [128, 256). Wave w stages half-image w of every K-tile (LDS-DMA pieces of 4 k-rows x 256
+// contiguous bytes: whole 128-B lines) and reads A half wr and B half wc only. K-tile t + 3 is in
+// flight while t is multiplied (tile_body4 below).
+
 #include "tn_multi.h"
 
 #include <cstdlib>
@@ -73,157 +68,11 @@ __device__ __forceinline__ void mfma_acc(v4f& acc, const v8s& a, const v8s& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
-template <bool DODB>
-__device__ __forceinline__ void tile_body(const GemmArgs& a, int m0, int n0, char* st0,
-                                          char* st1) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int nkt = a.K / BK;
-
-  // this wave's DMA source: half-image `wave`
-  const bf16_t* sbase = wave < 2 ? a.A : a.B;
-  const long sld = wave < 2 ? a.lda : a.ldb;
-  const int scol0 = wave < 2 ? m0 + wave * 128 : n0 + (wave - 2) * 128;
-  const int stot = wave < 2 ? a.M : a.N;
-  // the two stages are separate __shared__ objects and every access below names one at compile
-  // time: the compiler then knows a DMA into one stage cannot alias a read of the other. With
-  // one array it drains the LDS-DMA queue (s_waitcnt vmcnt(0)) before every transposed read
-  // (ds_read_b64_tr_b16 is not disambiguated like plain LDS loads are), i.e. waits for the DMA
-  // it just issued for a later K-tile
-  auto stp = [&](auto p_c) -> char* { return decltype(p_c)::value ? st1 : st0; };
-  auto issue = [&](int t, auto p_c) {
-    stage(sbase, sld, scol0, stot, t * BK, stp(p_c) + wave * HALF, lane);
-  };
-
-  v4f acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
-  float dbs[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) dbs[j] = 0.f;
-
-  // A fragments single-buffered (fragment j of the next k-step is read as soon as the 8 MFMAs
-  // of this k-step that use it are issued), B fragments double-buffered: 96 fragment VGPRs, so
-  // the 256 accumulators stay put in the AGPRs
-  v8s fa[8], fb0[8], fb1[8];
-  auto rd_a = [&](auto p_c, int ks, int j) {
-    return read_frag<false>(stp(p_c) + wr * HALF, j * 16, ks, lane);
-  };
-  auto rd_b = [&](auto p_c, int ks, v8s (&fb)[8]) {
-    const char* st = stp(p_c) + (2 + wc) * HALF;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fb[i] = read_frag<false>(st, i * 16, ks, lane);
-  };
-  auto db_add = [&](int j) {   // db[m]: the A fragment's 8 k-values of row (lane & 15), v_dot2
-    if constexpr (DODB) {
-      typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
-      const v2bf one = {(__bf16)1.0f, (__bf16)1.0f};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const unsigned w = (unsigned)(unsigned short)fa[j][2 * e] |
-                           ((unsigned)(unsigned short)fa[j][2 * e + 1] << 16);
-        dbs[j] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf, w), one, dbs[j], false);
-      }
-    }
-  };
-  // one k-step: for each A fragment j its 8 MFMAs, then (RD) its successor from (tn, ksn)
-  auto kstep = [&](const v8s (&fb)[8], auto pn_c, int ksn, auto rd_c) {
-    constexpr bool RD = decltype(rd_c)::value;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        mfma_acc(acc[i][j], fb[i], fa[j]);
-      db_add(j);
-      if constexpr (RD) fa[j] = rd_a(pn_c, ksn, j);
-    }
-  };
-
-  using P0 = std::false_type;
-  using P1 = std::true_type;
-  if (nkt > 0) {
-    issue(0, P0{});
-    issue(1, P1{});
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-#pragma unroll
-    for (int j = 0; j < 8; ++j) fa[j] = rd_a(P0{}, 0, j);
-    rd_b(P0{}, 0, fb0);
-    // K-tile t in stage P (compile time); NEXT: K-tile t+1 exists; ISSUE: K-tile t+2 exists
-    auto ktile = [&](int t, auto p_c, auto next_c, auto issue_c) {
-      constexpr bool P = decltype(p_c)::value;
-      constexpr bool NEXT = decltype(next_c)::value, ISSUE = decltype(issue_c)::value;
-      using PN = std::integral_constant<bool, !P>;
-      rd_b(p_c, 1, fb1);
-      kstep(fb0, p_c, 1, std::true_type{});
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if constexpr (NEXT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (ISSUE) issue(t + 2, p_c);
-      if constexpr (NEXT) rd_b(PN{}, 0, fb0);
-      kstep(fb1, PN{}, 0, next_c);
-    };
-    using T = std::true_type;
-    using F = std::false_type;
-    // nkt is even (launch_tn4w_multi): pairs of K-tiles in stages 0, 1; the last pair drains
-    int t = 0;
-    for (; t + 2 < nkt; t += 2) {
-      ktile(t, P0{}, T{}, T{});
-      ktile(t + 1, P1{}, T{}, T{});
-    }
-    ktile(t, P0{}, T{}, F{});
-    ktile(t + 1, P1{}, F{}, F{});
-  }
-
-  // ---------------------------------------------------------------- epilogue
-  // acc[i][j]: n = n0 + 128 wc + 16 i + 4 (lane >> 4) + r, m = m0 + 128 wr + 16 j + (lane & 15)
-  const int g = lane >> 4, c = lane & 15;
-  if (DODB && wc == 0) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = dbs[j];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      const int m = m0 + wr * 128 + j * 16 + c;
-      if (g == 0 && m < a.M) a.dbias[m] = v;
-    }
-  }
-  // MFMA result -> VALU / v_accvgpr_read: 8-pass XDL needs 12 wait states after the last MFMA
-  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-  __syncthreads();   // every wave is past its last operand read: the LDS is free
-  char* region = (wave < 2 ? st0 : st1) + (wave & 1) * 32768;   // 2 x 16 KiB per wave
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    v4f sub[4][8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sub[i][j] = acc[4 * h + i][j];
-    if (a.staged)
-      epi_tile_staged<EPI_F32, 8>(a, sub, m0 + wr * 128, n0 + wc * 128 + h * 64, 0,
-                                  region + h * 16384, lane);
-    else
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int m = m0 + wr * 128 + j * 16 + c;
-        if (m >= a.M) continue;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int n = n0 + wc * 128 + h * 64 + i * 16 + g * 4;
-          if (n < a.N) epi_store<EPI_F32>(a, sub[i][j], m, n, 0);
-        }
-      }
-  }
-}
-
-// Deeper variant (VINF_TN4W_STAGES=4): 32-deep K-tiles in 4 stages of 32 KiB (separate
-// __shared__ objects, compile-time stage per access), K-tile t+3 issued while t is computed, so
-// up to 96 KiB per CU are in flight instead of 64; one barrier per 64 MFMAs.
+// 32-deep K-tiles in 4 stages of 32 KiB (separate __shared__ objects, compile-time stage per
+// access), K-tile t + PD issued while t is computed (PD = 3: up to 96 KiB per CU in flight); one
+// barrier per 64 MFMAs. (A 2-stage body of 64-deep K-tiles, 64 KiB in flight, took 2193-2316 us
+// per real multi-layer launch against 1959-2075 for this one: profiles/r4/tn4w4_layout_probe.jsonl;
+// prefetch distance 2 2217-2234 us: profiles/r4/tn4w4_pd_layout.jsonl.)
 template <bool DODB, int PD>
 __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, char* q0, char* q1,
                                            char* q2, char* q3) {
@@ -344,7 +193,11 @@ __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, ch
       if (g == 0 && m < a.M) a.dbias[m] = v;
     }
   }
+  // the accumulators are written by asm MFMAs the compiler cannot see: keep every epilogue read
+  // of them below the pad (no v_accvgpr read may be scheduled above it)
+  __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
   __syncthreads();
   char* region = (wave == 0 ? q0 : wave == 1 ? q1 : wave == 2 ? q2 : q3);   // 32 KiB per wave
 #pragma unroll
@@ -398,54 +251,17 @@ __global__ void __launch_bounds__(NTHR, 1) gemm_tn4w4_kernel(g256::TnMulti t) {
   else tile_body4<false, PD>(a, tm * BM, tn * BN, q0, q1, q2, q3);
 }
 
-__global__ void __launch_bounds__(NTHR, 1) gemm_tn4w_kernel(g256::TnMulti t) {
-  __shared__ __attribute__((aligned(16))) char st0[STAGE];
-  __shared__ __attribute__((aligned(16))) char st1[STAGE];
-  const int pos = xcd_remap(blockIdx.x, t.ntiles);
-  const int id = t.tile0 + (t.use_perm ? (int)t.perm[pos] : pos);
-  int p = 0;
-  for (int q = 1; q < t.n; ++q)
-    if (id >= t.d[q].start) p = q;
-  const g256::TnDesc& d = t.d[p];
-  GemmArgs a{};
-  a.A = d.A; a.lda = d.lda;
-  a.B = d.B; a.ldb = d.ldb;
-  a.C = d.C; a.ldc = d.ldc;
-  a.dbias = d.db;
-  a.M = d.M; a.N = d.N; a.K = d.K;
-  a.staged = d.staged;
-  a.cmask = d.cmask;
-  const int local = d.tiles ? (int)d.tiles[id - d.start] : id - d.start;
-  const int ntn = (a.N + BN - 1) / BN;
-  const int tm = local / ntn, tn = local % ntn;
-  if (a.dbias != nullptr && tn == 0) tile_body<true>(a, tm * BM, tn * BN, st0, st1);
-  else tile_body<false>(a, tm * BM, tn * BN, st0, st1);
-}
-
 }  // namespace tn4w
 
 bool launch_tn4w_multi(const g256::TnMulti& t, hipStream_t stream) {
   for (int i = 0; i < t.n; ++i) {
     const g256::TnDesc& d = t.d[i];
     // an even number of 64-deep K-tiles, 16-B operand rows (8 bf16 columns), 16-B aligned bases
-    if (d.K % (2 * tn4w::BK) || d.M % 8 || d.N % 8 || d.lda % 8 || d.ldb % 8 ||
+    if (d.K <= 0 || d.K % (2 * tn4w::BK) || d.M % 8 || d.N % 8 || d.lda % 8 || d.ldb % 8 ||
         ((unsigned long)d.A & 15) || ((unsigned long)d.B & 15))
       return false;
   }
-  static const int stages = [] {
-    const char* e = getenv("VINF_TN4W_STAGES");
-    return e ? atoi(e) : 4;   // 4: profiles/r4/tn4w4_layout_probe.jsonl (2: tn4w_layout_probe)
-  }();
-  static const int pd = [] {
-    const char* e = getenv("VINF_TN4W_PD");
-    return e && atoi(e) == 2 ? 2 : 3;
-  }();
-  if (stages == 4 && pd == 2)
-    hipLaunchKernelGGL(tn4w::gemm_tn4w4_kernel<2>, dim3(t.ntiles), dim3(tn4w::NTHR), 0, stream, t);
-  else if (stages == 4)
-    hipLaunchKernelGGL(tn4w::gemm_tn4w4_kernel<3>, dim3(t.ntiles), dim3(tn4w::NTHR), 0, stream, t);
-  else
-    hipLaunchKernelGGL(tn4w::gemm_tn4w_kernel, dim3(t.ntiles), dim3(tn4w::NTHR), 0, stream, t);
+  hipLaunchKernelGGL(tn4w::gemm_tn4w4_kernel<3>, dim3(t.ntiles), dim3(tn4w::NTHR), 0, stream, t);
   NF_HIP_CHECK(hipGetLastError());
   return true;
 }

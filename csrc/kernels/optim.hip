@@ -204,17 +204,12 @@ void nf_launch_flat_optimizer(int kind, float* p, const float* g, float* m, floa
   a.step_ptr = step_ptr; a.step_host = step_host;
   a.gscale_ptr = gscale_ptr; a.gscale_host = gscale_host;
   a.skip_ptr = skip_ptr; a.kind = kind; a.warmup = warmup;
-  // knobs: VINF_OPT_NT=0 plain loads/stores (nontemporal is the default: 446 -> 397 us for the
-  // headline's 72.2M parameters, tools/opt_probe.py), VINF_OPT_BLOCKS grid cap
-  static const int nt = [] { const char* e = getenv("VINF_OPT_NT"); return !(e && e[0] == '0'); }();
-  static const long cap = [] { const char* e = getenv("VINF_OPT_BLOCKS"); return e ? atol(e) : 2048L; }();
+  // nontemporal loads / stores (446 -> 397 us for the headline's 72.2M parameters against plain
+  // ones, tools/opt_probe.py), grid capped at 2048 blocks (grid-stride loop)
   long blocks = ((n >> 2) + 255) / 256;
   if (blocks < 1) blocks = 1;
-  if (blocks > cap) blocks = cap;
-  if (nt)
-    hipLaunchKernelGGL(flat_optimizer_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
-  else
-    hipLaunchKernelGGL(flat_optimizer_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(flat_optimizer_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   NF_HIP_CHECK(hipGetLastError());
 }
 

@@ -13,47 +13,17 @@ case $name in
   dma)            # LDS-DMA operand stream: segment size x footprint x DMA depth per wave
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/mem_issue_bench.hip -o $O/mem_issue_bench &&
     timeout -k 10 120 $O/mem_issue_bench dma > $O/dma.jsonl ;;
-  desync)         # persistent GEMMs with a start offset on half the blocks: bit 0 = XCD parity,
-                  # bit 5 = half the CUs of every XCD; args: batch
-    b=${1:-262144}
-    for cfg in "0 0" "4 0" "4 5" "6 5" "4 3"; do set -- $cfg
-      VINF_G256_DESYNC=$1 VINF_G256_DESYNC_BIT=$2 VINF_BENCH_TAG=b${b}_d$1_bit$2 \
-        timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --batch $b --iters 10 \
-        --only fwd_l1,fwd_l2,cpl_fwd,dgrad_l2,cpl_bwd >> $O/sg.jsonl || exit 1
-    done ;;
-  wgrad_ab)       # the deferred weight-gradient launch: baseline, deeper ring, XCD packing off
-    for r in 1 2; do
-      VINF_BENCH_TAG=base timeout -k 10 180 python -m vi_normflows_amd.bench.wgrad_bench --layers 13 >> $O/wg.jsonl || exit 1
-      VINF_BENCH_TAG=depth6 VINF_G256_DEPTH=6 timeout -k 10 180 python -m vi_normflows_amd.bench.wgrad_bench --layers 13 >> $O/wg.jsonl || exit 1
-      VINF_BENCH_TAG=xcdpack0 VINF_WGRAD_XCD_PACK=0 timeout -k 10 180 python -m vi_normflows_amd.bench.wgrad_bench --layers 13 >> $O/wg.jsonl || exit 1
-    done ;;
   wgrad_probe)    # TN weight-gradient loop: real vs cache-resident operands vs the NT kernel
-    VINF_BENCH_TAG=${1:-cur} timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 > $O/probe.jsonl &&
+    timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --tag ${1:-cur} --probe --iters 5 > $O/probe.jsonl &&
     true ;;
   wgrad_quick)    # weight-gradient correctness + the real deferred launch + the TN/NT probe
     timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 &&
-    VINF_BENCH_TAG=${1:-cur} timeout -k 10 180 python -m vi_normflows_amd.bench.wgrad_bench --layers 13 >> $O/wg.jsonl &&
-    VINF_BENCH_TAG=${1:-cur} timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 >> $O/probe.jsonl ;;
+    timeout -k 10 180 python -m vi_normflows_amd.bench.wgrad_bench --tag ${1:-cur} --layers 13 >> $O/wg.jsonl &&
+    timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --tag ${1:-cur} --probe --iters 5 >> $O/probe.jsonl ;;
   wgrad_pmc)      # L2 hit / miss and wave-state counters of the TN / NT probe (one counter pass)
     export TMPDIR=/tmp
     timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES \
       -d $O/pmc -o probe --output-format csv -- python3 -m vi_normflows_amd.bench.wgrad_bench --probe --iters 2 > $O/probe.log 2>&1 ;;
-  pp_ab)          # two-blocks-per-CU forward GEMM: correctness, then per-product A/B
-    timeout -k 10 300 python -u -m pytest tests/test_gemm_pp_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
-    VINF_GEMM_PP=3 timeout -k 10 300 python -u -m pytest tests/test_realnvp_engine.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider >> $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
-    for r in 1 2; do
-      VINF_GEMM_PP=0 VINF_BENCH_TAG=g256 timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,cpl_bwd >> $O/sg.jsonl || exit 1
-      VINF_GEMM_PP=3 VINF_BENCH_TAG=pp timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,cpl_bwd >> $O/sg.jsonl || exit 1
-    done ;;
-  dp_policy)      # 1-rank RCCL path (--force-reduce): backward GEMM policy A/B
-    timeout -k 10 300 python -u -m pytest tests/test_gemm_persistent_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
-    for r in 1 2; do
-      for pol in 1 fwd reserve:16 reserve:8; do
-        p=${pol%%:*}; res=${pol#*:}; [ "$res" = "$pol" ] && res=0
-        VINF_DP_PERSIST=$p VINF_G256_RESERVE=$res timeout -k 10 240 python bench.py --steps 20 --warmup 5 --force-reduce > $O/b.json 2> $O/b.err || { tail -20 $O/b.err; exit 1; }
-        python -c "import json,sys;d=json.load(open('$O/b.json'));print(json.dumps({'policy':'$pol','ms':d['ms_per_step'],'replicas_identical':d['notes']['replicas_identical']}))" >> $O/ab.jsonl
-      done
-    done ;;
   step_ab)        # whole-step A/B of an environment switch: args NAME VALUE_A VALUE_B [rounds]
     var=$1; va=$2; vb=$3; n=${4:-3}
     for r in $(seq $n); do
@@ -81,48 +51,11 @@ case $name in
     timeout -k 10 300 python -u -m pytest tests/test_iaf_engine.py -m gpu -k graph -v --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1
     rc=$?; grep -E "PASS|FAIL|assert|differs|Error" $O/pytest.txt | head -20
     [ $rc -le 1 ] || exit $rc ;;
-  tn4w)           # 4-wave TN weight-gradient kernel: bitwise vs the 8-wave launch, then the probe
-                  # (real / cache-resident operands) and the real multi-layer launch layouts 0-3
-    timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py -m gpu -x -q -k "tn4w or tn_multi" --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
-    tail -1 $O/pytest.txt
-    VINF_BENCH_TAG=${1:-cur} timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 > $O/probe.jsonl &&
-    VINF_BENCH_TAG=${1:-cur} timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --layout-probe --layers 13 --iters 3 > $O/layout.jsonl &&
-    cat $O/probe.jsonl $O/layout.jsonl
-    VINF_TN4W_STAGES=4 timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py -m gpu -x -q -k "tn4w" --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_s4.txt 2>&1 || { tail -30 $O/pytest_s4.txt; exit 1; }
-    tail -1 $O/pytest_s4.txt
-    VINF_TN4W_STAGES=4 VINF_BENCH_TAG=stages4 timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 > $O/probe_s4.jsonl &&
-    VINF_TN4W_STAGES=4 VINF_BENCH_TAG=stages4 timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --layout-probe --layers 13 --iters 3 > $O/layout_s4.jsonl &&
-    cat $O/probe_s4.jsonl $O/layout_s4.jsonl
-    # a variant build (e.g. --variant builtindma -D NF_G256_BUILTIN_DMA): correctness, then the same
-    if [ -f vi_normflows_amd/_native/libvinf_hip_asmdma.so ]; then
-      export VINF_NATIVE_LIB=vi_normflows_amd/_native/libvinf_hip_asmdma.so
-      timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py tests/test_gemm_persistent_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_asmdma.txt 2>&1 || { tail -30 $O/pytest_asmdma.txt; exit 1; }
-      tail -1 $O/pytest_asmdma.txt
-      VINF_BENCH_TAG=asmdma timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --probe --iters 5 > $O/probe_asmdma.jsonl &&
-      VINF_BENCH_TAG=asmdma timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --layout-probe --layers 13 --iters 3 > $O/layout_asmdma.jsonl &&
-      cat $O/probe_asmdma.jsonl $O/layout_asmdma.jsonl
-      unset VINF_NATIVE_LIB
-    fi ;;
-  tn4w_pd)        # 4-stage TN kernel, prefetch distance 2 vs 3: layout probe + whole step
-    for r in 1 2; do
-      for pd in 3 2; do
-        VINF_TN4W_PD=$pd VINF_BENCH_TAG=pd$pd timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --layout-probe --layers 13 --iters 3 >> $O/layout.jsonl || exit 1
-        VINF_TN4W_PD=$pd timeout -k 10 240 python bench.py --steps 20 --warmup 5 > $O/b.json 2> $O/b.err || { tail -20 $O/b.err; exit 1; }
-        python -c "import json;d=json.load(open('$O/b.json'));print(json.dumps({'pd':$pd,'ms':d['ms_per_step'],'F':d['notes']['final_free_energy']}))" >> $O/ab.jsonl
-      done
-    done
-    grep '"layout": [03]' $O/layout.jsonl; cat $O/ab.jsonl
-    # L2 hit / fabric reads of the real launch at both distances (one counter pass each)
-    export TMPDIR=/tmp
-    for pd in 3 2; do
-      VINF_TN4W_PD=$pd timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum \
-        -d $O/pmc_pd$pd -o wg --output-format csv -- python3 -m vi_normflows_amd.bench.wgrad_bench --layers 13 --iters 1 > $O/pmc_pd$pd.log 2>&1 || { tail -20 $O/pmc_pd$pd.log; exit 1; }
-    done ;;
   wg_pitch)       # weight-gradient launch vs operand row pitch (power of two or padded), both
                   # kernels, plus the L2 counters of the 4-wave one at each pitch
     for r in 1 2; do
       for pad in 0 64 32; do
-        VINF_BENCH_TAG=pad$pad timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --layout-probe --layers 13 --iters 3 --layouts 0,3 --pitch-pad $pad >> $O/layout.jsonl || exit 1
+        timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --tag pad$pad --layout-probe --layers 13 --iters 3 --layouts 0,3 --pitch-pad $pad >> $O/layout.jsonl || exit 1
       done
     done
     cat $O/layout.jsonl ;;
@@ -150,7 +83,7 @@ PY
   wg_kchunk)      # timing probe: the weight-gradient launch as 1 / 2 / 4 / 8 K-chunk launches
     for r in 1 2; do
       for kc in 1 2 4 8; do
-        VINF_BENCH_TAG=kc$kc timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --layout-probe --layers 13 --iters 3 --layouts 3 --kchunks $kc >> $O/layout.jsonl || exit 1
+        timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --tag kc$kc --layout-probe --layers 13 --iters 3 --layouts 3 --kchunks $kc >> $O/layout.jsonl || exit 1
       done
     done
     cat $O/layout.jsonl ;;
@@ -160,8 +93,8 @@ PY
     VINF_NATIVE_LIB=$P timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py tests/test_gemm_persistent_gpu.py tests/test_realnvp_engine.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_$v.txt 2>&1 || { tail -30 $O/pytest_$v.txt; exit 1; }
     tail -1 $O/pytest_$v.txt
     for r in 1 2; do
-      VINF_BENCH_TAG=default timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,dgrad_l2 >> $O/sg.jsonl || exit 1
-      VINF_NATIVE_LIB=$P VINF_BENCH_TAG=$v timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l1,fwd_l2,dgrad_l2 >> $O/sg.jsonl || exit 1
+      timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --tag default --iters 20 --only fwd_l1,fwd_l2,dgrad_l2 >> $O/sg.jsonl || exit 1
+      VINF_NATIVE_LIB=$P timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --tag $v --iters 20 --only fwd_l1,fwd_l2,dgrad_l2 >> $O/sg.jsonl || exit 1
     done
     for r in 1 2 3; do
       for lib in default $v; do
@@ -172,9 +105,6 @@ PY
     done
     unset VINF_NATIVE_LIB
     grep -v sum $O/sg.jsonl; cat $O/bench.jsonl ;;
-  cumask)         # CU-mask stream probe: mask bit -> XCD / SE / CU, and graph replay vs the mask
-    /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/cumask_probe.hip -o $O/cumask_probe &&
-    timeout -k 10 120 $O/cumask_probe > $O/cumask.jsonl && tail -3 $O/cumask.jsonl ;;
   tests)          # selected GPU test files: args "<pytest paths / -k expr>" [tag]
     tag=${2:-t}
     timeout -k 10 900 python -u -m pytest $1 -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > $O/$tag.txt 2>&1 || { tail -40 $O/$tag.txt; exit 1; }
@@ -187,9 +117,6 @@ PY
   dp_contention)  # RCCL CU-occupancy emulation on the headline step (bench/dp_contention.py)
     timeout -k 10 600 python -m vi_normflows_amd.bench.dp_contention "$@" > $O/dpc.jsonl 2> $O/dpc.err || { tail -20 $O/dpc.err; exit 1; }
     cat $O/dpc.jsonl ;;
-  partition)      # backward's chain and weight gradients on two CU-masked streams (bench/partition_probe.py)
-    timeout -k 10 600 python -m vi_normflows_amd.bench.partition_probe "$@" > $O/part.jsonl 2> $O/part.err || { tail -20 $O/part.err; exit 1; }
-    cat $O/part.jsonl ;;
   bench)          # headline bench on this box: args [tag] [extra bench args]
     tag=${1:-base}; shift
     timeout -k 10 240 python bench.py --steps 20 --warmup 5 "$@" > $O/$tag.json 2> $O/$tag.err || { tail -20 $O/$tag.err; exit 1; }
@@ -222,7 +149,7 @@ PY
     for r in 1 2; do
       for lib in default $v; do
         if [ $lib = default ]; then unset VINF_NATIVE_LIB; else export VINF_NATIVE_LIB=$L; fi
-        VINF_BENCH_TAG=$lib timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only fwd_l2,cpl_fwd,dgrad_l2,cpl_bwd >> $O/sg.jsonl || exit 1
+        timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --tag $lib --iters 20 --only fwd_l2,cpl_fwd,dgrad_l2,cpl_bwd >> $O/sg.jsonl || exit 1
         timeout -k 10 240 python bench.py --steps 20 --warmup 5 > $O/b.json 2> $O/b.err || { tail -20 $O/b.err; exit 1; }
         python -c "import json;d=json.load(open('$O/b.json'));print(json.dumps({'lib':'$lib','ms':d['ms_per_step'],'F':d['notes']['final_free_energy']}))" >> $O/bench.jsonl
         for pr in bf16 fp8; do
@@ -232,10 +159,5 @@ PY
       done
     done
     unset VINF_NATIVE_LIB ;;
-  mask_ab)        # forward product with / without the ReLU bitmask output, bitmask vs bf16 read
-    for r in 1 2; do
-      timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --iters 20 \
-        --only fwd_l2,fwd_l2_nomask,dgrad_l2,dgrad_l2_bf16aux >> $O/sg.jsonl || exit 1
-    done ;;
   *) echo "unknown experiment $name"; exit 2 ;;
 esac

@@ -49,3 +49,16 @@ def _gemm_backend_guard():
     prev = gemm.backend()
     yield
     assert gemm.backend() == prev, f"test changed the GEMM backend to {gemm.backend()}"
+
+
+@pytest.fixture
+def kpaths(monkeypatch):
+    """kpaths(cpl_xbf16=0, ...): switch engine kernel paths (utils.config.KernelPaths) for the
+    engines constructed afterwards in this test, through VINF_KERNEL_PATHS (merged with what
+    earlier calls of the same test set)."""
+    cur = {}
+
+    def set_(**kw):
+        cur.update({k: int(bool(v)) for k, v in kw.items()})
+        monkeypatch.setenv("VINF_KERNEL_PATHS", ",".join(f"{k}={v}" for k, v in cur.items()))
+    return set_

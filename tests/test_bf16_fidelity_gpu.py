@@ -84,9 +84,9 @@ def test_bf16_engine_matches_fp32_oracle_at_headline_shape(gpu, layers, tol_laye
     rec["layer_grad_rel_max"] = worst
     rec["layer_grad_rel"] = per_layer
     print(json.dumps(rec))
-    out = os.environ.get("VINF_FIDELITY_OUT")
+    out = os.environ.get("VINF_EVIDENCE_DIR")   # a directory: evidence files of GPU tests
     if out:
-        with open(out, "a") as f:
+        with open(os.path.join(out, "bf16_fidelity.jsonl"), "a") as f:
             f.write(json.dumps(rec) + "\n")
     assert math.isfinite(rec["loss_bf16"])
     assert rec["zK_rel"] < 2e-2

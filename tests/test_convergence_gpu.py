@@ -11,7 +11,7 @@ B = 4096 MC samples per step, 1500 hipGraph-replayed steps. Asserted:
   initial F is ~840 (1.07 nat/dim), and a q that ignores the twist entirely sits at
   1 nat per pair = 392;
 * F_end > -1 (the KL floor, up to Monte-Carlo noise of a B = 4096 estimate).
-The trajectory is written to ``VINF_CONVERGENCE_OUT`` when set (``profiles/``).
+The trajectory is written to ``$VINF_EVIDENCE_DIR/headline_convergence.jsonl`` when set (``profiles/``).
 """
 import os
 
@@ -23,8 +23,8 @@ pytestmark = pytest.mark.gpu
 def test_headline_realnvp32_converges_towards_floor(gpu):
     from vi_normflows_amd.bench.convergence import run
 
-    out = os.environ.get("VINF_CONVERGENCE_OUT")
-    f = open(out, "w") if out else None
+    out = os.environ.get("VINF_EVIDENCE_DIR")   # a directory: evidence files of GPU tests
+    f = open(os.path.join(out, "headline_convergence.jsonl"), "w") if out else None
     try:
         recs = run(batch=4096, steps=1500, every=10, lr=1e-3, lr_warmup=100.0, pairing="split",
                    out=f)

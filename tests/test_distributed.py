@@ -96,7 +96,7 @@ def test_bucket_layout_reverse_order_and_contiguous():
 def _fault_worker(rank, world, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
-                      VINF_FAULT_STEP="2", VINF_FAULT_RANK="0", VINF_FAULT_KIND="nan")
+                      VINF_FAULT="nan:2:0")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from vi_normflows_amd.parallel.dist import DistInfo
     from vi_normflows_amd.parallel.runner import DataParallelRunner

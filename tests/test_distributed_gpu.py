@@ -28,8 +28,8 @@ def _port():
 def _worker(rank, world, port, eps_all, out_dir, side):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), VINF_DIST_BACKEND="gloo",
-                      VINF_WGRAD_STREAM="1" if side == "1" else "0",
-                      VINF_WGRAD_DEFER="1" if side == "defer" else "0")
+                      VINF_KERNEL_PATHS=f"wgrad_stream={int(side == '1')},"
+                                        f"wgrad_defer={int(side == 'defer')}")
     from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI
     from vi_normflows_amd.parallel import dist as vdist
     from vi_normflows_amd.parallel.runner import DataParallelRunner
@@ -91,13 +91,9 @@ def _rccl_worker(rank, port, out_dir):
     cfg = RealNVPConfig(dim=64, n_layers=4, hidden=256, target="banana", anneal="none",
                         init_out_std=0.2)
     out = {}
-    for name in ("plain", "rccl_eager", "rccl_graph", "rccl_fence"):
-        # rccl_fence: the opt-in weight-gradient fence (each launch waits for the collectives
-        # in flight, VINF_DP_WGRAD_FENCE=1) must not change a bit either
-        os.environ["VINF_DP_WGRAD_FENCE"] = "1" if name == "rccl_fence" else "0"
+    for name in ("plain", "rccl_eager", "rccl_graph"):
         eng = RealNVPVI(cfg, batch=512, device=dev, seed=7, lr=1e-3)
         run = DataParallelRunner(eng, info, bucket_cap_mb=0.05, force_reduce=(name != "plain"))
-        assert (eng.wgrad_fence_hook is not None) == (name == "rccl_fence")
         if name == "plain":
             assert run.reducer is None
         else:
@@ -121,11 +117,10 @@ def _rccl_worker(rank, port, out_dir):
 def test_rccl_reducer_eager_and_captured_bitwise(tmp_path):
     mp.spawn(_rccl_worker, args=(_port(), str(tmp_path)), nprocs=1, join=True)
     r = torch.load(tmp_path / "rccl.pt", weights_only=True)
-    for k in ("plain", "rccl_eager", "rccl_graph", "rccl_fence"):
+    for k in ("plain", "rccl_eager", "rccl_graph"):
         assert r[k + "_step"] == 3.0
     assert torch.equal(r["plain"], r["rccl_eager"])
     assert torch.equal(r["plain"], r["rccl_graph"])
-    assert torch.equal(r["plain"], r["rccl_fence"])
     assert r["plain_loss"] == r["rccl_graph_loss"]
 
 

@@ -22,7 +22,7 @@ def _port():
 
 def _run(out, fault_env=None):
     env = dict(os.environ, OMP_NUM_THREADS="1")
-    env.pop("VINF_FAULT_STEP", None)
+    env.pop("VINF_FAULT", None)
     if fault_env:
         env.update(fault_env)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
@@ -37,8 +37,7 @@ def _run(out, fault_env=None):
 
 def test_rank_loss_restart_resumes_bitwise(tmp_path):
     _, clean = _run(tmp_path / "clean")
-    p, faulted = _run(tmp_path / "faulted", {"VINF_FAULT_STEP": "6", "VINF_FAULT_RANK": "1",
-                                              "VINF_FAULT_KIND": "exit"})
+    p, faulted = _run(tmp_path / "faulted", {"VINF_FAULT": "exit:6:1"})
     log = p.stdout + p.stderr
     assert "resumed from" in log                       # the restarted attempt loaded step 4
     assert int(clean["engine"]["step"]) == int(faulted["engine"]["step"]) == 12
@@ -53,13 +52,13 @@ def test_rank_loss_restart_resumes_bitwise(tmp_path):
 def test_fault_arming():
     from vi_normflows_amd.utils.faults import armed
 
-    os.environ.update(VINF_FAULT_STEP="3", VINF_FAULT_RANK="0", VINF_FAULT_KIND="nan")
+    os.environ.update(VINF_FAULT="nan:3:0")
     try:
         assert armed(3, 0) == "nan" and armed(3, 1) is None and armed(2, 0) is None
         os.environ["TORCHELASTIC_RESTART_COUNT"] = "1"      # restarted attempts run clean
         assert armed(3, 0) is None
     finally:
-        for k in ("VINF_FAULT_STEP", "VINF_FAULT_RANK", "VINF_FAULT_KIND", "TORCHELASTIC_RESTART_COUNT"):
+        for k in ("VINF_FAULT", "TORCHELASTIC_RESTART_COUNT"):
             os.environ.pop(k, None)
 
 

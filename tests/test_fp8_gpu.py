@@ -112,9 +112,9 @@ def test_gemm_fp8_fused_output_quantisation(gpu):
 
 @pytest.fixture
 def force256():
-    torch.ops.vinf.gemm_set_mode(2, 4)
+    torch.ops.vinf.gemm_set_mode(2)
     yield
-    torch.ops.vinf.gemm_set_mode(0, 4)
+    torch.ops.vinf.gemm_set_mode(0)
 
 
 @pytest.mark.parametrize("M,N,K", [(512, 512, 256), (1000, 272, 384), (2048, 1024, 1024)])

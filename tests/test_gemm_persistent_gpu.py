@@ -205,7 +205,7 @@ def test_engine_persistent_forward_only_bitwise(gpu):
 
 def test_wgrad_xcd_packing_bitwise(gpu):
     """The weight-gradient launches pack each problem's tiles into one XCD's block range
-    (gemm256.hip, VINF_WGRAD_XCD_PACK): a permutation of which block computes which tile, so
+    (gemm256.hip, gemm_wgrad_xcd_pack): a permutation of which block computes which tile, so
     every gradient is bitwise equal to the unpacked order. RealNVP-8 at B = 16384: 320 tiles
     in launches of one tile per CU, problems of 16 / 16 / 8 tiles straddling the bins."""
     from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI

@@ -245,3 +245,31 @@ def test_profiling_hooks(tmp_path):
     assert "flow_backward" in table and "optimizer" in table
     assert (tmp_path / "trace.json").exists() and not profiling.enabled()
     assert profiling.debug_env()["HIP_LAUNCH_BLOCKING"] == "1"
+
+
+def test_train_cli_closes_its_runners(tmp_path, monkeypatch):
+    """Every DataParallelRunner a train.py task creates is closed when the task returns, so the
+    process-global multi-rank GEMM policy a runner holds never outlives the run."""
+    from vi_normflows_amd.parallel import runner as R
+    from vi_normflows_amd.train import _RUNNER_STACKS, main
+
+    made, closed = [], []
+    orig_init, orig_close = R.DataParallelRunner.__init__, R.DataParallelRunner.close
+
+    def init(self, *a, **k):
+        made.append(self)
+        orig_init(self, *a, **k)
+
+    def close(self):
+        closed.append(self)
+        orig_close(self)
+
+    monkeypatch.setattr(R.DataParallelRunner, "__init__", init)
+    monkeypatch.setattr(R.DataParallelRunner, "close", close)
+    main(["--config", "config2_realnvp8", "device=cpu", "iters=2", "batch=16", "dim=8",
+          "hidden=16", "log_every=1", f"out_dir={tmp_path}"])
+    main(["--config", "config5_maf64", "device=cpu", "iters=2", "batch=32", "dim=16",
+          "hidden=32", "K=2", "log_every=1", f"out_dir={tmp_path}"])
+    assert len(made) == 2 and [id(r) for r in made] == [id(r) for r in closed]
+    assert not _RUNNER_STACKS
+    assert R._POLICY["refs"] == 0

@@ -64,7 +64,7 @@ def _made_ref(made, x, c, w):
 
 
 @pytest.mark.parametrize("n_hidden,ctx_dim", [(1, 32), (2, 0), (1, 0)])
-def test_fused_made_matches_per_layer(gpu, monkeypatch, n_hidden, ctx_dim):
+def test_fused_made_matches_per_layer(gpu, monkeypatch, n_hidden, ctx_dim, kpaths):
     """Fused MADE vs the per-layer path and fp32 torch. Both bf16 paths sit a few % from fp32
     in the input gradients: a hidden pre-activation within bf16 rounding of 0 flips its ReLU
     gate (measured 3.3 % per-layer vs 4.1 % fused on this case), so the bound is relative to
@@ -79,12 +79,12 @@ def test_fused_made_matches_per_layer(gpu, monkeypatch, n_hidden, ctx_dim):
     x = torch.randn(256, 64, device=gpu)
     c = torch.randn(256, ctx_dim, device=gpu) if ctx_dim else None
     w = torch.randn(256, 2, 64, device=gpu)
-    monkeypatch.setenv("VINF_MADE_FUSED", "1")
+    kpaths(made_fused=1)
     assert made_fused.supported(made, x, c)
     oR, gxR, gcR = _made_ref(made, x, c, w.reshape(256, 128))
     res = {}
     for fused in ("1", "0"):
-        monkeypatch.setenv("VINF_MADE_FUSED", fused)
+        kpaths(made_fused=int(fused))
         made.zero_grad(set_to_none=True)
         xr = x.clone().requires_grad_(True)
         cr = c.clone().requires_grad_(True) if c is not None else None
@@ -105,7 +105,7 @@ def test_fused_made_matches_per_layer(gpu, monkeypatch, n_hidden, ctx_dim):
         assert (L.weight.grad[L.mask == 0] == 0).all()
 
 
-def test_fused_iaf_layer_matches_per_layer(gpu, monkeypatch):
+def test_fused_iaf_layer_matches_per_layer(gpu, monkeypatch, kpaths):
     torch.manual_seed(5)
     iaf = IAF(64, 128, 1, context_dim=32, reverse=True).to(gpu)
     with torch.no_grad():
@@ -116,7 +116,7 @@ def test_fused_iaf_layer_matches_per_layer(gpu, monkeypatch):
     h = torch.randn(512, 32, device=gpu)
     res = []
     for fused in ("1", "0"):
-        monkeypatch.setenv("VINF_MADE_FUSED", fused)
+        kpaths(made_fused=int(fused))
         iaf.zero_grad(set_to_none=True)
         zr, hr = z.clone().requires_grad_(True), h.clone().requires_grad_(True)
         y, ldj = iaf(zr, hr)
@@ -132,7 +132,7 @@ def test_fused_iaf_layer_matches_per_layer(gpu, monkeypatch):
         assert _rel(a, b) < 6e-2
 
 
-def test_iaf_vae_loss_fused_matches_per_layer(gpu, monkeypatch):
+def test_iaf_vae_loss_fused_matches_per_layer(gpu, monkeypatch, kpaths):
     from vi_normflows_amd.models.iaf_vae import IAFVAE, IAFVAEConfig, synthetic_images
 
     cfg = IAFVAEConfig(image_shape=(1, 16, 16), dim_z=64, hidden=256, context=64, n_flows=4,
@@ -141,7 +141,7 @@ def test_iaf_vae_loss_fused_matches_per_layer(gpu, monkeypatch):
     x = synthetic_images(256, shape=(1, 16, 16), device=gpu)
     vals = []
     for fused in ("1", "0"):
-        monkeypatch.setenv("VINF_MADE_FUSED", fused)
+        kpaths(made_fused=int(fused))
         model.zero_grad(set_to_none=True)
         g = torch.Generator(device=gpu).manual_seed(11)
         F = model.loss(x, generator=g, with_stats=False).F
@@ -154,7 +154,7 @@ def test_iaf_vae_loss_fused_matches_per_layer(gpu, monkeypatch):
     assert _rel(tot1, tot0) < 6e-2
 
 
-def test_fused_made_fp8_forward_matches_per_layer(gpu, monkeypatch):
+def test_fused_made_fp8_forward_matches_per_layer(gpu, monkeypatch, kpaths):
     """fp8 MADE layers (e4m3 forward, bf16 backward) through the fused node vs per-layer
     MaskedLinear: same quantisation (delayed activation scale, per-row weight scales)."""
     from vi_normflows_amd.flows.made import set_precision
@@ -165,7 +165,7 @@ def test_fused_made_fp8_forward_matches_per_layer(gpu, monkeypatch):
     x = torch.randn(512, 256, device=gpu)
     res = []
     for fused in ("1", "0"):
-        monkeypatch.setenv("VINF_MADE_FUSED", fused)
+        kpaths(made_fused=int(fused))
         for L in made.layers:
             L.__dict__.pop("_fp8_scale", None)
         made.zero_grad(set_to_none=True)
@@ -182,7 +182,7 @@ def test_fused_made_fp8_forward_matches_per_layer(gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp8"])
-def test_fused_maf_inverse_matches_per_layer(gpu, monkeypatch, precision):
+def test_fused_maf_inverse_matches_per_layer(gpu, monkeypatch, precision, kpaths):
     """MAF density direction through the fused node (MADE + maf_fwd / maf_bwd with a per-row
     log-det gradient) vs the per-layer path."""
     from vi_normflows_amd.flows.made import MAF, set_precision
@@ -198,7 +198,7 @@ def test_fused_maf_inverse_matches_per_layer(gpu, monkeypatch, precision):
     wl = torch.randn(512, device=gpu)           # per-row log-det weights
     res = []
     for fused in ("1", "0"):
-        monkeypatch.setenv("VINF_MADE_FUSED", fused)
+        kpaths(made_fused=int(fused))
         for L in maf.made.layers:
             L.__dict__.pop("_fp8_scale", None)
         maf.zero_grad(set_to_none=True)

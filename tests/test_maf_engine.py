@@ -2,6 +2,8 @@
 model; masked weights stay exactly zero; NLL decreases toward the data entropy."""
 import math
 
+import dataclasses
+
 import pytest
 import torch
 
@@ -98,18 +100,18 @@ def test_engine_gpu_matches_cpu_and_trains(gpu, precision):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("tile", [0, 2], ids=["auto", "force256"])
-def test_engine_deferred_masked_wgrad_and_256_kernels(gpu, tile, monkeypatch):
+def test_engine_deferred_masked_wgrad_and_256_kernels(gpu, tile, monkeypatch, kpaths):
     """Masked products on the 256x256 kernels (per-tile K ranges) and the deferred multi-layer
     weight gradients (entirely-masked tiles never launched, dense mask in the epilogue) ==
     the per-layer 128x128 split-K schedule; masked gradient entries exactly zero."""
     cfg = MAFEngineConfig(dim=512, n_layers=3, hidden=768, init_out_std=0.3, precision="bf16")
     x = torch.randn(512, 512, generator=torch.Generator().manual_seed(3)).to(gpu)
-    torch.ops.vinf.gemm_set_mode(tile, 4)
+    torch.ops.vinf.gemm_set_mode(tile)
     try:
         a = MAFEngine(cfg, batch=512, device=gpu, seed=7)
         a._wchunk = 5                       # chunks straddle problems and layers
-        monkeypatch.setenv("VINF_WGRAD_DEFER", "0")
-        torch.ops.vinf.gemm_set_mode(1 if tile == 0 else tile, 4)
+        kpaths(wgrad_defer=0)
+        torch.ops.vinf.gemm_set_mode(1 if tile == 0 else tile)
         b = MAFEngine(cfg, batch=512, device=gpu, seed=7)
         assert a.wgrad_defer and not b.wgrad_defer
         fired = []
@@ -121,7 +123,7 @@ def test_engine_deferred_masked_wgrad_and_256_kernels(gpu, tile, monkeypatch):
             e.backward()
         torch.cuda.synchronize()
     finally:
-        torch.ops.vinf.gemm_set_mode(0, 4)
+        torch.ops.vinf.gemm_set_mode(0)
     assert fired == [2, 1, 0]
     ga, gb = a.params.grad, b.params.grad
     assert torch.isfinite(ga).all()
@@ -133,14 +135,14 @@ def test_engine_deferred_masked_wgrad_and_256_kernels(gpu, tile, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_engine_masked_dgrad_nt_matches_nn(gpu, monkeypatch):
-    """Masked input gradients against (W*M)^T (NT, VINF_DGRAD_NT=1) == the NN path."""
+def test_engine_masked_dgrad_nt_matches_nn(gpu, monkeypatch, kpaths):
+    """Masked input gradients against (W*M)^T (NT, KernelPaths.dgrad_nt) == the NN path."""
     from vi_normflows_amd.models.maf_engine import MAFEngine, MAFEngineConfig
 
     cfg = MAFEngineConfig(dim=256, hidden=512, n_layers=3, precision="bf16")
-    monkeypatch.setenv("VINF_MAF_FUSE", "0")      # both on the separate MAF kernels
+    kpaths(maf_fuse=0)      # both on the separate MAF kernels
     a = MAFEngine(cfg, batch=512, device=gpu, seed=4)
-    monkeypatch.setenv("VINF_DGRAD_NT", "0")
+    kpaths(dgrad_nt=0)
     b = MAFEngine(cfg, batch=512, device=gpu, seed=4)
     assert a.wt_dgrad and not b.wt_dgrad
     for e in (a, b):
@@ -155,9 +157,11 @@ def test_engine_masked_dgrad_nt_matches_nn(gpu, monkeypatch):
 def _fused_vs_separate(gpu, monkeypatch, cfg, batch, seed=4):
     from vi_normflows_amd.models.maf_engine import MAFEngine
 
+    from vi_normflows_amd.utils.config import KernelPaths
+
     a = MAFEngine(cfg, batch=batch, device=gpu, seed=seed)
-    monkeypatch.setenv("VINF_MAF_FUSE", "0")
-    b = MAFEngine(cfg, batch=batch, device=gpu, seed=seed)
+    b = MAFEngine(dataclasses.replace(cfg, paths=KernelPaths(maf_fuse=False)), batch=batch,
+                  device=gpu, seed=seed)
     assert a.fuse and not b.fuse
     x = torch.randn(batch, cfg.dim, generator=torch.Generator().manual_seed(seed + 1)).to(gpu)
     for e in (a, b):
@@ -175,7 +179,7 @@ def _fused_vs_separate(gpu, monkeypatch, cfg, batch, seed=4):
 @pytest.mark.parametrize("precision", ["bf16", "fp8"])
 def test_engine_fused_maf_transforms_match_separate_kernels(gpu, monkeypatch, precision):
     """The MAF transform in the second MADE product's epilogue and the MAF backward in the first
-    product's input-gradient epilogue (VINF_MAF_FUSE=1) == the separate maf_fwd / maf_bwd
+    product's input-gradient epilogue (KernelPaths.maf_fuse) == the separate maf_fwd / maf_bwd
     kernels: u_L, log-det, loss and every gradient (the epilogues see the same bf16 [mu | s_raw]
     the separate kernels read back; the difference is fast_tanhf vs tanhf, ~1e-6 relative)."""
     cfg = MAFEngineConfig(dim=256, hidden=512, n_layers=3, precision=precision, init_out_std=0.3)
@@ -210,15 +214,15 @@ def test_engine_fused_maf_paired_tiles_headline_width(gpu, monkeypatch, precisio
 @pytest.mark.gpu
 @pytest.mark.parametrize("dim,hidden,batch", [(256, 512, 1024), (1024, 1024, 16384)],
                          ids=["small", "config5_width"])
-def test_engine_fp8_input_gradients(gpu, monkeypatch, dim, hidden, batch):
+def test_engine_fp8_input_gradients(gpu, monkeypatch, dim, hidden, batch, kpaths):
     """fp8 engine with e4m3 input-gradient products (after a bf16 bootstrap step seeds the
     gradients' delayed scales) vs the same engine with bf16 input gradients, same weights and
     data: the loss is the same forward, the gradient differs by the e4m3 rounding of dO / dH /
     (W*M)^T only (3 mantissa bits: ~3 % per product, averaged over the reduction)."""
     cfg = MAFEngineConfig(dim=dim, hidden=hidden, n_layers=4, precision="fp8", init_out_std=0.3)
-    monkeypatch.setenv("VINF_FP8_WGRAD", "0")      # input gradients only (weight gradients: below)
+    kpaths(fp8_wgrad=0)      # input gradients only (weight gradients: below)
     a = MAFEngine(cfg, batch=batch, device=gpu, seed=4)
-    monkeypatch.setenv("VINF_FP8_DGRAD", "0")
+    kpaths(fp8_dgrad=0)
     b = MAFEngine(cfg, batch=batch, device=gpu, seed=4)
     assert a.fp8_bwd and not b.fp8_bwd and not a.f8_wgrad
     x = torch.randn(batch, dim, generator=torch.Generator().manual_seed(9)).to(gpu)
@@ -247,14 +251,14 @@ def test_engine_fp8_input_gradients(gpu, monkeypatch, dim, hidden, batch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("dim,hidden,batch", [(256, 512, 1024), (1024, 1024, 16384)],
                          ids=["small", "config5_width"])
-def test_engine_fp8_weight_gradients(gpu, monkeypatch, dim, hidden, batch):
+def test_engine_fp8_weight_gradients(gpu, monkeypatch, dim, hidden, batch, kpaths):
     """e4m3 weight gradients (per-layer e4m3 copies of x / h / dO / dH, the e4m3 TN multi-layer
     launch, bias gradients by fp8_colsum) vs the same fp8 engine with bf16 weight gradients:
     same loss, gradients apart by the e4m3 rounding of the weight-gradient operands only,
     masked weights' gradients exactly zero, every bias gradient close."""
     cfg = MAFEngineConfig(dim=dim, hidden=hidden, n_layers=4, precision="fp8", init_out_std=0.3)
     a = MAFEngine(cfg, batch=batch, device=gpu, seed=4)
-    monkeypatch.setenv("VINF_FP8_WGRAD", "0")
+    kpaths(fp8_wgrad=0)
     b = MAFEngine(cfg, batch=batch, device=gpu, seed=4)
     assert a.f8_wgrad and b.fp8_bwd and not b.f8_wgrad
     x = torch.randn(batch, dim, generator=torch.Generator().manual_seed(9)).to(gpu)

@@ -71,14 +71,14 @@ def test_masked_dgrad_two_k_ranges_256(gpu, order):
     dy = torch.randn(B, 2 * D, device=gpu).to(torch.bfloat16)
     h = torch.randn(B, H, device=gpu).to(torch.bfloat16)
     ref = (dy.float() @ W.float()) * (h.float() > 0)
-    torch.ops.vinf.gemm_set_mode(2, 4)
+    torch.ops.vinf.gemm_set_mode(2)
     try:
         out = torch.empty(B, H, device=gpu, dtype=torch.bfloat16)
         torch.ops.vinf.masked_gemm_nn(dy, W, h, out, plan.bwd, False, plan.bwd256)
         acc = torch.full((B, H), 1.0, device=gpu)
         torch.ops.vinf.masked_gemm_nn(dy, W, None, acc, plan.bwd, True, plan.bwd256)
     finally:
-        torch.ops.vinf.gemm_set_mode(0, 4)
+        torch.ops.vinf.gemm_set_mode(0)
     err = (out.float() - ref).abs().max().item()
     assert err <= 1e-2 * ref.abs().max().item(), err
     ref2 = dy.float() @ W.float() + 1.0
@@ -90,16 +90,18 @@ def _pair_env_subprocess(code: str):
     import subprocess
     import sys
 
-    env = dict(os.environ, VINF_GEMM_PAIR="2", VINF_GEMM_TILE="256")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
-                       timeout=300)
+    # column-tile pairing forced on (gemm_pair(2)) and the 256x256 kernels (gemm_set_mode(2)), in
+    # a process of its own so no other test sees the settings
+    code = code.replace("\nnative()\n", "\nnative()\nnative().gemm_pair(2)\nnative().gemm_set_mode(2)\n", 1)
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ), capture_output=True,
+                       text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "OK" in r.stdout, r.stdout
 
 
 def test_masked_paired_column_tiles_256(gpu):
     """Paired column tiles per block (descending K-length rank p with ntn-1-p; forced on
-    through VINF_GEMM_PAIR=2, read once per process): masked fwd (bf16 and e4m3) and two-range
+    through gemm_pair(2)): masked fwd (bf16 and e4m3) and two-range
     dgrad equal the dense products of the masked weights."""
     _pair_env_subprocess('''
 import torch

@@ -1,5 +1,6 @@
-"""GPU ``nn.Module`` model paths run their dense products on the MFMA kernels: ``MfmaLinear``
-matches an fp32 ``F.linear`` oracle (forward and all three gradients) on awkward shapes, and a
+"""GPU ``nn.Module`` model paths run their dense products on the matrix-core kernels:
+``MfmaLinear`` keeps an fp32 / fp64 model in its own precision (f32 / f64 MFMA, vs an fp64
+oracle), runs bf16 operands with fp32 outputs when asked (``precision="bf16"``), and a
 forward + backward of the coupling, flat-MLP, IAF-VAE and latent-model modules never reaches
 ``torch.mm`` / ``F.linear`` / ``@`` (those are trapped for the duration)."""
 import contextlib
@@ -11,31 +12,88 @@ import torch.nn.functional as F
 from vi_normflows_amd.ops.linear import MfmaLinear, linear
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("M,K,N", [(37, 5, 3), (128, 392, 1024), (256, 64, 40), (1, 2, 2),
-                                   (1000, 784, 200)])
-def test_mfma_linear_matches_fp32_oracle(gpu, M, K, N):
+SHAPES = [(37, 5, 3), (128, 392, 1024), (256, 64, 40), (1, 2, 2), (1000, 784, 200)]
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-300))
+
+
+def _run(gpu, M, K, N, dtype, precision):
     g = torch.Generator(device="cpu").manual_seed(M + K + N)
-    x = torch.randn(M, K, generator=g).to(gpu).requires_grad_(True)
-    lin = MfmaLinear(K, N).to(gpu)
+    x = torch.randn(M, K, generator=g, dtype=torch.float64).to(gpu, dtype).requires_grad_(True)
+    lin = MfmaLinear(K, N, precision=precision).to(gpu, dtype)
     y = lin(x)
-    gy = torch.randn(M, N, generator=g).to(gpu)
+    gy = torch.randn(M, N, generator=g, dtype=torch.float64).to(gpu, dtype)
     y.backward(gy)
-    xr = x.detach().clone().requires_grad_(True)
-    Wr = lin.weight.detach().clone().requires_grad_(True)
-    br = lin.bias.detach().clone().requires_grad_(True)
-    yr = F.linear(xr.double(), Wr.double(), br.double())
+    xr = x.detach().double().requires_grad_(True)
+    Wr = lin.weight.detach().double().requires_grad_(True)
+    br = lin.bias.detach().double().requires_grad_(True)
+    yr = F.linear(xr, Wr, br)
     yr.backward(gy.double())
+    return (y, x.grad, lin.weight.grad, lin.bias.grad), (yr, xr.grad, Wr.grad, br.grad)
 
-    def rel(a, b):
-        return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-12))
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,K,N", SHAPES)
+def test_fp32_module_layer_is_full_precision(gpu, M, K, N):
+    """An fp32 model keeps fp32 arithmetic (gemm_fp.hip, f32 MFMA): output and all three
+    gradients within 1e-5 relative of the fp64 oracle - no silent bf16 rounding."""
+    from vi_normflows_amd.ops.linear import precision_counts
+
+    precision_counts(reset=True)
+    got, ref = _run(gpu, M, K, N, torch.float32, None)
+    assert got[0].dtype == torch.float32 and got[0].shape == (M, N)
+    for a, b in zip(got, ref):
+        assert _rel(a, b) < 1e-5
+    assert precision_counts()["fp32"] == 1 and precision_counts()["bf16"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,K,N", SHAPES[:3])
+def test_fp64_module_layer_matches_fp64(gpu, M, K, N):
+    got, ref = _run(gpu, M, K, N, torch.float64, None)
+    assert got[0].dtype == torch.float64
+    for a, b in zip(got, ref):
+        assert _rel(a, b) < 1e-12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,K,N", SHAPES)
+def test_bf16_opt_in_layer(gpu, M, K, N):
+    """precision="bf16": bf16 operands, fp32 accumulator stored unrounded (fp32 output)."""
+    got, ref = _run(gpu, M, K, N, torch.float32, "bf16")
+    assert got[0].dtype == torch.float32
     # bf16 operands (u = 2^-8) with fp32 accumulation: ~K^0.5 u relative error at worst
-    assert y.dtype == torch.float32 and y.shape == (M, N)
-    assert rel(y, yr) < 1e-2
-    assert rel(x.grad, xr.grad) < 1e-2
-    assert rel(lin.weight.grad, Wr.grad) < 1e-2
-    assert rel(lin.bias.grad, br.grad) < 1e-2
+    for a, b in zip(got, ref):
+        assert _rel(a, b) < 1e-2
+
+
+@pytest.mark.gpu
+def test_latent_model_log_joint_and_grad_fp32(gpu):
+    """The latent models' ELBO integrand in fp32 on the GPU - the encoder's dense layers and
+    the log-joint's x = A z + B divided by the likelihood variance - and its parameter gradient
+    agree with an fp64 run of the same module to 1e-5 / 1e-4 relative (the bf16 module path of
+    round 4 rounded xhat to bf16 here)."""
+    from vi_normflows_amd.models.latent import LinearGaussianLatent
+
+    torch.manual_seed(3)
+    lat = LinearGaussianLatent(dim_x=6, dim_z=2, K=2, hidden=16)
+    x = torch.randn(256, 6, dtype=torch.float64) * 3 + 5
+    z = torch.randn(256, 2, dtype=torch.float64)
+    outs = {}
+    for dt in (torch.float32, torch.float64):
+        m = LinearGaussianLatent(dim_x=6, dim_z=2, K=2, hidden=16).to(gpu, dt)
+        m.load_state_dict({k: v.to(dt) for k, v in lat.state_dict().items()})
+        xg, zg = x.to(gpu, dt), z.to(gpu, dt)
+        mu, lv, (W, U, b) = m.encoder(xg)
+        val = m.log_joint(xg, zg + mu * torch.exp(0.5 * lv)).mean() + (W * U).sum() + b.sum()
+        val.backward()
+        outs[dt] = (val.detach().double(),
+                    torch.cat([p.grad.double().flatten() for p in m.parameters() if p.grad is not None]))
+    (f32, g32), (f64, g64) = outs[torch.float32], outs[torch.float64]
+    assert _rel(f32, f64) < 1e-5
+    assert _rel(g32, g64) < 1e-4
 
 
 @contextlib.contextmanager

@@ -257,7 +257,14 @@ def main(argv=None):
     ap.add_argument("--cpu", action="store_true", help="config 0 on the CPU")
     ap.add_argument("--impl", default="engine", choices=["engine", "module"],
                     help="configs 4 / 5: explicit-backward IAF / MAF engine or the autograd modules")
+    ap.add_argument("--dense-precision", default=None, choices=["auto", "fp32", "bf16"],
+                    help="module paths: precision of the dense (MfmaLinear) layers; default: "
+                         "config 4 bf16 (its label), otherwise the model dtype's own (fp32)")
     a = ap.parse_args(argv)
+    from ..ops.linear import precision_counts, set_default_precision
+
+    dense = a.dense_precision or ("bf16" if a.config == 4 else "auto")
+    set_default_precision(dense)
     info = vdist.init(device_type="cpu" if a.config == 1 or (a.config == 0 and a.cpu) else None)
     step, B, dev, dtype = build(a.config, info, a.batch, a.precision, a.graph == "on", a.impl)
     for _ in range(a.warmup):
@@ -271,9 +278,12 @@ def main(argv=None):
     vdist.barrier()
     dt = vdist.all_reduce_max(time.perf_counter() - t0)
     if info.is_main:
+        # dense-layer precision actually taken by the module paths (forward calls per path)
         print(json.dumps({"config": a.config, "name": NAMES[a.config], "n_ranks": info.world,
                           "per_rank_batch": B, "ms_per_step": 1000 * dt / a.steps,
-                          "samples_per_s": B * info.world * a.steps / dt, "dtype": dtype}))
+                          "samples_per_s": B * info.world * a.steps / dt, "dtype": dtype,
+                          "impl": a.impl, "dense_precision": dense,
+                          "dense_calls": precision_counts()}))
     vdist.shutdown()
 
 

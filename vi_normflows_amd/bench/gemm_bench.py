@@ -136,9 +136,9 @@ def main():
                 for m in res:
                     mode = 1 if m == "128" else (3 if m.startswith("256t") else
                                                  (2 if m.startswith("256") else 0))
-                    ops.gemm_set_mode(mode, 6 if m.endswith("d6") else 4)
+                    ops.gemm_set_mode(mode)
                     res[m].append(_time(mine, a.iters))
-            ops.gemm_set_mode(0, 4)
+            ops.gemm_set_mode(0)
             rec = {"shape": name, "M": M, "N": N, "K": K}
             for m, ts in res.items():
                 rec[f"{m}_us"] = round(min(ts) * 1e6, 1)

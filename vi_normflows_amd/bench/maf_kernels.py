@@ -92,24 +92,6 @@ def main():
         a.reps)
     out["maf_bwd"] = timeit(lambda: fused.maf_bwd(e.gU, e.X[l], O, e.dOL[l - 1], e.gX,
                                                    bound=bound, c_ldj=1.0 / B), a.reps)
-    os.environ["VINF_PAIR_ALT"] = "1"
-    out["alt_fwd2_fp8_fused"] = timeit(lambda: native().maf_gemm_fwd(
-        e.Hq, sh, W2q, s2, b2, mk["P2pair"], e.S[l], e.X[l], e.X[l + 1], e.Xbf[l + 1], e.ldjp,
-        False, bound, e.Xq, nx.amax[0:1], nx.scale, nx.cur), a.reps)
-    out["alt_fwd2_bf16_fused"] = timeit(lambda: native().maf_gemm_fwd(
-        e.Hbf[l], None, P.c(f"l{l}.W2"), None, b2, mk["P2pair"], e.S[l], e.X[l], e.X[l + 1],
-        e.Xbf[l + 1], e.ldjp, False, bound), a.reps)
-    out["alt_dgrad1_fp8_fused"] = timeit(lambda: native().maf_gemm_bwd(
-        e.dHq, e.W1Tq[l * D:(l + 1) * D], mk["P1"].bwd256, e.gX, e.S[l - 1], e.X[l],
-        e.dOL[l - 1], e.gU, bound, 1.0 / B, sdh.scale, e.sW1T[l * D:(l + 1) * D], e.dOq,
-        nd.amax[0:1], nd.scale, nd.cur), a.reps)
-    out["alt_dgrad1_bf16_fused"] = timeit(lambda: native().maf_gemm_bwd(
-        e.dHL[l], WT[l][0], mk["P1"].bwd256, e.gX, e.S[l - 1], e.X[l], e.dOL[l - 1], e.gU,
-        bound, 1.0 / B), a.reps)
-    out["alt_fwd2_fp8_gemm"] = timeit(lambda: gemm_fp8(e.Hq, sh, W2q, s2, b2, relu=False,
-                                                        krange=mk["P2"].fwd, out=O,
-                                                        krange256=mk["P2"].fwd256), a.reps)
-    os.environ["VINF_PAIR_ALT"] = "0"
     print(json.dumps({"batch": B, "us": {k: round(v, 1) for k, v in out.items()}}))
 
 

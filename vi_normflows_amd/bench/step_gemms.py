@@ -5,7 +5,7 @@ gradient with the fused coupling backward), random operands, min / median over i
 
     python -m vi_normflows_amd.bench.step_gemms [--batch 65536] [--iters 20] [--out f.jsonl]
 
-Environment switches of the GEMM launchers (VINF_G256_PERSIST, VINF_G256_DESYNC, ...) apply,
+The GEMM launchers' runtime settings (gemm_persist, gemm_set_mode, ...) apply,
 so A/B arms are separate invocations on the same box.
 """
 from __future__ import annotations
@@ -55,16 +55,6 @@ def build(B: int, dev):
     ldjp = torch.empty((Dh + 127) // 128, B, device=dev)
     fns["cpl_fwd"] = (lambda: gemm.linear_fwd_coupling(h2, W3, b3, st, x, y, yb, ldjp, True, 1.0),
                       2.0 * B * 2 * Dh * H)
-    # probe: the last 8 features through cpl_edge_fwd_kernel instead of the fused edge tile
-
-    def cpl_edge_kernel():
-        from ..ops._ext import native
-
-        prev = native().gemm_cpl_edge(1)
-        gemm.linear_fwd_coupling(h2, W3, b3, st, x, y, yb, ldjp, True, 1.0)
-        native().gemm_cpl_edge(prev)
-
-    fns["cpl_fwd_edge_kernel"] = (cpl_edge_kernel, 2.0 * B * 2 * Dh * H)
     # probe: the same product with Dh = 384 features (3 whole 128-feature column tiles, no
     # 8-feature edge tile) - what the edge tile costs
     D3 = 384
@@ -107,7 +97,7 @@ def main(argv=None):
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default=None)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--tag", default=os.environ.get("VINF_BENCH_TAG", ""))
+    ap.add_argument("--tag", default="")
     a = ap.parse_args(argv)
     dev = torch.device("cuda")
     fns = build(a.batch, dev)

@@ -170,13 +170,12 @@ def layout_probe(B: int, layers: int, iters: int, tag: str, dev, pad: int = 0,
                           "max_rel_diff_vs_layout0": err}), flush=True)
 
 
-def nt_probe(B: int, iters: int, tag: str, dev):
+def nt_probe(B: int, iters: int, tag: str, dev, masks_only: bool = False):
     """The forward products of the headline step (x [B, K] bf16 times W [N, K]^T, bias + ReLU +
     bitmask or plain) and the bitmask input gradient (dy [B, 1024] times Wt^T): the 8-wave
     persistent 256x256 kernel with the activation operand real vs stride-0 (every row the same
-    K-vector, so its LDS-DMA stream always hits L2; W is 2 MiB and always does), and the 4-wave
-    kernel (gemm_nt4w.hip) on the real operands with its outputs checked bitwise against the
-    8-wave ones."""
+    K-vector, so its LDS-DMA stream always hits L2; W is 2 MiB and always does). (A 4-wave NT
+    kernel measured here in round 4 was slower on every shape: profiles/r4/nt4w_probe.jsonl.)"""
     from ..ops import gemm
     from ..ops._ext import native
 
@@ -204,8 +203,7 @@ def nt_probe(B: int, iters: int, tag: str, dev):
         d.update(extra or {})
         print(json.dumps(d), flush=True)
 
-    only = os.environ.get("VINF_NT_PROBE_MASKS")   # "1": the ReLU-mask split only
-    if only:
+    if masks_only:   # the ReLU-mask split only
         K = N = 1024
         x = torch.randn(B, K, device=dev, generator=g).to(bf)
         W = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(bf)
@@ -227,20 +225,10 @@ def nt_probe(B: int, iters: int, tag: str, dev):
         flops = 2.0 * B * N * K
         name = f"nt_K{K}_N{N}_{'relu' if relu else 'plain'}"
         ref = None
-        for arm, xin, w4 in (("a_real", x, 0), ("a_cached", x0, 0), ("nt4w", x, 1)):
-            prev = native().gemm_nt4w(w4)
-            try:
-                t = timeit(lambda: gemm.linear_fwd(xin, W, bias, out, relu=relu, mask_out=bits))
-                extra = {}
-                if arm == "a_real":
-                    ref = (out.clone(), bits.clone() if bits is not None else None)
-                elif arm == "nt4w":
-                    extra["bitwise_vs_8wave"] = bool(torch.equal(out, ref[0]) and (
-                        bits is None or torch.equal(bits, ref[1])))
-            finally:
-                native().gemm_nt4w(prev)
-            emit(f"{name}_{arm}", flops, t, extra)
-        del x, out, bits, ref
+        for arm, xin in (("a_real", x), ("a_cached", x0)):
+            t = timeit(lambda: gemm.linear_fwd(xin, W, bias, out, relu=relu, mask_out=bits))
+            emit(f"{name}_{arm}", flops, t)
+        del x, out, bits
 
     # bitmask input gradient dh = (dy Wt^T) * 1(bits), K = N = 1024 (NT through Wt)
     K = N = 1024
@@ -249,19 +237,8 @@ def nt_probe(B: int, iters: int, tag: str, dev):
     Wt = W.t().contiguous()
     rb = torch.randint(0, 256, (B, N // 8), device=dev, generator=g, dtype=torch.int32).to(torch.uint8)
     dh = torch.empty(B, N, device=dev, dtype=bf)
-    ref = None
-    for arm, w4 in (("8wave", 0), ("nt4w", 1)):
-        prev = native().gemm_nt4w(w4)
-        try:
-            t = timeit(lambda: gemm.linear_dgrad(dy, W, dh, relu_bits=rb, Wt=Wt))
-            extra = {}
-            if ref is None:
-                ref = dh.clone()
-            else:
-                extra["bitwise_vs_8wave"] = bool(torch.equal(dh, ref))
-        finally:
-            native().gemm_nt4w(prev)
-        emit(f"dgrad_bits_K{K}_N{N}_{arm}", 2.0 * B * N * K, t, extra)
+    t = timeit(lambda: gemm.linear_dgrad(dy, W, dh, relu_bits=rb, Wt=Wt))
+    emit(f"dgrad_bits_K{K}_N{N}", 2.0 * B * N * K, t)
 
 
 def main(argv=None):
@@ -269,10 +246,11 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--layers", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--tag", default=os.environ.get("VINF_BENCH_TAG", ""))
+    ap.add_argument("--tag", default="")
     ap.add_argument("--probe", action="store_true")
     ap.add_argument("--layout-probe", action="store_true")
     ap.add_argument("--nt-probe", action="store_true")
+    ap.add_argument("--nt-probe-masks", action="store_true", help="nt probe: ReLU-mask split only")
     ap.add_argument("--pitch-pad", type=int, default=0, help="layout probe: extra row elements")
     ap.add_argument("--layouts", default="0,1,2,3")
     ap.add_argument("--kchunks", type=int, default=1,
@@ -283,7 +261,7 @@ def main(argv=None):
         probe(a.batch, a.iters, a.tag, dev)
         return
     if a.nt_probe:
-        nt_probe(a.batch, a.iters, a.tag, dev)
+        nt_probe(a.batch, a.iters, a.tag, dev, a.nt_probe_masks)
         return
     if a.layout_probe:
         layout_probe(a.batch, a.layers, a.iters, a.tag, dev, a.pitch_pad,

@@ -20,6 +20,7 @@ import torch.distributed as dist
 
 from .annealing import get_schedule
 from .optimizers import make_optimizer
+from ..ops.linear import precision_counts
 
 
 @dataclass
@@ -214,6 +215,9 @@ class Trainer:
             if t % self.cfg.log_every == 0 or self.t == end:
                 rec = {"step": t, "F": res.item(), "skipped": self.n_skipped,
                        "elapsed_s": time.perf_counter() - t0, **res.stats}
+                dense = precision_counts()
+                if any(dense.values()):   # which dense-layer precision path(s) the model took
+                    rec["dense_precision"] = ",".join(k for k, v in dense.items() if v)
                 self.history.append(rec)
                 if self.logger is not None:
                     self.logger.log(rec)

@@ -29,13 +29,14 @@ entropy is the NLL floor.
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import torch
 
 from ..flows.made import made_degrees, made_masks
 from ..ops import fused
 from ..ops import gemm
+from ..utils.config import KernelPaths
 from ..utils.flat import FlatLayout, FlatParams
 from ..utils.profiling import trace_range
 
@@ -53,6 +54,9 @@ class MAFEngineConfig:
     banana_sigma1: float = 1.0
     banana_sigma2: float = 0.5
     banana_bend: float = 0.5
+    # fused / deferred kernel paths (utils.config.KernelPaths); None: the defaults, overridden
+    # by VINF_KERNEL_PATHS at engine construction
+    paths: KernelPaths | None = None
 
     def n_params(self) -> int:
         D, H = self.dim, self.hidden
@@ -150,13 +154,12 @@ class MAFEngine:
         self.X = torch.empty(L + 1, B, D, dtype=f32, device=dev)          # x_0 .. u_L
         self.Xbf = torch.empty(L + 1, B, D, dtype=self.cdt, device=dev)
         self.Hbf = torch.empty(L, B, H, dtype=self.cdt, device=dev)        # relu(h) per layer
-        import os
-
+        kp = cfg.paths if cfg.paths is not None else KernelPaths.from_env()
         # fused MAF transforms (GPU): the forward's second MADE product writes u / s_raw / the
         # log-det shares from its epilogue (no [mu | s_raw] tensor, no maf_fwd pass) and each
         # layer's first input-gradient product finishes the MAF backward of the layer below (no
-        # maf_bwd pass except at the top); VINF_MAF_FUSE=0 keeps the separate kernels
-        fuse_env = os.environ.get("VINF_MAF_FUSE", "1") != "0"
+        # maf_bwd pass except at the top); paths.maf_fuse = False keeps the separate kernels
+        fuse_env = kp.maf_fuse
 
         self.ldj = torch.empty(B, dtype=f32, device=dev)
         self.nll_row = torch.empty(B, dtype=f32, device=dev)
@@ -169,10 +172,10 @@ class MAFEngine:
         # weight gradients of several layers run as one launch of whole 256x256 tiles with the
         # full batch as K, entirely-masked tiles left out (ops.gemm.WgradPlan) - 13 GB at
         # B = 32768, nothing next to 288 GB of HBM
-        self.wgrad_defer = dev.type == "cuda" and os.environ.get("VINF_WGRAD_DEFER", "1") != "0"
+        self.wgrad_defer = dev.type == "cuda" and kp.wgrad_defer
         self._wplan = None
         # masked input gradients as NT products against a per-step (W*M)^T copy (ops.layout)
-        self.wt_dgrad = self.wgrad_defer and os.environ.get("VINF_DGRAD_NT", "1") != "0"
+        self.wt_dgrad = self.wgrad_defer and kp.dgrad_nt
         # (the fused backward is an NT product against (W*M)^T)
         self.fuse = dev.type == "cuda" and D % 128 == 0 and fuse_env and self.wt_dgrad
         if self.fuse:
@@ -201,8 +204,8 @@ class MAFEngine:
 
             # fp8 input-gradient products too (fused engine): e4m3 copies of each layer's
             # [dmu | ds_raw] and hidden gradient come from the producing epilogues under delayed
-            # scales, against e4m3 (W*M)^T with per-row scales; VINF_FP8_DGRAD=0 keeps bf16
-            self.fp8_bwd = self.fuse and os.environ.get("VINF_FP8_DGRAD", "1") != "0"
+            # scales, against e4m3 (W*M)^T with per-row scales; paths.fp8_dgrad = False: bf16
+            self.fp8_bwd = self.fuse and kp.fp8_dgrad
             self.amax_pool = torch.zeros(4 * L, 1 + AMAX_SLOTS, dtype=f32, device=dev)
             # per delayed-scale state: steps whose amax exceeded the scale it was quantised with
             # (amax_cur > amax_prev > 0: values beyond 448 * scale were clipped, the e4m3 weight
@@ -226,9 +229,9 @@ class MAFEngine:
             # e4m3 weight gradients (fp8 backward, deferred plan): every layer keeps the e4m3
             # copies of its four GEMM operands (x, h, dO, dH: 10.7 GB at B = 32768, L = 64), and
             # the weight gradients of all layers run on the e4m3 TN kernel (WgradPlan f8 form)
-            # instead of the bf16 one over bf16 copies; VINF_FP8_WGRAD=0 keeps bf16
+            # instead of the bf16 one over bf16 copies; paths.fp8_wgrad = False keeps bf16
             self.f8_wgrad = (self.fp8_bwd and self.wgrad_defer and B % 128 == 0
-                             and os.environ.get("VINF_FP8_WGRAD", "1") != "0")
+                             and kp.fp8_wgrad)
             self._wplan8 = None
             if self.f8_wgrad:
                 self.XqL = torch.empty(L, B, D, dtype=e4, device=dev)

@@ -30,13 +30,13 @@ MI355X-first structure (no autograd tape on the hot path):
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass, field
 
 import torch
 
 from ..ops import fused
 from ..ops import gemm
+from ..utils.config import KernelPaths
 from ..utils.flat import FlatLayout, FlatParams
 from ..utils.profiling import trace_range
 
@@ -68,6 +68,9 @@ class RealNVPConfig:
     anneal: str = "reference"      # "reference" | "none" (beta_t schedule)
     anneal_iters: int = 10000      # max_iter for the reference schedule
     k_align: int = 32              # pad GEMM K/N dims (392 -> 416, 784 -> 800) for MFMA tiles
+    # fused / deferred kernel paths (utils.config.KernelPaths); None: the defaults, overridden
+    # by VINF_KERNEL_PATHS at engine construction
+    paths: KernelPaths | None = None
     extra: dict = field(default_factory=dict)
 
     @property
@@ -174,9 +177,10 @@ class RealNVPVI:
         self.Act = torch.empty(L, cfg.n_hidden, B, H, dtype=self.cdt, device=dev)
         # ReLU bitmasks of the hidden activations, written by the forward GEMM epilogue and read
         # by the input-gradient epilogue instead of the bf16 activation (B*H/8 bytes vs 2*B*H)
-        # (VINF_RELU_BITS=0: no bitmask; the input gradient reads the bf16 activation)
+        # (H % 8 != 0: no bitmask; the input gradient reads the bf16 activation)
         self.Mk = None
-        if dev.type == "cuda" and H % 8 == 0 and os.environ.get("VINF_RELU_BITS", "1") != "0":
+        kp = cfg.paths if cfg.paths is not None else KernelPaths.from_env()
+        if dev.type == "cuda" and H % 8 == 0:
             self.Mk = torch.empty(L, cfg.n_hidden, B, H // 8, dtype=torch.uint8, device=dev)
         # per-layer conditioner outputs [s_hat | t] (compute dtype): the backward recomputes
         # s = scale * tanh(s_hat) from them instead of reading a saved fp32 s
@@ -195,12 +199,12 @@ class RealNVPVI:
         # (dst, dH: ~6 GB at B = 32768 - nothing next to 288 GB of HBM) so the weight gradients
         # of several layers run as ONE launch of whole 256x256 tiles with the full batch as K
         # (ops.gemm.WgradPlan) instead of a split-K launch + reduce per layer
-        self.wgrad_defer = dev.type == "cuda" and os.environ.get("VINF_WGRAD_DEFER", "1") != "0"
+        self.wgrad_defer = dev.type == "cuda" and kp.wgrad_defer
         # fuse coupling layer l-1's backward into the epilogue of layer l's last input-gradient
         # GEMM (gemm_tile.h EPI_CPL_BWD): dL/dh_{l+1} is finished there and consumed at once
-        self.cpl_fuse = self.wgrad_defer and os.environ.get("VINF_CPL_FUSE", "1") != "0"
+        self.cpl_fuse = self.wgrad_defer and kp.cpl_fuse
         # ... reading x = h_{l-1} from its bf16 operand copy (EPI_CPL_BWD_XB, see _cpl_x)
-        self.cpl_xbf16 = os.environ.get("VINF_CPL_XBF16", "1") != "0"
+        self.cpl_xbf16 = kp.cpl_xbf16
         self.dstL = self.dHL = None
         # fuse each layer's coupling forward into its last conditioner GEMM (gemm256
         # EPI_CPL_FWD): s_hat / t never make an HBM round trip and t is never stored; the
@@ -208,18 +212,13 @@ class RealNVPVI:
         kc = H if cfg.n_hidden else Dp
         self.cf_fuse = (dev.type == "cuda" and self.cdt == torch.bfloat16
                         and Dh % 8 == 0 and kc % 32 == 0
-                        and os.environ.get("VINF_CPL_FWD_FUSE", "1") != "0")
+                        and kp.cpl_fwd_fuse)
         self.ldjp = None
         if self.cf_fuse:
             self.ldjp = torch.empty((Dh + 127) // 128, B, dtype=f32, device=dev)
-        # experiment (VINF_WGRAD_DEFER_STREAM=1): the deferred weight-gradient chunks on a side
-        # HIP stream, concurrent with the input-gradient chain
-        self.defer_stream = None
-        if self.wgrad_defer and os.environ.get("VINF_WGRAD_DEFER_STREAM", "0") == "1":
-            self.defer_stream = torch.cuda.Stream(device=dev)
         # input gradients dx = dy W as NT products against a per-step copy of W^T (one batched
         # transpose launch, ops.layout): both operands k-major, 5-7 % faster than the NN form
-        self.wt_dgrad = self.wgrad_defer and os.environ.get("VINF_DGRAD_NT", "1") != "0"
+        self.wt_dgrad = self.wgrad_defer and kp.dgrad_nt
         self.WT = None
         self._wt_plan = None
         self._wplan = None
@@ -230,24 +229,15 @@ class RealNVPVI:
         self.wgrad_stream = None
         # off by default: the 256x256 grouped launch holds one block on nearly every CU, so
         # overlapping it with the backward chain measured 1.2 % slower (on: +2 % with 128x128)
-        if dev.type == "cuda" and os.environ.get("VINF_WGRAD_STREAM", "0") == "1":
+        if dev.type == "cuda" and kp.wgrad_stream:
             self.wgrad_stream = torch.cuda.Stream(device=dev)
         self._G = torch.zeros(L + 2, B, Dp, dtype=f32, device=dev)   # dL/dh_i, 0-padded rows
         self.G = self._G[:, :, :Dh]
-        # opt-in (VINF_CPL_GBF16=1; measured slower: 34.90-35.09 vs 34.70-34.81 ms/step on one
-        # box, profiles/r4/cpl_gbf16_step_ab.jsonl - the 8-B loads / stores cost more than the
-        # 110 MB per call they save): the middle of the G chain in bf16. The fused coupling backward
-        # of layer l-1 (EPI_CPL_BWD_XB) reads G[l+1] / writes G[l-1] in bf16 where both sides are
-        # bf16-x fused epilogues (reads 2 <= l <= L-3, writes 4 <= l <= L-1); the chain's ends
-        # (target gradient, top coupling backward, layers 0-1, base backward) stay fp32
-        self.g_bf16 = (self.cpl_fuse and self.cpl_xbf16 and self.cdt == torch.bfloat16
-                       and os.environ.get("VINF_CPL_GBF16", "0") == "1")
-        self._G16 = (torch.zeros(L + 2, B, Dp, dtype=torch.bfloat16, device=dev)
-                     if self.g_bf16 else None)
+        # (the G chain stays fp32 end to end: a bf16 middle measured slower - 34.90-35.09 vs
+        # 34.70-34.81 ms/step on one box, profiles/r4/cpl_gbf16_step_ab.jsonl)
         # per-slab column sums of the base backward (HIP path: float4 columns, <= 1024 wide)
         self._rg_partial = None
-        if (dev.type == "cuda" and D % 4 == 0 and Dh % 4 == 0 and Dp % 4 == 0 and D <= 1024
-                and os.environ.get("VINF_REPARAM_GRAD", "1") == "1"):
+        if dev.type == "cuda" and D % 4 == 0 and Dh % 4 == 0 and Dp % 4 == 0 and D <= 1024:
             self._rg_partial = torch.empty(512 * 2 * D, dtype=f32, device=dev)
         self.logq0 = torch.empty(B, dtype=f32, device=dev)
         self.ldj = torch.empty(B, dtype=f32, device=dev)
@@ -271,7 +261,7 @@ class RealNVPVI:
     def _cpl_x(self, i: int, has_wt: bool) -> torch.Tensor:
         """x operand of the fused coupling backward (input half h_i of coupling layer i): the
         bf16 conditioner-operand copy Hbf[i-1] the forward already wrote when it exists (i >= 1,
-        bf16 compute, W^T given; VINF_CPL_XBF16=0 keeps the fp32 state). The epilogue is at the
+        bf16 compute, W^T given; KernelPaths(cpl_xbf16=False) keeps the fp32 state). The epilogue is at the
         HBM roof (profiles/r4/roofline_step.txt) and x only enters dS_hat, stored in bf16."""
         if i >= 1 and self.cpl_xbf16 and has_wt and self.cdt == torch.bfloat16:
             return self.Hbf[i - 1][:, :self.cfg.half]
@@ -467,20 +457,9 @@ class RealNVPVI:
         sched = gemm.WgradScheduler(plan, [(l + 1, plan.layer_end[l]) for l in range(L - 1, -1, -1)],
                                     self._wchunk, self.unit_ready_hook, self.wgrad_fence_hook)
         fuse = self.cpl_fuse
-        side = self.defer_stream
-        main = torch.cuda.current_stream(self.device) if side is not None else None
 
         def wgrad_ready(l):
-            if side is None:
-                sched.ready(plan.layer_end[l], final=(l == 0))
-                return
-            # the chunk runs beside the input-gradient chain: CUs in a GEMM's prologue /
-            # epilogue burst and CUs streaming a weight-gradient tile overlap
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                sched.ready(plan.layer_end[l], final=(l == 0))
+            sched.ready(plan.layer_end[l], final=(l == 0))
 
         def cpl_bwd(l):
             fused.coupling_bwd(self.G[l + 2], self.ST[l][:, :cfg.half], self.h(l), self.dstL[l],
@@ -505,11 +484,7 @@ class RealNVPVI:
                     # dL/dh_{l+1} = G[l+1] + d W0 is finished and consumed by layer l-1's
                     # coupling backward in the same epilogue (writes dstL[l-1], G[l-1])
                     xb = self._cpl_x(l - 1, WT is not None)
-                    # bf16 G is read by layers 2 <= l <= L-3 (bf16-x form, written by a fused
-                    # epilogue) and written by layers 4 <= l <= L-1 (their readers l-2)
-                    g16 = self.g_bf16 and xb.dtype == torch.bfloat16
-                    gin = self._G16[l + 1] if g16 and 2 <= l <= L - 3 else self._G[l + 1]
-                    gout = (self._G16[l - 1] if g16 and l >= 4 else self._G[l - 1])[:, :cfg.half]
+                    gin, gout = self._G[l + 1], self._G[l - 1][:, :cfg.half]
                     gemm.linear_dgrad_coupling(d, P.c(f"l{l}.W0"), gin,
                                                s_hat=self.ST[l - 1][:, :cfg.half],
                                                x=xb, dst=self.dstL[l - 1], gx=gout,
@@ -518,8 +493,6 @@ class RealNVPVI:
                 else:
                     gemm.linear_dgrad(d, P.c(f"l{l}.W0"), self._G[l + 1], accumulate=True)
             wgrad_ready(l)
-        if side is not None:
-            main.wait_stream(side)
         self._base_backward()
         if self.unit_ready_hook is not None:
             self.unit_ready_hook(0)

@@ -26,7 +26,6 @@ per-layer path and fp32 torch in ``tests/test_made_fused_gpu.py``.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -37,7 +36,10 @@ _BF = torch.bfloat16
 
 
 def enabled() -> bool:
-    return os.environ.get("VINF_MADE_FUSED", "1") != "0"
+    """``KernelPaths.made_fused`` (VINF_KERNEL_PATHS="made_fused=0" runs the unfused layers)."""
+    from ..utils.config import KernelPaths
+
+    return KernelPaths.from_env().made_fused
 
 
 def _mask0(made) -> torch.Tensor:

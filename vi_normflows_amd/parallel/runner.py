@@ -40,22 +40,18 @@ def _init_single_rank_group(info: DistInfo) -> None:
 
 
 # Process-global multi-rank GEMM policy, reference counted: the first runner that needs it
-# saves the library's persistent-grid / CU-reserve switches, every live runner keeps it applied,
-# the last one to close restores the saved values (LIFO-safe whatever order runners close in).
+# saves the library's persistent-grid switch, every live runner keeps it applied, the last one
+# to close restores the saved value (LIFO-safe whatever order runners close in).
 _POLICY = {"refs": 0, "saved": None}
 
 
-def _policy_acquire(reserve_mode: bool, reserve_cus: int) -> None:
+def _policy_acquire() -> None:
     from ..ops._ext import native
 
     if _POLICY["refs"] == 0:
-        _POLICY["saved"] = (int(native().gemm_persist(-1)), int(native().gemm_grid_reserve(-1)))
+        _POLICY["saved"] = int(native().gemm_persist(-1))
     _POLICY["refs"] += 1
-    if reserve_mode:
-        native().gemm_persist(1)
-        native().gemm_grid_reserve(reserve_cus)
-    else:
-        native().gemm_persist(0)
+    native().gemm_persist(0)
 
 
 def _policy_release() -> None:
@@ -63,42 +59,49 @@ def _policy_release() -> None:
 
     _POLICY["refs"] = max(0, _POLICY["refs"] - 1)
     if _POLICY["refs"] == 0 and _POLICY["saved"] is not None:
-        persist, reserve = _POLICY["saved"]
-        native().gemm_persist(persist)
-        native().gemm_grid_reserve(reserve)
+        native().gemm_persist(_POLICY["saved"])
         _POLICY["saved"] = None
 
 
 class DataParallelRunner:
-    """``force_reduce`` (or ``VINF_FORCE_REDUCE=1``) keeps the bucketed all-reduce on at world
-    size 1 when a process group exists: a 1-rank RCCL communicator then runs the exact
-    collective / stream-ordering / graph-capture path of the multi-GPU job on one GPU."""
+    """``force_reduce`` keeps the bucketed all-reduce on at world size 1 when a process group
+    exists: a 1-rank RCCL communicator then runs the exact collective / stream-ordering /
+    graph-capture path of the multi-GPU job on one GPU.
+
+    ``persist``: the multi-rank GEMM grid policy - ``"fwd"`` (default): persistent grids (one
+    block per CU) in the forward only, one block per tile in the backward, where RCCL kernels
+    take CUs; ``"all"``: persistent everywhere (measured 38.64 vs 39.05 ms on the 1-rank RCCL
+    path, but a collective holding CUs stalls whole tile lists on a real node);
+    ``"none"``: one block per tile everywhere. (A grid that left 16 / 8 CUs to RCCL measured
+    41.0-41.3 ms: profiles/r3/dp_backward_policy_ab.jsonl.)
+    ``graph_collectives``: capture the step WITH its collectives into the hipGraph at world > 1
+    (default off: eager replay costs ~0.1 ms of a ~37 ms step,
+    profiles/r2_graph_vs_eager_rccl_ab.jsonl); a 1-rank communicator is captured by default."""
 
     def __init__(self, engine, info: DistInfo, bucket_cap_mb: float = 32.0,
-                 compress_bf16: bool = False, force_reduce: bool = False):
+                 compress_bf16: bool = False, force_reduce: bool = False, persist: str = "fwd",
+                 graph_collectives: bool | None = None):
+        if persist not in ("fwd", "all", "none"):
+            raise ValueError(f"persist must be fwd | all | none, got {persist!r}")
+        self.graph_collectives = graph_collectives
         self.engine = engine
         self.info = info
         self.graph = None
         self.reducer = None
         self._t = int(engine.step_t.item())   # host step counter (fault injection only)
-        force = force_reduce or os.environ.get("VINF_FORCE_REDUCE", "0") == "1"
+        force = force_reduce
         if force and info.world == 1 and not dist.is_initialized():
             _init_single_rank_group(info)
-        # "1" all | "0" none | "fwd" (default) | "reserve"
-        persist = os.environ.get("VINF_DP_PERSIST", "fwd")
         self._policy_held = False     # this runner holds a reference on the global GEMM policy
-        if (info.world > 1 or force) and engine.device.type == "cuda" and persist != "1":
+        if (info.world > 1 or force) and engine.device.type == "cuda" and persist != "all":
             # multi-rank: RCCL kernels run on CUs beside the backward's GEMMs; a persistent GEMM
             # grid (one block per CU, each owning a fixed tile list) would wait for every CU an
-            # all-reduce holds. "fwd": the backward's products launch one block per tile;
-            # "reserve": they keep the persistent grid, sized to leave VINF_G256_RESERVE CUs
-            # (default 16, whole XCD rounds) to RCCL. The forward has no collective in flight:
-            # engines that support it run the full persistent grid there
-            # (``persist_forward_only``).
-            reserve = int(os.environ.get("VINF_G256_RESERVE", "16")) if persist == "reserve" else 0
-            _policy_acquire(persist == "reserve", reserve)
+            # all-reduce holds, so the backward's products launch one block per tile. The
+            # forward has no collective in flight: engines that support it run the full
+            # persistent grid there (``persist_forward_only``).
+            _policy_acquire()
             self._policy_held = True
-            if persist in ("fwd", "reserve") and hasattr(engine, "persist_forward_only"):
+            if persist == "fwd" and hasattr(engine, "persist_forward_only"):
                 engine.persist_forward_only = True
         if info.world > 1 or (force and dist.is_initialized()):
             P = engine.params
@@ -110,12 +113,10 @@ class DataParallelRunner:
                                              bucket_cap_mb=bucket_cap_mb,
                                              compress_bf16=compress_bf16, force=force)
             engine.unit_ready_hook = self.reducer.mark_ready
-            # VINF_DP_WGRAD_FENCE=1: weight-gradient launches wait for the buckets in flight.
-            # Off by default: with the 4-wave weight-gradient kernel a collective resident at a
-            # launch's start costs nothing measurable (-0.24 / -0.03 ms at 250 / 500 us holds)
-            # while the fence waits it out (+1.0 / +2.4 ms), profiles/r4/dp_contention_tn4w.jsonl
-            if hasattr(engine, "wgrad_fence_hook") and os.environ.get("VINF_DP_WGRAD_FENCE", "0") == "1":
-                engine.wgrad_fence_hook = self.reducer.wait_inflight
+            # (no fence between the weight-gradient launches and the buckets in flight: with the
+            # 4-wave weight-gradient kernel a collective resident at a launch's start costs
+            # nothing measurable, -0.24 / -0.03 ms at 250 / 500 us holds, while a fence waits it
+            # out, +1.0 / +2.4 ms: profiles/r4/dp_contention_tn4w.jsonl)
 
     def _eager_step(self):
         kind = faults.armed(self._t, self.info.rank)
@@ -169,14 +170,13 @@ class DataParallelRunner:
 
         Collectives inside the graph: a 1-rank RCCL communicator (``force_reduce``) is captured
         by default (tested: tests/test_distributed_gpu.py). A multi-rank job replays eager steps
-        unless ``VINF_GRAPH_COLLECTIVES=1`` opts in (eager costs ~0.1 ms of a ~37 ms step,
-        profiles/r2_graph_vs_eager_rccl_ab.jsonl); with the opt-in, whether to use the graph is
+        unless ``graph_collectives=True`` opts in; with the opt-in, whether to use the graph is
         decided collectively, so no rank replays a graph while another steps eagerly."""
         if self.engine.device.type != "cuda":
             return False
         multi = self.reducer is not None and self.info.world > 1
-        env = os.environ.get("VINF_GRAPH_COLLECTIVES")
-        if self.reducer is not None and (env == "0" or (multi and env != "1")):
+        gc = self.graph_collectives
+        if self.reducer is not None and (gc is False or (multi and gc is not True)):
             return False
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())

@@ -12,6 +12,8 @@ weights + ``free_energy.txt`` line.
 from __future__ import annotations
 
 import argparse
+import contextlib
+import functools
 import json
 import math
 import os
@@ -38,6 +40,30 @@ def _device(cfg, info):
     return info.device
 
 
+# Every DataParallelRunner a run_* function creates is closed when it returns (or raises): a
+# runner holds the process-global multi-rank GEMM policy (parallel/runner.py), which must not
+# leak into whatever the process runs next (tests, benchmarks).
+_RUNNER_STACKS: list = []
+
+
+def _closes_runners(fn):
+    @functools.wraps(fn)
+    def wrap(*a, **k):
+        with contextlib.ExitStack() as st:
+            _RUNNER_STACKS.append(st)
+            try:
+                return fn(*a, **k)
+            finally:
+                _RUNNER_STACKS.pop()
+    return wrap
+
+
+def _runner(eng, info, **kw):
+    from .parallel.runner import DataParallelRunner
+
+    return _RUNNER_STACKS[-1].enter_context(DataParallelRunner(eng, info, **kw))
+
+
 def run_flow_vi(cfg, out, info, logger):
     from .inference.flow_vi import fit_flow_vi
     from .viz.plots import plot_density_and_samples, plot_loss
@@ -57,6 +83,7 @@ def run_flow_vi(cfg, out, info, logger):
     return r.final
 
 
+@_closes_runners
 def run_realnvp(cfg, out, info, logger):
     from .models.realnvp import RealNVPConfig, RealNVPVI
     from .parallel.runner import DataParallelRunner
@@ -82,8 +109,8 @@ def run_realnvp(cfg, out, info, logger):
         load_engine(eng, ckpt, info.rank)
         if info.is_main:
             print(f"[train] resumed from {ckpt} at step {int(eng.step_t.item())}", flush=True)
-    run = DataParallelRunner(eng, info)
-    fault = os.environ.get("VINF_FAULT_STEP") is not None
+    run = _runner(eng, info)
+    fault = bool(os.environ.get("VINF_FAULT"))
     if dev.type == "cuda" and cfg.extra.get("graph", True) and not fault:
         run.capture(warmup=1)
     t0 = time.perf_counter()
@@ -107,6 +134,7 @@ def run_realnvp(cfg, out, info, logger):
             "skipped_steps": float(eng.n_skipped.item())}
 
 
+@_closes_runners
 def run_planar_vae(cfg, out, info, logger):
     import numpy as np
 
@@ -160,7 +188,7 @@ def run_planar_vae(cfg, out, info, logger):
             return xb if n == cfg.batch else xb[torch.arange(cfg.batch) % n]
 
         eng.set_batch(full(it(0)).to(dev))
-        run = DataParallelRunner(eng, info)
+        run = _runner(eng, info)
         if dev.type == "cuda" and cfg.extra.get("graph", True):
             run.capture(warmup=1)
         eng.params.reset_optimizer_state()   # the capture warm-up stepped the optimizer
@@ -218,6 +246,7 @@ def run_planar_vae(cfg, out, info, logger):
     return {"free_energy_per_sample": F, "engine": "module"}
 
 
+@_closes_runners
 def run_iaf_vae(cfg, out, info, logger):
     from .inference.trainer import TrainConfig, Trainer
     from .models.iaf_vae import IAFVAE, IAFVAEConfig, synthetic_images
@@ -240,7 +269,7 @@ def run_iaf_vae(cfg, out, info, logger):
                         device=dev, seed=rank_seed(cfg.seed, info.rank), rank=info.rank,
                         lr=cfg.lr, model=model, anneal=cfg.schedule, anneal_iters=cfg.iters,
                         optimizer=cfg.optimizer)
-        run = DataParallelRunner(eng, info)
+        run = _runner(eng, info)
         if cfg.extra.get("graph", True):
             run.capture(warmup=1)
             eng.load_module(model)     # the capture warm-up stepped Adam: start from the init
@@ -274,6 +303,7 @@ def run_iaf_vae(cfg, out, info, logger):
     return {"free_energy": tr.history[-1]["F"], "engine": "module"}
 
 
+@_closes_runners
 def run_maf(cfg, out, info, logger):
     """MAF density estimation. ``extra.impl``: "engine" (default: flat-buffer explicit-backward
     engine, fp8/bf16 forward, DP runner + hipGraph) or "module" (autograd MAFDensity)."""
@@ -287,7 +317,7 @@ def run_maf(cfg, out, info, logger):
                              precision=cfg.extra.get("precision", "fp8"))
         eng = MAFEngine(mc, batch=cfg.batch, device=dev, seed=cfg.seed, rank=info.rank, lr=cfg.lr,
                         optimizer=cfg.optimizer)
-        run = DataParallelRunner(eng, info)
+        run = _runner(eng, info)
         if dev.type == "cuda" and cfg.extra.get("graph", True):
             run.capture(warmup=1)
         t0 = time.perf_counter()

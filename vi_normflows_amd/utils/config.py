@@ -160,3 +160,40 @@ def rank_seed(seed: int, rank: int) -> int:
 
 def is_config(obj) -> bool:
     return is_dataclass(obj)
+
+
+@dataclass
+class KernelPaths:
+    """Which fused / deferred kernel paths the explicit-backward engines take.
+
+    Every field defaults to the measured-fastest path (docs/PERF_NOTES.md); switching one off
+    runs the unfused composition of the same math, which is what the equivalence tests compare
+    the fused kernels against. ``VINF_KERNEL_PATHS="wgrad_defer=0,wgrad_stream=1"`` overrides
+    the defaults for a whole process (subprocess tests, A/B scripts) - the one environment knob
+    of the engines (docs/ARCHITECTURE.md, "Runtime switches")."""
+    wgrad_defer: bool = True     # weight gradients of many layers as one multi-layer launch
+    dgrad_nt: bool = True        # input gradients as NT products against a per-step W^T copy
+    cpl_fuse: bool = True        # coupling backward fused into the conditioner's input gradient
+    cpl_fwd_fuse: bool = True    # coupling forward fused into the conditioner's last product
+    cpl_xbf16: bool = True       # fused coupling backward reads x as its bf16 operand copy
+    wgrad_stream: bool = False   # per-layer weight gradients on a side stream (DP tests)
+    maf_fuse: bool = True        # MAF transform fused into the MADE GEMM epilogues
+    fp8_dgrad: bool = True       # MAF fp8: e4m3 input gradients
+    fp8_wgrad: bool = True       # MAF fp8: e4m3 weight gradients
+    made_fused: bool = True      # module path: fused MADE autograd function (ops.made_fused)
+
+    @classmethod
+    def from_env(cls) -> "KernelPaths":
+        import os
+
+        p = cls()
+        spec = os.environ.get("VINF_KERNEL_PATHS", "").strip()
+        if not spec:
+            return p
+        names = {f.name for f in fields(cls)}
+        for item in spec.split(","):
+            k, _, v = item.strip().partition("=")
+            if k not in names:
+                raise ValueError(f"VINF_KERNEL_PATHS: unknown path {k!r} (known: {sorted(names)})")
+            setattr(p, k, v.strip().lower() not in ("0", "false", "off", "no"))
+        return p

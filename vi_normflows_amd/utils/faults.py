@@ -1,14 +1,15 @@
 """Fault injection for recovery tests.
 
-Driven by environment variables so a launcher (torchrun, a test) can arm it without code
-changes; inert unless ``VINF_FAULT_STEP`` is set:
+Driven by one environment variable so a launcher (torchrun, a test) can arm it without code
+changes; inert unless ``VINF_FAULT`` is set:
 
-    VINF_FAULT_STEP=k    step at which to fire
-    VINF_FAULT_RANK=r    rank that fires (default 0)
-    VINF_FAULT_KIND=exit|nan|inf   exit: hard process exit (simulated node/rank loss);
-                         nan/inf: poison the gradient buffer (exercises the non-finite guard)
-    VINF_FAULT_ONCE=1    (default) fire only on the first attempt: torchrun exports
-                         TORCHELASTIC_RESTART_COUNT, and a restarted job must run clean
+    VINF_FAULT=KIND:STEP[:RANK[:always]]
+        KIND   exit | nan | inf    exit: hard process exit (simulated node / rank loss);
+                                   nan / inf: poison the gradient buffer (non-finite guard)
+        STEP   step at which to fire
+        RANK   rank that fires (default 0)
+        always fire on every attempt; by default only the first one fires: torchrun exports
+               TORCHELASTIC_RESTART_COUNT, and a restarted job must run clean
 """
 from __future__ import annotations
 
@@ -17,15 +18,32 @@ import os
 EXIT_CODE = 13
 
 
+def spec(kind: str, step: int, rank: int = 0, always: bool = False) -> str:
+    """The ``VINF_FAULT`` value arming ``kind`` at (step, rank)."""
+    return f"{kind}:{int(step)}:{int(rank)}" + (":always" if always else "")
+
+
+def _parse():
+    s = os.environ.get("VINF_FAULT", "").strip()
+    if not s:
+        return None
+    parts = s.split(":")
+    if len(parts) < 2 or parts[0] not in ("exit", "nan", "inf"):
+        raise ValueError(f"VINF_FAULT={s!r}: expected KIND:STEP[:RANK[:always]], KIND exit|nan|inf")
+    rank = int(parts[2]) if len(parts) > 2 and parts[2] else 0
+    return parts[0], int(parts[1]), rank, len(parts) > 3 and parts[3] == "always"
+
+
 def armed(step: int, rank: int) -> str | None:
-    s = os.environ.get("VINF_FAULT_STEP")
-    if s is None or int(s) != int(step):
+    p = _parse()
+    if p is None:
         return None
-    if int(os.environ.get("VINF_FAULT_RANK", "0")) != int(rank):
+    kind, fstep, frank, always = p
+    if fstep != int(step) or frank != int(rank):
         return None
-    if os.environ.get("VINF_FAULT_ONCE", "1") == "1" and int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")) > 0:
+    if not always and int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")) > 0:
         return None
-    return os.environ.get("VINF_FAULT_KIND", "exit")
+    return kind
 
 
 def maybe_inject(step: int, rank: int, grad=None) -> None:

@@ -91,5 +91,4 @@ def kernel_stats(path, steps: int | None = None, top: int = 30) -> str:
 def debug_env() -> dict:
     """Environment for a synchronous-launch debug run (set BEFORE the process touches HIP):
     every kernel launch blocks, so a fault is reported at the launch that caused it."""
-    return {"HIP_LAUNCH_BLOCKING": "1", "AMD_SERIALIZE_KERNEL": "3", "AMD_SERIALIZE_COPY": "3",
-            "VINF_GRAPH": "off"}
+    return {"HIP_LAUNCH_BLOCKING": "1", "AMD_SERIALIZE_KERNEL": "3", "AMD_SERIALIZE_COPY": "3"}
