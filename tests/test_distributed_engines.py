@@ -1,0 +1,224 @@
+"""Data parallelism of the config-5 MAF engine (bf16 and fp8 with delayed per-tensor scales)
+and the config-0 PlanarVAE engine on the DP runner: ranks over gloo (CPU: one process per
+rank; GPU: two ranks sharing one MI355X - RCCL refuses two ranks per GPU).
+
+* the DP gradient equals the single-process gradient on the concatenated batch;
+* replicas are bitwise identical after 5 runner steps (rank 0's parameters broadcast, then the
+  all-reduced gradient applied on every rank);
+* fp8: the delayed activation / gradient scales are RANK-LOCAL state (each rank quantises its
+  own batch with the amax history of its own batch): the test checks that the ranks' scale
+  pools differ while the replicas stay bitwise identical - the weights' e4m3 copies are
+  re-derived from the (identical) master weights every step, and every GEMM output is
+  dequantised before it reaches a gradient, so rank-local scales never reach the parameters.
+
+The reference trains sequentially on one CPU (``normflows/normflows/utils.py:41-60``, batches
+of one process); this is the multi-process check of SURVEY §4 item 5 for these engines.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+B = 256
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _maf_cfg(precision, gpu):
+    from vi_normflows_amd.models.maf_engine import MAFEngineConfig
+
+    if gpu:
+        return MAFEngineConfig(dim=256, hidden=512, n_layers=3, precision=precision,
+                               init_out_std=0.3)
+    return MAFEngineConfig(dim=16, hidden=32, n_layers=3, precision=precision, init_out_std=0.3)
+
+
+def _init(rank, world, port, gpu):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0", VINF_DIST_BACKEND="gloo")
+    from vi_normflows_amd.parallel import dist as vdist
+
+    info = vdist.init(device_type="cuda" if gpu else "cpu")
+    return info
+
+
+def _maf_worker(rank, world, port, data_all, out_dir, precision, gpu):
+    info = _init(rank, world, port, gpu)
+    from vi_normflows_amd.models.maf_engine import MAFEngine
+    from vi_normflows_amd.parallel.runner import DataParallelRunner
+
+    dev = info.device
+    eng = MAFEngine(_maf_cfg(precision, gpu), batch=B, device=dev, seed=5 + rank, rank=rank)
+    with DataParallelRunner(eng, info, bucket_cap_mb=0.05 if gpu else 0.001) as run:
+        assert run.reducer is not None and len(run.reducer.buckets) > 2
+        # one step by hand: the all-reduced gradient before the optimizer
+        eng.data_override = data_all[rank * B:(rank + 1) * B].to(dev)
+        run.reducer.start_step()
+        eng._update_schedule()
+        eng.forward()
+        eng.backward()
+        run.reducer.finish()
+        if gpu:
+            torch.cuda.synchronize()
+        out = {"grad": eng.params.grad.to("cpu", copy=True), "master0": eng.params.master.to("cpu", copy=True)}
+        # 5 runner steps on each rank's own data stream (rank Philox streams)
+        eng.data_override = None
+        for _ in range(5):
+            run.step()
+        if gpu:
+            torch.cuda.synchronize()
+        out["master5"] = eng.params.master.to("cpu", copy=True)
+        out["loss5"] = float(eng.loss.item())
+        if getattr(eng, "fp8", False):
+            out["amax_pool"] = eng.amax_pool.to("cpu", copy=True)
+            out["scale_pool"] = eng.f8_scale_pool.to("cpu", copy=True)
+            out["f8_wgrad"] = bool(eng.f8_wgrad)
+    torch.save(out, os.path.join(out_dir, f"maf{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def _check_maf(tmp_path, precision, gpu):
+    from vi_normflows_amd.models.maf_engine import MAFEngine
+
+    world = 2
+    cfg = _maf_cfg(precision, gpu)
+    torch.manual_seed(0)
+    data_all = torch.randn(world * B, cfg.dim) * 0.8
+    mp.spawn(_maf_worker, args=(world, _port(), data_all, str(tmp_path), precision, gpu),
+             nprocs=world, join=True)
+    r0 = torch.load(tmp_path / "maf0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "maf1.pt", weights_only=True)
+    # broadcast: rank 1 started from another seed but holds rank 0's parameters
+    assert torch.equal(r0["master0"], r1["master0"])
+    # the all-reduce result is the same on every rank
+    assert torch.equal(r0["grad"], r1["grad"])
+    # replicas after 5 all-reduced steps: bitwise identical
+    assert torch.isfinite(r0["master5"]).all()
+    assert torch.equal(r0["master5"], r1["master5"])
+    assert not torch.equal(r0["master5"], r0["master0"])
+    dev = torch.device("cuda" if gpu else "cpu")
+    single = MAFEngine(cfg, batch=world * B, device=dev, seed=5)
+    single.params.master.copy_(r0["master0"].to(dev))
+    single.params.sync_compute()
+    if getattr(single, "fp8", False):
+        single.quantize_weights()
+    single.data_override = data_all.to(dev)
+    single._update_schedule()
+    single.forward()
+    single.backward()
+    ref = single.params.grad.cpu()
+    dp = r0["grad"] / world
+    rel = float((dp - ref).norm() / ref.norm())
+    # fp32 (CPU): summation order only; bf16 GEMMs: the same per-row products, only the
+    # batch reduction splits; fp8: per-tensor activation scales depend on each rank's batch
+    tol = {"fp32": 1e-5, "bf16": 1e-3, "fp8": 5e-2}["fp32" if not gpu else precision]
+    assert rel < tol, rel
+    if precision == "fp8" and gpu:
+        assert r0["f8_wgrad"]
+        # rank-local delayed scales: the ranks saw different data, so their amax histories
+        # differ - and the replicas above are still bitwise identical
+        assert not torch.equal(r0["amax_pool"], r1["amax_pool"])
+        assert torch.isfinite(r0["scale_pool"]).all() and (r0["scale_pool"] > 0).all()
+    return rel
+
+
+def test_dp_maf_engine_cpu(tmp_path):
+    _check_maf(tmp_path, "bf16", gpu=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["bf16", "fp8"])
+def test_dp_maf_engine_gpu(tmp_path, precision):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    rel = _check_maf(tmp_path, precision, gpu=True)
+    print(f"[dp maf {precision}] DP vs single-process gradient rel {rel:.2e}")
+
+
+def _vae_cfg():
+    from vi_normflows_amd.models.vae import VAEConfig
+
+    return VAEConfig(dim_x=64, dim_z=8, K=4, width=64, hidden_layers=2)
+
+
+def _vae_worker(rank, world, port, x_all, eps_all, out_dir, gpu):
+    info = _init(rank, world, port, gpu)
+    from vi_normflows_amd.models.vae_engine import PlanarVAEEngine
+    from vi_normflows_amd.parallel.runner import DataParallelRunner
+
+    dev = info.device
+    eng = PlanarVAEEngine(_vae_cfg(), batch=B, device=dev, seed=11 + rank, lr=1e-3)
+    with DataParallelRunner(eng, info, bucket_cap_mb=0.01) as run:
+        assert run.reducer is not None
+        sl = slice(rank * B, (rank + 1) * B)
+        eng.set_batch(x_all[sl].to(dev))
+        eng.eps_override = eps_all[sl].to(dev)
+        run.reducer.start_step()
+        eng._update_schedule()
+        eng.forward_backward()
+        for u in range(len(eng.layout.unit_ranges) - 1, -1, -1):
+            eng.unit_ready_hook(u)
+        run.reducer.finish()
+        if gpu:
+            torch.cuda.synchronize()
+        out = {"grad": eng.params.grad.to("cpu", copy=True), "master0": eng.params.master.to("cpu", copy=True),
+               "loss": float(eng.loss.item())}
+        eng.eps_override = None      # rank-distinct in-kernel noise from here on
+        for _ in range(5):
+            run.step()
+        if gpu:
+            torch.cuda.synchronize()
+        out["master5"] = eng.params.master.to("cpu", copy=True)
+    torch.save(out, os.path.join(out_dir, f"vae{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def _check_vae(tmp_path, gpu):
+    from vi_normflows_amd.models.vae_engine import PlanarVAEEngine
+
+    world = 2
+    cfg = _vae_cfg()
+    g = torch.Generator().manual_seed(1)
+    x_all = (torch.rand(world * B, cfg.dim_x, generator=g) < 0.3).float()
+    eps_all = torch.randn(world * B, cfg.dim_z, generator=g)
+    mp.spawn(_vae_worker, args=(world, _port(), x_all, eps_all, str(tmp_path), gpu),
+             nprocs=world, join=True)
+    r0 = torch.load(tmp_path / "vae0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "vae1.pt", weights_only=True)
+    assert torch.equal(r0["master0"], r1["master0"])
+    assert torch.equal(r0["grad"], r1["grad"])
+    assert torch.isfinite(r0["master5"]).all()
+    assert torch.equal(r0["master5"], r1["master5"])
+    dev = torch.device("cuda" if gpu else "cpu")
+    single = PlanarVAEEngine(cfg, batch=world * B, device=dev, seed=11)
+    single.params.master.copy_(r0["master0"].to(dev))
+    single.set_batch(x_all.to(dev))
+    single.eps_override = eps_all.to(dev)
+    single._update_schedule()
+    single.forward_backward()
+    ref = single.params.grad.cpu()
+    dp = r0["grad"] / world
+    rel = float((dp - ref).norm() / ref.norm())
+    assert rel < 1e-5, rel        # fp32 engine: summation order only
+    return rel
+
+
+def test_dp_vae_engine_cpu(tmp_path):
+    _check_vae(tmp_path, gpu=False)
+
+
+@pytest.mark.gpu
+def test_dp_vae_engine_gpu(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    rel = _check_vae(tmp_path, gpu=True)
+    print(f"[dp vae] DP vs single-process gradient rel {rel:.2e}")

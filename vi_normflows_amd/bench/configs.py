@@ -48,6 +48,9 @@ def graphed(step_fn, dev, warmup: int = 3):
     return g
 
 
+_ENGINES: list = []   # explicit-backward engines built by build() (replica check in main)
+
+
 def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: bool = True,
           impl: str = "engine"):
     dev = info.device
@@ -56,25 +59,30 @@ def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: b
         from ..models.vae import PlanarVAE, VAEConfig, synthetic_binary_images
 
         B = batch or 128
-        if impl == "engine" and dev.type == "cuda" and info.world == 1:
+        if impl == "engine" and dev.type == "cuda":
             # models/vae_engine.py: two HIP launches (row-parallel fwd + input-gradient chain,
-            # batch-reduction weight gradients) + fused guard + flat Adam, one hipGraph
+            # batch-reduction weight gradients) + fused guard + flat Adam, one hipGraph; DP:
+            # the runner's bucketed all-reduce (rank 0's parameters broadcast)
             from ..models.vae_engine import PlanarVAEEngine
+            from ..parallel.runner import DataParallelRunner
 
             eng = PlanarVAEEngine(VAEConfig(dim_x=784, dim_z=40, K=4, width=64, hidden_layers=3),
                                   batch=B, device=dev, seed=info.rank, lr=1e-3)
+            _ENGINES.append(eng)
             X = synthetic_binary_images(max(2000, 4 * B), 784, seed=info.rank).to(dev)
             eng.set_batch(X[:B])
-            g = eng.capture(warmup=2) if graph else None
+            run = DataParallelRunner(eng, info)
+            if graph:
+                run.capture(warmup=2)
             it = [0]
 
             def step():
                 i = it[0] % (X.shape[0] // B)
                 it[0] += 1
                 eng.set_batch(X[i * B:(i + 1) * B])
-                g.replay() if g is not None else eng.train_step()
+                run.step()
             return step, B, dev, "fp32 PlanarVAE engine (vae.hip two-launch step + flat Adam)" + (
-                ", hipGraph" if g is not None else "")
+                ", hipGraph" if run.graph is not None else "")
         model = PlanarVAE(VAEConfig(dim_x=784, dim_z=40, K=4, width=64, hidden_layers=3))
         model.init_reference(generator=torch.Generator().manual_seed(0))
         model = model.to(dev)
@@ -125,6 +133,7 @@ def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: b
         B = batch or 16384
         eng = RealNVPVI(RealNVPConfig(n_layers=8 if cfg_id == 2 else 32), batch=B, device=dev,
                         rank=info.rank)
+        _ENGINES.append(eng)
         run = DataParallelRunner(eng, info)
         if dev.type == "cuda":
             run.capture(warmup=1)
@@ -137,6 +146,7 @@ def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: b
         B = batch or 8192
         X = synthetic_images(B * 4, device=dev, seed=info.rank).reshape(B * 4, -1)
         eng = IAFEngine(IAFVAEConfig(), B, X, device=dev, seed=0, rank=info.rank)
+        _ENGINES.append(eng)
         run = DataParallelRunner(eng, info)
         if graph:
             run.capture(warmup=2)
@@ -174,6 +184,7 @@ def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: b
 
         B = batch or 8192
         eng = MAFEngine(MAFEngineConfig(precision=precision), batch=B, device=dev, rank=info.rank)
+        _ENGINES.append(eng)
         run = DataParallelRunner(eng, info)
         if graph and dev.type == "cuda":
             run.capture(warmup=2)
@@ -277,13 +288,20 @@ def main(argv=None):
     _sync(dev)
     vdist.barrier()
     dt = vdist.all_reduce_max(time.perf_counter() - t0)
+    # replica check (after the timed steps): every rank's fp32 master weights against rank 0's;
+    # the modules' DDP replicas (torch) are not checked here
+    rep = None
+    if _ENGINES and info.world > 1:
+        rep = vdist.replica_max_diff(_ENGINES[-1].params.master)
     if info.is_main:
         # dense-layer precision actually taken by the module paths (forward calls per path)
         print(json.dumps({"config": a.config, "name": NAMES[a.config], "n_ranks": info.world,
                           "per_rank_batch": B, "ms_per_step": 1000 * dt / a.steps,
                           "samples_per_s": B * info.world * a.steps / dt, "dtype": dtype,
                           "impl": a.impl, "dense_precision": dense,
-                          "dense_calls": precision_counts()}))
+                          "dense_calls": precision_counts(),
+                          "replicas_identical": None if rep is None else rep == 0.0,
+                          "max_replica_diff": rep}))
     vdist.shutdown()
 
 

@@ -104,6 +104,17 @@ def all_reduce_max(x: float, device=None) -> float:
     return float(t.item())
 
 
+def replica_max_diff(t: torch.Tensor) -> float:
+    """max over ranks of max |t - rank 0's t| (0.0 at world size 1): the DP replica check."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return 0.0
+    ref = t.detach().clone()
+    dist.broadcast(ref, 0)
+    d = torch.tensor([float((t.detach() - ref).abs().max())], dtype=torch.float64, device=t.device)
+    dist.all_reduce(d, op=dist.ReduceOp.MAX)
+    return float(d.item())
+
+
 def all_reduce_mean_(t: torch.Tensor) -> torch.Tensor:
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t)
