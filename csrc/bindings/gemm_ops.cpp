@@ -403,17 +403,23 @@ void fp8_colsum(at::TensorList q, at::TensorList out, const at::Tensor& scales,
 
 // Last conditioner product of coupling layer l with the layer's coupling forward in the epilogue:
 // st[:, :Dh] = s_hat (bf16), y = x e^s + t, yb = bf16(y) (0-padded), ldjp[tn] (+)= partial sum s.
+// inverse: x = (y - t) e^-s from the layer output (passed as x) into y / yb, ldj share -sum s;
+// st may then be None (s_hat not stored)
 void gemm_nt_cpl(const at::Tensor& h, const at::Tensor& W, const c10::optional<at::Tensor>& b,
-                 const at::Tensor& st, const at::Tensor& x, const at::Tensor& y,
+                 const c10::optional<at::Tensor>& st_opt, const at::Tensor& x, const at::Tensor& y,
                  const c10::optional<at::Tensor>& yb, const at::Tensor& ldjp, bool ldj_init,
-                 double scale) {
+                 double scale, bool inverse) {
   chk_mat(h, "h", at::kBFloat16);
   chk_mat(W, "W", at::kBFloat16);
-  chk_mat(st, "st", at::kBFloat16);
   const int M = h.size(0), K = h.size(1), Dh = x.size(1);
+  const bool has_st = st_opt && st_opt->defined();
+  TORCH_CHECK(has_st || inverse, "st (s_hat output) is required in the forward");
+  if (has_st) {
+    chk_mat(*st_opt, "st", at::kBFloat16);
+    TORCH_CHECK(st_opt->size(0) == M && st_opt->size(1) >= Dh, "st shape");
+  }
   TORCH_CHECK(W.size(1) == K && W.size(0) >= 2 * Dh, "W: [>= 2 Dh, K]");
   TORCH_CHECK(K % 32 == 0 && Dh % 8 == 0, "K % 32 and Dh % 8 required");
-  TORCH_CHECK(st.size(0) == M && st.size(1) >= Dh, "st shape");
   for (const at::Tensor* t : {&x, &y})
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->dim() == 2 &&
                     t->stride(1) == 1 && t->size(0) == M && t->size(1) == Dh &&
@@ -440,9 +446,10 @@ void gemm_nt_cpl(const at::Tensor& h, const at::Tensor& W, const c10::optional<a
     ybw = (int)yb->size(1);
   }
   nf_launch_gemm256_nt_cpl(h.data_ptr(), ld2(h), W.data_ptr(), ld2(W), (int)W.size(0), bp,
-                           st.data_ptr(), ld2(st), M, K, Dh, x.data_ptr<float>(), ld2(x),
-                           y.data_ptr<float>(), ld2(y), ybp, ldyb, ybw, ldjp.data_ptr<float>(),
-                           ldjp.stride(0), ldj_init, (float)scale, cur_stream());
+                           has_st ? st_opt->data_ptr() : nullptr, has_st ? ld2(*st_opt) : 0, M,
+                           K, Dh, x.data_ptr<float>(), ld2(x), y.data_ptr<float>(), ld2(y), ybp,
+                           ldyb, ybw, ldjp.data_ptr<float>(), ldjp.stride(0), ldj_init,
+                           (float)scale, cur_stream(), inverse ? 1 : 0);
 }
 
 // Conditioner input gradient of coupling layer l (gy = G + dy W, fp32, not stored) fused with the
@@ -1075,7 +1082,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("gemm_tn_multi_layout(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles, int layout) -> ()");
   m.def("fp8_colsum(Tensor[] q, Tensor(a!)[] out, Tensor scales, int[] sidx, Tensor(b!) part) -> ()");
   m.def("gemm_tn_multi_f8(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles, Tensor?[] tiles, Tensor?[] cmask, Tensor scales, int[] sa_idx, int[] sb_idx) -> ()");
-  m.def("gemm_nt_cpl(Tensor h, Tensor W, Tensor? b, Tensor(a!) st, Tensor x, Tensor(b!) y, Tensor(c!)? yb, Tensor(d!) ldjp, bool ldj_init, float scale) -> ()");
+  m.def("gemm_nt_cpl(Tensor h, Tensor W, Tensor? b, Tensor(a!)? st, Tensor x, Tensor(b!) y, Tensor(c!)? yb, Tensor(d!) ldjp, bool ldj_init, float scale, bool inverse=False) -> ()");
   m.def("gemm_nn_cpl(Tensor dy, Tensor W, Tensor G, Tensor s_hat, Tensor x, Tensor(a!) dst, Tensor(b!) gx, float scale, float c, Tensor? Wt=None) -> ()");
   m.def("maf_gemm_fwd(Tensor h, Tensor? hs, Tensor W, Tensor? ws, Tensor? b, Tensor krange, Tensor(a!) s_out, Tensor x, Tensor(b!) u, Tensor(c!)? ubf, Tensor(d!) ldjp, bool ldj_init, float bound, Tensor(e!)? uq=None, Tensor? q_amax_prev=None, Tensor(f!)? q_scale=None, Tensor(g!)? q_amax_cur=None) -> ()");
   m.def("maf_gemm_bwd(Tensor dy, Tensor Wt, Tensor krange256, Tensor G, Tensor s_raw, Tensor u, Tensor(a!)? dst, Tensor(b!) gx, float bound, float c, Tensor? sa=None, Tensor? sb=None, Tensor(c!)? dstq=None, Tensor? q_amax_prev=None, Tensor(d!)? q_scale=None, Tensor(e!)? q_amax_cur=None) -> ()");

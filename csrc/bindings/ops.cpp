@@ -174,6 +174,46 @@ void bernoulli_logits(const at::Tensor& logits, const at::Tensor& x,
                              opt_ptr<float>(logpx), B, P, cur_stream());
 }
 
+void energy2d(int64_t kind, const at::Tensor& z, const c10::optional<at::Tensor>& logp,
+              const c10::optional<at::Tensor>& grad, double gscale,
+              const c10::optional<at::Tensor>& logq0, const c10::optional<at::Tensor>& ldj,
+              const c10::optional<at::Tensor>& beta, const c10::optional<at::Tensor>& frow) {
+  check_2d(z, "z");
+  check_dtype(z, at::kFloat, "z");
+  TORCH_CHECK(kind >= 0 && kind <= 6, "unknown 2-D target kind");
+  TORCH_CHECK(z.size(1) == 2 && z.stride(1) == 1, "z must be [B, 2] with unit column stride");
+  const int B = z.size(0);
+  // float2 row loads / stores: 8-B aligned rows
+  auto al8 = [](const at::Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 8 == 0; };
+  TORCH_CHECK(ld_of(z) % 2 == 0 && al8(z), "z rows must be 8-B aligned");
+  long ldg = 0;
+  if (grad && grad->defined()) {
+    check_2d(*grad, "grad");
+    check_dtype(*grad, at::kFloat, "grad");
+    TORCH_CHECK(grad->size(0) == B && grad->size(1) == 2 && grad->stride(1) == 1, "grad shape");
+    ldg = ld_of(*grad);
+    TORCH_CHECK(ldg % 2 == 0 && al8(*grad), "grad rows must be 8-B aligned");
+  }
+  auto vec = [&](const c10::optional<at::Tensor>& t, const char* nm) {
+    if (t && t->defined()) {
+      check_dtype(*t, at::kFloat, nm);
+      TORCH_CHECK(t->is_contiguous() && t->numel() == B, nm, " must be a contiguous (B,) vector");
+    }
+  };
+  vec(logp, "logp");
+  vec(logq0, "logq0");
+  vec(ldj, "ldj");
+  vec(frow, "frow");
+  if (beta && beta->defined()) {
+    check_dtype(*beta, at::kFloat, "beta");
+    TORCH_CHECK(beta->numel() >= 1, "beta");
+  }
+  nf_launch_energy2d((int)kind, z.data_ptr<float>(), ld_of(z), opt_ptr<float>(logp),
+                     opt_ptr<float>(grad), ldg, (float)gscale, opt_ptr<float>(logq0),
+                     opt_ptr<float>(ldj), opt_ptr<float>(beta), opt_ptr<float>(frow), B,
+                     cur_stream());
+}
+
 // ---------------------------------------------------------------- sampling
 void reparam_sample(const c10::optional<at::Tensor>& mu, const c10::optional<at::Tensor>& logvar,
                     int64_t seed, const c10::optional<at::Tensor>& offset, int64_t offset_host,
@@ -309,6 +349,8 @@ TORCH_LIBRARY(vinf, m) {
         "Tensor(c!)? logp_out, Tensor(d!)? frow_out) -> ()");
   m.def("bernoulli_logits(Tensor logits, Tensor x, Tensor(a!)? dlogits, Tensor? coef, "
         "float coef_host, Tensor(b!)? logpx) -> ()");
+  m.def("energy2d(int kind, Tensor z, Tensor(a!)? logp, Tensor(b!)? grad, float gscale, "
+        "Tensor? logq0, Tensor? ldj, Tensor? beta, Tensor(c!)? frow) -> ()");
   m.def("reparam_sample(Tensor? mu, Tensor? logvar, int seed, Tensor? offset, int offset_host, "
         "int stream_id, Tensor(a!) z, Tensor(b!)? eps, Tensor(c!)? zbf, int nbf, "
         "Tensor(d!)? logq0) -> ()");
@@ -328,6 +370,7 @@ TORCH_LIBRARY_IMPL(vinf, CUDA, m) {
   m.impl("coupling_bwd", &coupling_bwd);
   m.impl("target_logp_grad", &target_logp_grad);
   m.impl("bernoulli_logits", &bernoulli_logits);
+  m.impl("energy2d", &energy2d);
   m.impl("reparam_sample", &reparam_sample);
   m.impl("normal_fill", &normal_fill);
   m.impl("reparam_grad", &reparam_grad);

@@ -117,6 +117,9 @@ struct GemmArgs {
   // ldj share is -sum alpha, C = s_raw; with f8_cq also the e4m3 copy of u (delayed scale)
   int cf_pair;
   int cf_mode;
+  // cf_mode 0 inverse: x = (y - t) e^-s from the layer's output y (cf_x) into cf_y / cf_yb, the
+  // ldj share is -sum s; C (s_hat) may be null
+  int cf_inverse;
 };
 
 // The alignment the LDS-staged epilogue's 16-B row accesses need (host side); shapes that miss

@@ -28,6 +28,11 @@ void nf_launch_target_logp_grad(int kind, const float* A, long lda, const float*
 void nf_launch_bernoulli_logits(const void* logits, int is_bf16, long ldl_, const float* x, long ldx,
                                 void* dlogits, long ldd, const float* coef_ptr, float coef_host,
                                 float* logpx, int B, int P, hipStream_t stream);
+// energy2d.hip: the reference's 2-D targets (U1-U4, trial1): log p, gscale * beta * grad log p,
+// optional ELBO row logq0 - ldj - beta log p; z [B][2] fp32 rows (ldz, ldg even)
+void nf_launch_energy2d(int kind, const float* z, long ldz, float* logp, float* grad, long ldg,
+                        float gscale, const float* logq0, const float* ldj, const float* beta,
+                        float* frow, int B, hipStream_t stream);
 
 // sampling.hip
 void nf_launch_reparam_sample(const float* mu, const float* logvar, uint64_t seed,
@@ -119,7 +124,7 @@ void nf_launch_gemm256_nt_cpl(const void* h, long ldh, const void* W, long ldw, 
                               const void* bias, void* st, long ld_st, int M, int K, int Dh,
                               const float* x, long ld_x, float* y, long ld_y, void* yb, long ld_yb,
                               int yb_width, float* ldjp, long ld_ldjp, int ldj_init, float scale,
-                              hipStream_t stream);
+                              hipStream_t stream, int inverse = 0);
 // input gradient of coupling layer l's conditioner (fp32, + G) fused with coupling layer l-1's
 // backward: writes dst (bf16 [dS_hat | dT | 0]) and gx; G itself is not written
 // e4m3 operand scales of an fp8 product: sa (A, per-tensor), sb (B, per-row) and the optional

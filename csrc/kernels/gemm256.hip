@@ -330,6 +330,16 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
               y[e] = (xs[e] - tv) * __expf(-al);
               part -= al;
             }
+          } else if (a.cf_inverse) {   // x = (y - t) e^-s, ldj share -sum s
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const unsigned us = sh[e >> 1], ut = tt[e >> 1];
+              const float shv = __uint_as_float((e & 1) ? (us & 0xffff0000u) : (us << 16));
+              const float tv = __uint_as_float((e & 1) ? (ut & 0xffff0000u) : (ut << 16));
+              const float sv = a.cf_scale * fast_tanhf(shv);
+              y[e] = (xs[e] - tv) * __expf(-sv);
+              part -= sv;
+            }
           } else {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -367,8 +377,9 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
             o.w = (unsigned)f2bf(y[6]) | ((unsigned)f2bf(y[7]) << 16);
             *reinterpret_cast<uint4*>(a.cf_yb + (long)m * a.ld_cf_yb + jf) = o;
           }
-          *reinterpret_cast<uint4*>((bf16_t*)a.C + (long)m * a.ldc + jf) =
-              make_uint4(sh[0], sh[1], sh[2], sh[3]);
+          if (a.C)
+            *reinterpret_cast<uint4*>((bf16_t*)a.C + (long)m * a.ldc + jf) =
+                make_uint4(sh[0], sh[1], sh[2], sh[3]);
         } else if (a.cf_yb && jf < a.cf_yb_width) {   // zero the next operand's pad columns
           *reinterpret_cast<uint4*>(a.cf_yb + (long)m * a.ld_cf_yb + jf) = make_uint4(0, 0, 0, 0);
         }
@@ -1179,7 +1190,7 @@ void nf_launch_gemm256_nt_cpl(const void* h, long ldh, const void* W, long ldw, 
                               const void* bias, void* st, long ld_st, int M, int K, int Dh,
                               const float* x, long ld_x, float* y, long ld_y, void* yb, long ld_yb,
                               int yb_width, float* ldjp, long ld_ldjp, int ldj_init, float scale,
-                              hipStream_t stream) {
+                              hipStream_t stream, int inverse) {
   if (M <= 0) return;
   GemmArgs a{};
   a.A = (const nf::bf16_t*)h; a.lda = ldh;
@@ -1193,10 +1204,11 @@ void nf_launch_gemm256_nt_cpl(const void* h, long ldh, const void* W, long ldw, 
   a.cf_yb = (nf::bf16_t*)yb; a.ld_cf_yb = ld_yb; a.cf_yb_width = yb_width;
   a.cf_ldj = ldjp; a.ld_cf_ldj = ld_ldjp; a.cf_ldj_init = ldj_init;
   a.cf_dh = Dh; a.cf_b_rows = w_rows; a.cf_scale = scale; a.cf_pair = Dh;
+  a.cf_inverse = inverse;
   auto al16 = [](const void* p) { return ((unsigned long)p & 15) == 0; };
-  if (Dh % 8 || w_rows < 2 * Dh || ld_x % 4 || ld_y % 4 || ld_st % 8 ||
+  if (Dh % 8 || w_rows < 2 * Dh || ld_x % 4 || ld_y % 4 || (st && ld_st % 8) ||
       (yb && (ld_yb % 8 || !al16(yb) || yb_width < Dh || yb_width % 8)) || !al16(x) || !al16(y) ||
-      !al16(st)) {
+      !al16(st) || (!st && !inverse)) {
     fprintf(stderr, "vinf: fused coupling-forward GEMM needs Dh %% 8 == 0, 16-B aligned rows and "
                     "2 Dh weight rows\n");
     abort();

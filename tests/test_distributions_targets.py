@@ -99,3 +99,19 @@ def test_log_normalizers():
     # exactly normalised: E_{N(0, I)}[p/N] = 1 via importance sampling
     lw = b.log_prob(z) - (-0.5 * (z * z).sum(1) - 2 * math.log(2 * math.pi))
     assert torch.logsumexp(lw, 0).item() - math.log(z.shape[0]) == pytest.approx(0.0, abs=0.05)
+
+
+def test_2d_targets_name_their_fused_kernel_kind():
+    """GPU fp32 log_prob of the 2-D reference targets goes to csrc/kernels/energy2d.hip
+    (tests/test_energy2d_gpu.py checks it against these composites); on CPU it IS the composite."""
+    from vi_normflows_amd.ops.fused import ENERGY2D_KINDS
+
+    kinds = {("U1", ()): "U1", ("U2", (("gate", False),)): "U2", ("U2", ()): "U2_gated",
+             ("U3", ()): "U3", ("U4", ()): "U4", ("U4", (("theano", True),)): "U4_theano",
+             ("trial1", ()): "trial1"}
+    z = torch.randn(64, 2)
+    for (name, kw), kname in kinds.items():
+        t = get_target(name, **dict(kw))
+        assert t.kernel_kind == ENERGY2D_KINDS[kname]
+        assert torch.equal(t.log_prob(z), t.fn(z))
+    assert get_target("gmm").kernel_kind is None

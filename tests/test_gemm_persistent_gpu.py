@@ -231,3 +231,44 @@ def test_wgrad_xcd_packing_bitwise(gpu):
         torch.ops.vinf.gemm_wgrad_xcd_pack(prev)
     assert torch.equal(out[0], out[1])
     assert out[0].abs().sum() > 0
+
+
+@pytest.mark.parametrize("M,K,init", [(700, 1024, True), (65, 512, False), (65536, 1024, True),
+                                      (4096, 256, False)])
+def test_cpl_fwd_persistent_matches_one_tile_per_block(gpu, M, K, init):
+    """The fused coupling forward on the persistent kernel (one LDS-DMA stream per CU, two
+    staged row passes) vs the one-tile-per-block kernel (gemm_persist(0), one pass) at Dh = 392
+    (3 x 128 + an 8-feature edge column tile): the same MFMA k-sequence and epilogue math, so
+    s_hat, y and its bf16 copy are bitwise equal, the pad columns are zeroed, and the log-det
+    partial rows agree (also under ldj accumulate)."""
+    from vi_normflows_amd.ops import gemm
+
+    torch.manual_seed(11)
+    Dh = 392
+    h = _bf(M, K, device=gpu)
+    W = torch.zeros(800, K, device=gpu)
+    W[:2 * Dh] = torch.randn(2 * Dh, K, device=gpu) * 0.03
+    W = W.to(torch.bfloat16)
+    b = (torch.randn(800, device=gpu) * 0.1).to(torch.bfloat16)
+    x = torch.randn(M, Dh, device=gpu)
+    ldj0 = torch.randn(4, M, device=gpu)
+    outs = []
+    prev = torch.ops.vinf.gemm_persist(1)
+    try:
+        for persist in (1, 0):
+            torch.ops.vinf.gemm_persist(persist)
+            st = torch.full((M, 800), 5.0, device=gpu).to(torch.bfloat16)
+            y = torch.full((M, Dh), 7.0, device=gpu)
+            yb = torch.full((M, 416), 3.0, device=gpu).to(torch.bfloat16)
+            ldjp = ldj0.clone()
+            gemm.linear_fwd_coupling(h, W, b, st, x, y, yb, ldjp, init, 0.5)
+            outs.append((st[:, :Dh].clone(), y, yb, ldjp))
+    finally:
+        torch.ops.vinf.gemm_persist(prev)
+    torch.cuda.synchronize()
+    (s1, y1, b1, l1), (s2, y2, b2, l2) = outs
+    assert torch.equal(s1, s2)
+    assert torch.equal(y1, y2)
+    assert torch.equal(b1, b2)
+    assert (b1[:, Dh:] == 0).all()
+    assert torch.equal(l1, l2)

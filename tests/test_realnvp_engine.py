@@ -418,9 +418,11 @@ def test_engine_log_prob_inverts_sample_cpu():
 @pytest.mark.gpu
 def test_engine_log_prob_round_trip_headline_shape_gpu(gpu):
     """North-star inverse on the HIP path at the headline model shape (RealNVP-32, 784-d,
-    conditioner 392-1024-1024-784): sample() -> log_prob() reproduces the engine's log q to
-    1e-2 relative (bf16 MFMA conditioners, fp32 state / log-dets), and matches an fp32 oracle
-    (a CPU fp32 engine with the same master weights) on 256 of the points to 1e-2 relative."""
+    conditioner 392-1024-1024-784; the inverse map fused into the last conditioner product's
+    epilogue): sample() -> log_prob() reproduces the engine's log q to 2e-3 relative (bf16 MFMA
+    conditioners, fp32 state / log-dets; round 4 measured 1.4e-4), matches an fp32 oracle (a
+    CPU fp32 engine with the same master weights) on 256 of the points to 2e-3 relative, and
+    the unfused inverse (conditioner output through coupling.hip) to 1e-4."""
     eng = _nontrivial_engine(gpu, 784, 32, 1024, 4096, 150)
     z, lq = eng.sample()
     assert float(z.abs().max()) < 1e3 and float(eng.ldj.abs().mean()) > 1.0
@@ -428,14 +430,21 @@ def test_engine_log_prob_round_trip_headline_shape_gpu(gpu):
     torch.cuda.synchronize()
     rel = float(((lp - lq).abs() / lq.abs().clamp_min(1.0)).max())
     print(f"[realnvp inverse] round trip max rel |log q| diff {rel:.2e}, mean log q {float(lq.mean()):.2f}")
-    assert torch.isfinite(lp).all() and rel <= 1e-2
+    assert torch.isfinite(lp).all() and rel <= 2e-3
+    assert eng.cf_fuse
+    eng.cf_fuse = False           # the same engine through the separate coupling kernel
+    lu = eng.log_prob(z)
+    eng.cf_fuse = True
+    rel_u = float(((lp - lu).abs() / lu.abs().clamp_min(1.0)).max())
+    print(f"[realnvp inverse] fused vs unfused inverse max rel {rel_u:.2e}")
+    assert rel_u <= 1e-4
     cpu = RealNVPVI(eng.cfg, batch=256, device="cpu", seed=3)
     cpu.params.master.copy_(eng.params.master.cpu())
     cpu.params.sync_compute()
     lo = cpu.log_prob(z[:256].cpu())
     rel_o = float(((lp[:256].cpu() - lo).abs() / lo.abs().clamp_min(1.0)).max())
     print(f"[realnvp inverse] GPU vs fp32 oracle max rel {rel_o:.2e}")
-    assert rel_o <= 1e-2
+    assert rel_o <= 2e-3
 
 
 @pytest.mark.gpu

@@ -46,8 +46,15 @@ class Target:
     logZ: float | None = None
     grid: tuple = (-6.0, 6.0)
     meta: dict = field(default_factory=dict)
+    kernel_kind: int | None = None    # csrc/kernels/energy2d.hip kind (2-D reference targets)
+    fused: bool = True                # GPU fp32 z -> that kernel (log p and its gradient)
 
     def log_prob(self, z: torch.Tensor) -> torch.Tensor:
+        if (self.fused and self.kernel_kind is not None and z.is_cuda
+                and z.dtype == torch.float32 and z.dim() == 2 and z.shape[1] == 2):
+            from ..ops.fused import energy2d_logp
+
+            return energy2d_logp(self.kernel_kind, z)
         return self.fn(z)
 
     def energy(self, z):
@@ -180,17 +187,19 @@ def get_target(name: str, dim: int | None = None, **kw) -> Target:
     """Targets by name (reference aliases p1..p4, gmm, trial1 accepted)."""
     n = name.lower()
     if n in ("u1", "p1", "two_moons", "ring"):
-        return Target("U1", 2, _u1, grid=(-4.5, 4.5))
+        return Target("U1", 2, _u1, grid=(-4.5, 4.5), kernel_kind=0)
     if n in ("u2", "p2"):
         gate = kw.get("gate", True)
         return Target("U2", 2, _u2(gate), logZ=math.log(8 * 0.4 * math.sqrt(2 * math.pi)) if gate
-                      else None, grid=(-6, 6))
+                      else None, grid=(-6, 6), kernel_kind=2 if gate else 1)
     if n in ("u3", "p3"):
-        return Target("U3", 2, _u3, grid=(-6, 6), meta={"improper": True})
+        return Target("U3", 2, _u3, grid=(-6, 6), meta={"improper": True}, kernel_kind=3)
     if n in ("u4", "p4"):
-        return Target("U4", 2, _u4(kw.get("theano", False)), grid=(-6, 6), meta={"improper": True})
+        th = kw.get("theano", False)
+        return Target("U4", 2, _u4(th), grid=(-6, 6), meta={"improper": True},
+                      kernel_kind=5 if th else 4)
     if n == "trial1":
-        return Target("trial1", 2, _trial1, grid=(-6, 6))
+        return Target("trial1", 2, _trial1, grid=(-6, 6), kernel_kind=6)
     if n in ("gmm", "gmm1d"):  # get_data.py:59-64
         return Target("gmm1d", 1, gmm1d([0.3, 0.7], [-1, 3], [1, 1]), logZ=0.0, grid=(-8, 10))
     if n == "gmm1d_sym":  # experimentation.py:18-23

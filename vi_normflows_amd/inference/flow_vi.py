@@ -106,7 +106,7 @@ def fit_flow_vi(target="U1", flow="planar", K: int = 8, iters: int = 10000, lr: 
 
 
 def optimise(func, num_samples: int, num_iter: int, lr: float, K: int, dim_z: int = 2,
-             optimizer: str = "rmsprop", verbose: bool = True):
+             optimizer: str = "rmsprop", verbose: bool = True, device="cpu", seed: int = 0):
     """``get_data.optimise`` signature: planar VI with W=U=b=0.1 init, RMSProp (get_data.py:119-142).
 
     ``func`` is a target name ("p1".."p4", "gmm", "trial1") or a :class:`Target`.
@@ -120,7 +120,8 @@ def optimise(func, num_samples: int, num_iter: int, lr: float, K: int, dim_z: in
 
     tgt = get_target(func) if isinstance(func, str) else func
     assert tgt.dim == dim_z, f"target is {tgt.dim}-D, dim_z={dim_z}"
-    res = fit_flow_vi(tgt, "planar", K, num_iter, lr, num_samples, optimizer, callback=cb)
+    res = fit_flow_vi(tgt, "planar", K, num_iter, lr, num_samples, optimizer, device=device,
+                      seed=seed, callback=cb)
     if verbose:
         print("\nFINAL METRICS\n")
         print("Free energy: ", res.final["free_energy"])

@@ -632,9 +632,12 @@ class RealNVPVI:
             h_l = (h_{l+2} - t(h_{l+1})) e^{-s(h_{l+1})},  ldj_inv = -sum_l sum_j s_l
 
         Each layer's conditioner runs on the MFMA kernels from the bf16 copy of h_{l+1} (the
-        operand the forward used), and the inverse affine map + log-det on the HIP coupling
-        epilogue (coupling.hip, ``inverse``), which also writes the bf16 conditioner input of
-        the next (lower) layer. The reference's flows are forward-only
+        operand the forward used). On the fused path (``cf_fuse``) the inverse affine map and
+        the log-det share run in the epilogue of the conditioner's last product (gemm256
+        ``EPI_CPL_FWD`` with ``cf_inverse``: s_hat / t never leave registers and LDS, and the
+        epilogue writes h_l in fp32, its bf16 copy - the next lower layer's conditioner input -
+        and the per-column-tile ldj shares); otherwise the conditioner output goes through the
+        HIP coupling kernel (coupling.hip, ``inverse``). The reference's flows are forward-only
         (``normflows/normflows/flows.py:8-34``); the inverse is a north-star addition."""
         cfg = self.cfg
         n, D = z.shape
@@ -649,11 +652,22 @@ class RealNVPVI:
         top = self.Hbf[L - 1]
         top[:, Dh:].zero_()
         top[:, :Dh].copy_(self.h(L))
+        fuse = self.cf_fuse and gemm.backend() == "mfma"
+        P, nh = self.params, cfg.n_hidden
         for l in range(L - 1, -1, -1):
-            st = self._conditioner_fwd(l, self.Hbf[l])
             nxt = self.Hbf[l - 1] if l > 0 else None
+            if fuse:
+                a = self._conditioner_hidden(l, self.Hbf[l])
+                gemm.linear_fwd_coupling(a, P.c(f"l{l}.W{nh}"), P.c(f"l{l}.b{nh}"), None,
+                                         self.h(l + 2), self.h(l), nxt, self.ldjp,
+                                         ldj_init=(l == L - 1), scale=cfg.scale_bound,
+                                         inverse=True)
+                continue
+            st = self._conditioner_fwd(l, self.Hbf[l])
             fused.coupling_fwd(st, self.h(l + 2), self.h(l), ybf=nxt, ssav=None, ldj=self.ldj,
                                scale=cfg.scale_bound, inverse=True, ldj_init=(l == L - 1))
+        if fuse:
+            torch.sum(self.ldjp, 0, out=self.ldj)
         return self.z0[:n].clone(), self.ldj[:n].clone()
 
     @torch.no_grad()

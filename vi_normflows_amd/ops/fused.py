@@ -114,6 +114,57 @@ def target_logp_grad(kind, A, Bh, gA=None, gB=None, grad_accumulate=False, param
         ref.target_logp_grad(*args)
 
 
+# csrc/kernels/energy2d.hip target kinds (reference get_data.py:20-66, theano_implement.py:56-75)
+ENERGY2D_KINDS = {"U1": 0, "U2": 1, "U2_gated": 2, "U3": 3, "U4": 4, "U4_theano": 5, "trial1": 6}
+_energy2d_launches = 0
+
+
+def energy2d(kind, z, logp=None, grad=None, gscale=1.0, logq0=None, ldj=None, beta=None,
+             frow=None):
+    """One HIP pass over z [B, 2] fp32: log p(z) of a 2-D reference target, ``gscale * beta *
+    grad log p`` and the ELBO row ``logq0 - ldj - beta log p`` (each output optional; ``beta``
+    a device scalar or None = 1). GPU only: the CPU composite is the torch energy itself."""
+    global _energy2d_launches
+    if not _gpu(z):
+        raise RuntimeError("energy2d is the HIP kernel; CPU callers use Target.log_prob")
+    native().energy2d(int(kind), z, logp, grad, float(gscale), logq0, ldj, beta, frow)
+    _energy2d_launches += 1
+
+
+def energy2d_launches(reset: bool = False) -> int:
+    """Number of energy2d kernel launches so far (evidence that the fused target ran)."""
+    global _energy2d_launches
+    n = _energy2d_launches
+    if reset:
+        _energy2d_launches = 0
+    return n
+
+
+class Energy2DLogp(torch.autograd.Function):
+    """log p(z) of a 2-D reference target with grad log p from the SAME HIP pass
+    (csrc/kernels/energy2d.hip): the backward is one broadcast multiply by the incoming
+    per-row gradient instead of the ~30-kernel autograd graph of the torch composite
+    (sin / exp / sigmoid / logaddexp / norm and their derivatives)."""
+
+    @staticmethod
+    def forward(ctx, z, kind):
+        zc = z.contiguous()
+        lp = torch.empty(zc.shape[0], device=zc.device, dtype=torch.float32)
+        g = torch.empty_like(zc)
+        energy2d(kind, zc, logp=lp, grad=g)
+        ctx.save_for_backward(g)
+        return lp
+
+    @staticmethod
+    def backward(ctx, go):
+        (g,) = ctx.saved_tensors
+        return g * go.unsqueeze(1), None
+
+
+def energy2d_logp(kind: int, z: torch.Tensor) -> torch.Tensor:
+    return Energy2DLogp.apply(z, int(kind))
+
+
 def bernoulli_logits(logits, x, dlogits=None, coef=None, coef_host=1.0, logpx=None):
     if _gpu(logits):
         native().bernoulli_logits(logits, x, dlogits, coef, float(coef_host), logpx)

@@ -108,9 +108,9 @@ def linear_dgrad(dy: torch.Tensor, W: torch.Tensor, out: torch.Tensor,
 
 
 def linear_fwd_coupling(h: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None,
-                        st: torch.Tensor, x: torch.Tensor, y: torch.Tensor,
+                        st: torch.Tensor | None, x: torch.Tensor, y: torch.Tensor,
                         ybf: torch.Tensor | None, ldjp: torch.Tensor, ldj_init: bool,
-                        scale: float) -> None:
+                        scale: float, inverse: bool = False) -> None:
     """Last conditioner product of an affine coupling layer fused with the coupling forward
     (MFMA path: one GEMM, ``EPI_CPL_FWD`` - each column tile computes the s_hat AND t columns of
     the same 128 features, so the epilogue can apply the coupling):
@@ -119,12 +119,17 @@ def linear_fwd_coupling(h: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None
         st[:, :Dh] = s_hat (bf16),  ybf = bf16(y) (zero pad),  ldjp[tn] (+)= sum of s over tile tn
 
     ``ldjp`` [ceil(Dh/128), B]: per-column-tile partial log-dets (the caller sums them; no
-    atomics, bitwise reproducible). Elsewhere: torch, with the whole sum in ``ldjp[0]``."""
+    atomics, bitwise reproducible). Elsewhere: torch, with the whole sum in ``ldjp[0]``.
+
+    ``inverse``: the same product drives the inverse map of the layer - ``x`` is the layer's
+    OUTPUT, ``y = (x - t) e^{-s}`` its input, the log-det shares are ``-sum s`` and ``st`` may
+    be None (s_hat not stored)."""
     Dh = x.shape[1]
     if _mfma_ok(h, W):
         from ._ext import native
 
-        native().gemm_nt_cpl(h, W, b, st, x, y, ybf, ldjp, bool(ldj_init), float(scale))
+        native().gemm_nt_cpl(h, W, b, st, x, y, ybf, ldjp, bool(ldj_init), float(scale),
+                             bool(inverse))
         return
     o = h.float() @ W.float().t()
     if b is not None:
@@ -132,13 +137,14 @@ def linear_fwd_coupling(h: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None
     o = o.to(st.dtype).float()
     sh, t = o[:, :Dh], o[:, Dh:2 * Dh]
     s = scale * torch.tanh(sh)
-    yv = x * torch.exp(s) + t
-    st[:, :Dh].copy_(sh)
+    yv = (x - t) * torch.exp(-s) if inverse else x * torch.exp(s) + t
+    if st is not None:
+        st[:, :Dh].copy_(sh)
     y.copy_(yv)
     if ybf is not None:
         ybf[:, :Dh].copy_(yv)
         ybf[:, Dh:].zero_()
-    part = s.sum(1)
+    part = -s.sum(1) if inverse else s.sum(1)
     if ldj_init:
         ldjp.zero_()
         ldjp[0].copy_(part)
