@@ -48,7 +48,7 @@ def main(argv=None):
     if a.device != "cpu":
         print(f"[get_data] device {a.device}: {a.num_iter} iterations x {a.samples} samples in "
               f"{dt:.2f} s ({a.num_iter * a.samples / dt:.3e} samples/s); fused target kernel "
-              f"launches: {fused.energy2d_launches()}")
+              f"launches: {fused.energy2d_launches()}; final F {res.final['free_energy']:.4f}")
     return res
 
 

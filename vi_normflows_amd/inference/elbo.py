@@ -13,28 +13,44 @@ F = E_{q0}[ log q0(z0) - sum_k log|det J_k| - beta_t log p(x, z_K) ]  (= -ELBO a
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass, field
-
 import torch
 
 EPS = 1e-7
 LOG2PI = math.log(2 * math.pi)
 
 
-@dataclass
 class FreeEnergy:
-    F: torch.Tensor                       # scalar, differentiable
-    stats: dict = field(default_factory=dict)
+    """``F`` (scalar, differentiable) and the per-step diagnostics. ``stats`` may be given as a
+    dict or as a zero-argument callable that builds it: the estimators pass a callable, so a
+    training step never waits on the device for diagnostics nobody reads (the trainer reads
+    them at log steps only; on the GPU each eager ``float(mean)`` was a host sync per step)."""
+
+    __slots__ = ("F", "_stats", "_make")
+
+    def __init__(self, F: torch.Tensor, stats=None):
+        self.F = F
+        self._make = stats if callable(stats) else None
+        self._stats = None if callable(stats) else dict(stats or {})
+
+    @property
+    def stats(self) -> dict:
+        if self._stats is None:
+            self._stats = self._make()
+            self._make = None
+        return self._stats
 
     def item(self) -> float:
         return float(self.F.detach())
 
 
 def _stats(lq0, ldj, lp, beta):
-    lqK = lq0 - ldj
-    return {"log_q0": float(lq0.mean()), "ldj": float(ldj.mean()), "log_p": float(lp.mean()),
-            "log_qK": float(lqK.mean()), "joint": float(lp.mean()), "entropy": float(-lqK.mean()),
-            "beta": float(beta)}
+    """Deferred diagnostics: one stacked reduction and ONE device read when first accessed."""
+    def make():
+        lqK = lq0 - ldj
+        m = torch.stack([lq0.mean(), ldj.mean(), lp.mean(), lqK.mean()]).double().tolist()
+        return {"log_q0": m[0], "ldj": m[1], "log_p": m[2], "log_qK": m[3], "joint": m[2],
+                "entropy": -m[3], "beta": float(beta)}
+    return make
 
 
 def free_energy(base, flow, log_target, n_samples: int, beta: float = 1.0, generator=None,

@@ -88,8 +88,9 @@ class IAFVAE(nn.Module):
         F = (lq - ldj - beta * lp).mean()
         if not with_stats:   # no host syncs (hipGraph capture)
             return FreeEnergy(F, {})
-        st = {"log_q0": float(lq.mean()), "ldj": float(ldj.mean()), "log_p": float(lp.mean())}
-        return FreeEnergy(F, st)
+        lq, ldj, lp = lq.detach(), ldj.detach(), lp.detach()
+        return FreeEnergy(F, lambda: dict(zip(("log_q0", "ldj", "log_p"), torch.stack(
+            [lq.mean(), ldj.mean(), lp.mean()]).double().tolist())))
 
     @torch.no_grad()
     def sample(self, n: int, generator=None):

@@ -346,7 +346,7 @@ def run_maf(cfg, out, info, logger):
     def loss_fn(t, beta):
         x = banana_samples(cfg.batch, cfg.dim, generator=g, device=dev)
         nll = model.loss(x)
-        return FreeEnergy(nll, {"nll": float(nll)})
+        return FreeEnergy(nll, lambda: {"nll": float(nll)})
 
     tr = Trainer(model.parameters(), loss_fn,
                  TrainConfig(iters=cfg.iters, lr=cfg.lr, optimizer=cfg.optimizer,
