@@ -119,8 +119,13 @@ void gemm_fp(const at::Tensor& A, bool a_kmajor, const at::Tensor& B, bool b_kma
     dbp = dbias->data_ptr();
   }
   auto ld = [](const at::Tensor& t) { return t.size(0) <= 1 ? t.size(1) : t.stride(0); };
+  // split-K workspace for few-tile, long-K products (caching allocator: graph-capture safe)
+  const int S = nf_gemm_fp_splits(M, N, K);
+  at::Tensor work;
+  if (S > 1) work = at::empty({(long)S * ((long)M * N + M)}, C.options());
   nf_launch_gemm_fp(dt == at::kDouble, A.data_ptr(), ld(A), a_kmajor, B.data_ptr(), ld(B),
-                    b_kmajor, bp, C.data_ptr(), ld(C), dbp, M, N, K, accumulate, cur_stream());
+                    b_kmajor, bp, C.data_ptr(), ld(C), dbp, M, N, K, accumulate, cur_stream(),
+                    S > 1 ? work.data_ptr() : nullptr, S);
 }
 
 // dx = dy W  [* 1(h > 0)]: dy [M,K], W [K,N] bf16; dx bf16 (mask) or fp32 (+= when accumulate)

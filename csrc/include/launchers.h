@@ -72,9 +72,13 @@ void nf_launch_gemm_nt_f32out(const void* x, long ldx, const void* W, long ldw, 
                               int M, int N, int K, hipStream_t stream);
 // gemm_fp.hip: exact fp32 / fp64 GEMM on the f32 / f64 MFMA, C (+)= Aop Bop^T (+ bias),
 // dbias = row sums of Aop (see the kernel header for the operand layouts)
+// split-K: `work` holds splits * (M * N + M) elements of the output dtype (nf_gemm_fp_splits
+// picks the count: 1 = no split, work unused)
+int nf_gemm_fp_splits(int M, int N, int K);
 void nf_launch_gemm_fp(int is_f64, const void* A, long lda, int a_kmajor, const void* B, long ldb,
                        int b_kmajor, const void* bias, void* C, long ldc, void* dbias, int M, int N,
-                       int K, int accumulate, hipStream_t stream);
+                       int K, int accumulate, hipStream_t stream, void* work = nullptr,
+                       int splits = 1);
 void nf_launch_gemm_tn(const void* dy, long lddy, const void* x, long ldx, float* dW, long lddw,
                        float* db, int M, int N, int K, int splits, float* work,
                        hipStream_t stream);

@@ -12,7 +12,10 @@ import torch.nn.functional as F
 from vi_normflows_amd.ops.linear import MfmaLinear, linear
 
 
-SHAPES = [(37, 5, 3), (128, 392, 1024), (256, 64, 40), (1, 2, 2), (1000, 784, 200)]
+# the last two are the config-0 module shapes whose products run split-K (gemm_fp.hip: few
+# output tiles, long K - e.g. the 64 x 64 weight gradient over the batch)
+SHAPES = [(37, 5, 3), (128, 392, 1024), (256, 64, 40), (1, 2, 2), (1000, 784, 200),
+          (1024, 784, 64), (1024, 64, 64)]
 
 
 def _rel(a, b):
@@ -50,7 +53,7 @@ def test_fp32_module_layer_is_full_precision(gpu, M, K, N):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M,K,N", SHAPES[:3])
+@pytest.mark.parametrize("M,K,N", SHAPES[:3] + SHAPES[-2:])
 def test_fp64_module_layer_matches_fp64(gpu, M, K, N):
     got, ref = _run(gpu, M, K, N, torch.float64, None)
     assert got[0].dtype == torch.float64
