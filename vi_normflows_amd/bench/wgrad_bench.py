@@ -38,7 +38,7 @@ def build(B: int, layers: int, dev):
     return gemm.WgradPlan(items), grads
 
 
-def probe(B: int, iters: int, tag: str, dev):
+def probe(B: int, iters: int, tag: str, dev, only: str = ""):
     """One 256-tile product at M = N = 4096, K = B, three ways: the TN weight-gradient kernel
     on real operands, the same kernel on stride-0 operands (every k-row the same 8 KiB, so the
     operand stream always hits cache: what the loop does without memory), and the k-major NT
@@ -74,6 +74,9 @@ def probe(B: int, iters: int, tag: str, dev):
         "nn_real": lambda: gemm.linear_dgrad(dyt, x, out),
     }
     flops = 2.0 * B * n * n
+    if only:   # e.g. "tn4w_real,tn4w_cached" (counter passes: one kernel family per run)
+        keep = set(only.split(","))
+        cases = {k: v for k, v in cases.items() if k in keep}
     for name, fn in cases.items():
         for _ in range(2):
             fn()
@@ -248,6 +251,7 @@ def main(argv=None):
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--tag", default="")
     ap.add_argument("--probe", action="store_true")
+    ap.add_argument("--cases", default="", help="probe: comma-separated case names to run")
     ap.add_argument("--layout-probe", action="store_true")
     ap.add_argument("--nt-probe", action="store_true")
     ap.add_argument("--nt-probe-masks", action="store_true", help="nt probe: ReLU-mask split only")
@@ -258,7 +262,7 @@ def main(argv=None):
     a = ap.parse_args(argv)
     dev = torch.device("cuda")
     if a.probe:
-        probe(a.batch, a.iters, a.tag, dev)
+        probe(a.batch, a.iters, a.tag, dev, a.cases)
         return
     if a.nt_probe:
         nt_probe(a.batch, a.iters, a.tag, dev, a.nt_probe_masks)
