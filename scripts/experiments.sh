@@ -93,8 +93,8 @@ PY
     VINF_NATIVE_LIB=$P timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py tests/test_gemm_persistent_gpu.py tests/test_realnvp_engine.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_$v.txt 2>&1 || { tail -30 $O/pytest_$v.txt; exit 1; }
     tail -1 $O/pytest_$v.txt
     for r in 1 2; do
-      timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --tag default --iters 20 --only fwd_l1,fwd_l2,dgrad_l2 >> $O/sg.jsonl || exit 1
-      VINF_NATIVE_LIB=$P timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --tag $v --iters 20 --only fwd_l1,fwd_l2,dgrad_l2 >> $O/sg.jsonl || exit 1
+      timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --tag default --iters 20 --only fwd_l1,fwd_l2,dgrad_l3,dgrad_l2 >> $O/sg.jsonl || exit 1
+      VINF_NATIVE_LIB=$P timeout -k 10 120 python -m vi_normflows_amd.bench.step_gemms --tag $v --iters 20 --only fwd_l1,fwd_l2,dgrad_l3,dgrad_l2 >> $O/sg.jsonl || exit 1
     done
     for r in 1 2 3; do
       for lib in default $v; do
