@@ -37,6 +37,18 @@ def env_world() -> int:
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
+def rccl_env() -> None:
+    """Process-group settings for RCCL, applied before the first ``init_process_group``.
+
+    ``TORCH_NCCL_CUDA_EVENT_CACHE=0``: ProcessGroupNCCL recycles the completion events of
+    finished collectives. A warm-up all-reduce that the watchdog thread has not retired yet can
+    hand its event to a collective recorded inside a hipGraph capture. The watchdog's next
+    query of that event then fails with hipErrorCapturedEvent and terminates the process (seen
+    once on the 1-rank RCCL capture path, ``bench.py --force-reduce``). Without the cache, every
+    work owns its events, and the captured ones are never polled."""
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+
+
 def init(backend: str | None = None, device_type: str | None = None) -> DistInfo:
     """Initialise the default process group if WORLD_SIZE > 1 and pick this rank's device."""
     global _INFO
@@ -61,6 +73,7 @@ def init(backend: str | None = None, device_type: str | None = None) -> DistInfo
         kw = {}
         if backend == "nccl":
             kw["device_id"] = device
+            rccl_env()
         if "TORCHELASTIC_RESTART_COUNT" in os.environ:
             # under torchrun: key the rendezvous by restart attempt, so a job restarted by
             # --max-restarts never reads the dead attempt's peer addresses from the store

@@ -35,6 +35,9 @@ def _init_single_rank_group(info: DistInfo) -> None:
     backend = "nccl" if info.device.type == "cuda" else "gloo"
     if backend == "nccl":
         kw["device_id"] = info.device
+        from .dist import rccl_env
+
+        rccl_env()
     dist.init_process_group(backend=backend, rank=0, world_size=1, **kw)
     info.backend = backend
 
