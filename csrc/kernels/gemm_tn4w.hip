@@ -107,23 +107,33 @@ __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, ch
 #pragma unroll
     for (int i = 0; i < 8; ++i) fb[i] = read_frag<false>(st, i * 16, 0, lane);
   };
-  auto kstep = [&](const v8s (&fb)[8], auto qn_c, auto rd_c) {
+  // MFMAs of A fragment j (+ its bias-gradient dot products), then A fragment j of the next
+  // K-tile into the freed registers
+  auto mfma_j = [&](const v8s (&fb)[8], auto qn_c, auto rd_c, auto j_c) {
+    constexpr int j = decltype(j_c)::value;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int i = 0; i < 8; ++i) mfma_acc(acc[i][j], fb[i], fa[j]);
+    if constexpr (DODB) {
+      typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
+      const v2bf one = {(__bf16)1.0f, (__bf16)1.0f};
 #pragma unroll
-      for (int i = 0; i < 8; ++i) mfma_acc(acc[i][j], fb[i], fa[j]);
-      if constexpr (DODB) {
-        typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
-        const v2bf one = {(__bf16)1.0f, (__bf16)1.0f};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const unsigned w = (unsigned)(unsigned short)fa[j][2 * e] |
-                             ((unsigned)(unsigned short)fa[j][2 * e + 1] << 16);
-          dbs[j] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf, w), one, dbs[j], false);
-        }
+      for (int e = 0; e < 4; ++e) {
+        const unsigned w = (unsigned)(unsigned short)fa[j][2 * e] |
+                           ((unsigned)(unsigned short)fa[j][2 * e + 1] << 16);
+        dbs[j] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf, w), one, dbs[j], false);
       }
-      if constexpr (decltype(rd_c)::value) fa[j] = rd_a(qn_c, j);
     }
+    if constexpr (decltype(rd_c)::value) fa[j] = rd_a(qn_c, j);
+  };
+  // A fragments 1..7 of a K-tile (fragment 0 is issued first, see ktile)
+  auto kstep_from1 = [&](const v8s (&fb)[8], auto qn_c, auto rd_c) {
+    mfma_j(fb, qn_c, rd_c, std::integral_constant<int, 1>{});
+    mfma_j(fb, qn_c, rd_c, std::integral_constant<int, 2>{});
+    mfma_j(fb, qn_c, rd_c, std::integral_constant<int, 3>{});
+    mfma_j(fb, qn_c, rd_c, std::integral_constant<int, 4>{});
+    mfma_j(fb, qn_c, rd_c, std::integral_constant<int, 5>{});
+    mfma_j(fb, qn_c, rd_c, std::integral_constant<int, 6>{});
+    mfma_j(fb, qn_c, rd_c, std::integral_constant<int, 7>{});
   };
   using T = std::true_type;
   using F = std::false_type;
@@ -156,9 +166,16 @@ __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, ch
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    // the first 8 MFMAs go out right after the barrier (their operands are already in
+    // registers), the DMA issue and the next K-tile's B reads behind them: the MFMA pipe
+    // restarts one instruction after the barrier instead of ~25 (whole step -0.13 ms on one
+    // box, profiles/r5/tn4w_early_mfma_ab.jsonl)
+    mfma_j(fbc, QN{}, next_c, std::integral_constant<int, 0>{});
+    __builtin_amdgcn_sched_barrier(0);
     if constexpr (decltype(issue_c)::value) issue(t + PD, QI{});
     if constexpr (decltype(next_c)::value) rd_b(QN{}, fbn);
-    kstep(fbc, QN{}, next_c);
+    __builtin_amdgcn_sched_barrier(0);
+    kstep_from1(fbc, QN{}, next_c);
   };
   using Q0 = std::integral_constant<int, 0>;
   using Q1 = std::integral_constant<int, 1>;
