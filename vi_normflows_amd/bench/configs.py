@@ -49,6 +49,12 @@ def graphed(step_fn, dev, warmup: int = 3):
 
 
 _ENGINES: list = []   # explicit-backward engines built by build() (replica check in main)
+_RUNNERS: list = []   # their runners, closed at the end of main (restores the GEMM grid policy)
+
+
+def _runner(run):
+    _RUNNERS.append(run)
+    return run
 
 
 def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: bool = True,
@@ -71,7 +77,7 @@ def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: b
             _ENGINES.append(eng)
             X = synthetic_binary_images(max(2000, 4 * B), 784, seed=info.rank).to(dev)
             eng.set_batch(X[:B])
-            run = DataParallelRunner(eng, info)
+            run = _runner(DataParallelRunner(eng, info))
             if graph:
                 run.capture(warmup=2)
             it = [0]
@@ -134,7 +140,7 @@ def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: b
         eng = RealNVPVI(RealNVPConfig(n_layers=8 if cfg_id == 2 else 32), batch=B, device=dev,
                         rank=info.rank)
         _ENGINES.append(eng)
-        run = DataParallelRunner(eng, info)
+        run = _runner(DataParallelRunner(eng, info))
         if dev.type == "cuda":
             run.capture(warmup=1)
         return run.step, B, dev, "bf16"
@@ -147,7 +153,7 @@ def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: b
         X = synthetic_images(B * 4, device=dev, seed=info.rank).reshape(B * 4, -1)
         eng = IAFEngine(IAFVAEConfig(), B, X, device=dev, seed=0, rank=info.rank)
         _ENGINES.append(eng)
-        run = DataParallelRunner(eng, info)
+        run = _runner(DataParallelRunner(eng, info))
         if graph:
             run.capture(warmup=2)
         return run.step, B, dev, "bf16, IAF engine" + (", hipGraph" if run.graph else "")
@@ -185,7 +191,7 @@ def build(cfg_id: int, info, batch: int | None, precision: str = "fp8", graph: b
         B = batch or 8192
         eng = MAFEngine(MAFEngineConfig(precision=precision), batch=B, device=dev, rank=info.rank)
         _ENGINES.append(eng)
-        run = DataParallelRunner(eng, info)
+        run = _runner(DataParallelRunner(eng, info))
         if graph and dev.type == "cuda":
             run.capture(warmup=2)
         if precision == "fp8":
@@ -302,6 +308,8 @@ def main(argv=None):
                           "dense_calls": precision_counts(),
                           "replicas_identical": None if rep is None else rep == 0.0,
                           "max_replica_diff": rep}))
+    while _RUNNERS:
+        _RUNNERS.pop().close()
     vdist.shutdown()
 
 
