@@ -66,6 +66,8 @@ def _args(argv=None):
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--force-reduce", action="store_true",
                     help="run the bucketed all-reduce path even at world size 1 (RCCL check)")
+    ap.add_argument("--persist", choices=["fwd", "dyn", "all", "none"], default="dyn",
+                    help="multi-rank GEMM grid policy (parallel/runner.py DataParallelRunner)")
     ap.add_argument("--cpu", action="store_true", help="plumbing run on CPU (gloo; use tiny sizes)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -123,7 +125,8 @@ def main() -> int:
                         anneal_iters=10000, banana_pairing=a.pairing)
     eng = RealNVPVI(cfg, batch=a.batch, device=info.device, seed=1234, rank=info.rank, lr=a.lr,
                     lr_warmup=a.lr_warmup, max_grad_norm=a.max_grad_norm)
-    runner = DataParallelRunner(eng, info, bucket_cap_mb=a.bucket_mb, force_reduce=a.force_reduce)
+    runner = DataParallelRunner(eng, info, bucket_cap_mb=a.bucket_mb, force_reduce=a.force_reduce,
+                                persist=a.persist)
     cuda = info.device.type == "cuda"
 
     captured = False
@@ -200,6 +203,7 @@ def main() -> int:
                                    "no published number for this metric)",
                 "replicas_identical": identical,
                 "max_replica_diff": max_diff,
+                "gemm_grid_policy": a.persist if (world > 1 or a.force_reduce) else "persistent",
                 "allreduce_buckets": {"count": len(buckets),
                                       "mb": [round(b["mb"], 2) for b in buckets]},
             },

@@ -120,6 +120,10 @@ struct GemmArgs {
   // cf_mode 0 inverse: x = (y - t) e^-s from the layer's output y (cf_x) into cf_y / cf_yb, the
   // ldj share is -sum s; C (s_hat) may be null
   int cf_inverse;
+  // persistent launches with dynamic tile claims (gemm256.hip, persist mode 2): this launch's
+  // counter slot, 8 per-XCD claim counters + 1 finished-block counter, zero at launch start and
+  // zeroed again by the launch's last block
+  int* qctr;
 };
 
 // The alignment the LDS-staged epilogue's 16-B row accesses need (host side); shapes that miss

@@ -691,8 +691,24 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
 // the ring), i.e. bf16 outputs in two 64-row passes, fp32 outputs in their usual 32-row
 // passes. WAR on the slot pair: every wave's staging reads are consumed by its own stores
 // before the barrier that ends the epilogue, and the DMA into those slots is issued after it.
-template <bool A_KMAJOR, bool B_KMAJOR, int EPI>
+//
+// DYN (persist mode 2): the same body with tiles CLAIMED at run time instead of the fixed list
+// b, b + G, ...: XCD x's tiles (xcd_remap's contiguous range) are handed out by counter
+// a.qctr[x]; a block claims from its own XCD's counter only. A block that
+// starts late (its CU held by an RCCL kernel beside the backward) then takes fewer tiles, where a
+// fixed list would hold the whole launch until it ran. One lane claims (QL: wave 3, lane 0),
+// and claim latency stays off the critical path: tile s + 1 is claimed at the start of tile
+// s - 1's epilogue and resolved after that epilogue's own vmcnt(0). LDS is full (ring + staging),
+// so the id is published at the end of QL's own staging region (slot (4T + 7) % 8, T = the next
+// tile's first stream K-tile), which nothing touches between the epilogue-ending barrier and
+// the next tile's phase-2 DMA into that slot; every wave reads it at the loop top, before its
+// first barrier of the tile (read + readfirstlane: complete before any wave can issue that DMA).
+// Only the block's first claim is exposed. Every block increments a.qctr[8] once, as it
+// finishes; the last one zeroes the slot for the next launch that uses it. No block ever waits
+// on another (no spin), so the grid always drains.
+template <bool A_KMAJOR, bool B_KMAJOR, int EPI, bool DYN = false>
 __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char* smem) {
+  static_assert(!(DYN && EPI == EPI_CPL_FWD), "the coupling forward reads other waves' staging");
   constexpr int D = 4, NSLOT = 8;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -700,7 +716,31 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   const int ntiles = ntm * ntn;
   const int G = gridDim.x, b = blockIdx.x;
-  const int ns = (ntiles - b + G - 1) / G;          // tiles of this block
+  const int ns = DYN ? 0x7fffffff : (ntiles - b + G - 1) / G;   // tiles of this block
+  // DYN claims (lane QL only)
+  constexpr int QL = 192;
+  auto qaddr = [&](int T_) {   // tile id published for the tile starting at stream K-tile T_
+    return (volatile LDS_AS int*)(LDS_AS char*)(smem + ((4 * T_ + 7) & (NSLOT - 1)) * HALF_BYTES +
+                                                 HALF_BYTES - 16);
+  };
+  // one lane's claim: the VGPR offset the compiler cannot see is zero keeps the atomic optimizer
+  // from turning it into a wave-wide broadcast that waits for the result (vmcnt(0)) on the spot
+  auto claim_add = [&](int x) {
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return atomicAdd(a.qctr + x + z, 1);
+  };
+  const int xcd = b & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
+  auto xcount = [&](int x) { return x < r8 ? q8 + 1 : q8; };
+  auto xbase = [&](int x) { return x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8; };
+  // tile id for the own-XCD claim `raw`; -1: the XCD's tiles are all taken (no stealing across
+  // XCDs: RCCL's blocks spread over every XCD, and the claim code must stay register-cheap)
+  auto resolve = [&](int raw) -> int { return raw < xcount(xcd) ? xbase(xcd) + raw : -1; };
+  auto finished = [&](int old) {   // old: this block's pre-increment value of the done counter
+    if (old == G - 1)
+#pragma unroll
+      for (int x = 0; x < 9; ++x) atomicExch(a.qctr + x, 0);
+  };
   const int nkt = (a.K + BK - 1) / BK;              // K-tiles per tile
   // Column rotation: with every block holding the same number of tiles and each XCD's step-s
   // ids a run of whole tile rows, block b's s-th tile takes column (tn + s) % ntn - still one
@@ -714,6 +754,10 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
     const int id = xcd_remap(b + s * G, ntiles);
     m0 = (id / ntn) * BM;
     n0 = (rot ? (id % ntn + s) % ntn : id % ntn) * BN;
+  };
+  auto tile_at = [&](int id, int& m0, int& n0) {   // DYN: claimed tile id
+    m0 = (id / ntn) * BM;
+    n0 = (id % ntn) * BN;
   };
   // stage half j of K-tile tk of the tile at (tm0, tn0) into the ring slot of stream half
   // 4 Tg + j
@@ -831,16 +875,37 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
 
   if (ns <= 0) return;
   int m0, n0;
-  tile_org(0, m0, n0);
+  int raw = 0;   // DYN, lane QL: the claim in flight (own-XCD counter value or done count)
+  if constexpr (DYN) {
+    volatile LDS_AS int* q0 = (volatile LDS_AS int*)(LDS_AS char*)(smem + 7 * HALF_BYTES);
+    if (threadIdx.x == QL) {   // (slot 7 is free in the prologue)
+      const int id0 = resolve(claim_add(xcd));
+      *q0 = id0;
+      if (id0 < 0) finished(claim_add(8));
+      else raw = claim_add(xcd);   // tile 1, resolved after the prologue's DMA wait
+    }
+    __syncthreads();
+    const int id0 = __builtin_amdgcn_readfirstlane(*q0);
+    if (id0 < 0) return;
+    tile_at(id0, m0, n0);
+  } else {
+    tile_org(0, m0, n0);
+  }
   // prologue: the stream's first six halves (K-tile 0, and K-tile 1's A-lo / B-lo; nkt >= 2)
 #pragma unroll
   for (int h = 0; h < 6; ++h) issue_to(h >> 2, m0, n0, h >> 2, h & 3);
   vmwait<0>();
+  if constexpr (DYN) {
+    if (threadIdx.x == QL) *qaddr(0) = resolve(raw);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
   barrier();
   const bool tail_half = (a.K - (nkt - 1) * BK) <= 32;   // a tile's last K-tile has one k-step
   int T = 0;
   for (int s = 0; s < ns; ++s) {
-    const bool has_next = s + 1 < ns;
+    // DYN: tile s + 1's id, published before tile s began (prologue / the previous epilogue)
+    const int id_next = DYN ? __builtin_amdgcn_readfirstlane(*qaddr(T)) : 0;
+    const bool has_next = DYN ? id_next >= 0 : s + 1 < ns;
     if (wr == 1) barrier();
     auto tile_loop = [&](auto edge_c) {
       for (int t = 0; t < nkt - 2; ++t, ++T)
@@ -862,9 +927,15 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
     // r1) - not the free pair the epilogue stages through
     int m0n = 0, n0n = 0;
     if (has_next) {
-      tile_org(s + 1, m0n, n0n);
+      if constexpr (DYN) tile_at(id_next, m0n, n0n);
+      else tile_org(s + 1, m0n, n0n);
 #pragma unroll
       for (int h = 0; h < 6; ++h) issue_to(T + (h >> 2), m0n, n0n, h >> 2, h & 3);
+    }
+    // DYN: claim tile s + 2 (or, on the last tile, count this block finished); the result is
+    // used only after the epilogue's vmcnt(0)
+    if constexpr (DYN) {
+      if (threadIdx.x == QL) raw = claim_add(has_next ? xcd : 8);
     }
     if (wr == 0) barrier();
     // ---- epilogue of tile s through the free LDS (see above)
@@ -884,16 +955,26 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
                           },
                           lane_e, tid_e);
     } else if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_RELUMASK) {
-      epi_tile_staged<EPI, 4, false, 0, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, 0, region, lane);
+      // (DYN: offsets from the opaque lane too, else the claim's register spills them)
+      const int lane_b = DYN ? lane_e : lane;
+      epi_tile_staged<EPI, 4, false, 0, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, 0, region,
+                                           lane_b);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own readback done before re-staging
       epi_tile_staged<EPI, 4, false, 4, 8>(a, acc, m0 + wr * 128 + 64, n0 + wc * 64, 0, region,
-                                           lane);
+                                           lane_b);
     } else {
       epi_tile_staged<EPI, 8>(a, acc, m0 + wr * 128, n0 + wc * 64, 0, region, lane_e);
     }
     // the next tile's six halves (and this epilogue's stores) retired, and every wave's staging
     // reads done before the stream restages the slot pair
     vmwait<0>();
+    if constexpr (DYN) {   // tile s + 2's id, read at the top of tile s + 1 (stream K-tile T)
+      if (threadIdx.x == QL) {
+        if (has_next) *qaddr(T) = resolve(raw);
+        else finished(raw);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     barrier();
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -901,14 +982,15 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
       for (int j = 0; j < 8; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
     m0 = m0n;
     n0 = n0n;
+    if (!has_next) break;
   }
 }
 
-template <bool A_KMAJOR, bool B_KMAJOR, int EPI>
+template <bool A_KMAJOR, bool B_KMAJOR, int EPI, bool DYN = false>
 __global__ void __launch_bounds__(NTHR, 1) gemm256_persistent_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[8 * HALF_BYTES + 8 * 4096];
   NF_STAMP(5);   // stamps build: block start / end (the body ends on vmcnt(0) + barrier)
-  gemm256_persistent_body<A_KMAJOR, B_KMAJOR, EPI>(a, smem);
+  gemm256_persistent_body<A_KMAJOR, B_KMAJOR, EPI, DYN>(a, smem);
   NF_STAMP(6);
 }
 
@@ -1006,10 +1088,20 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
   gemm256_body<A_KM, B_KM, EPI_F32, D, true, F8>(a, local, 0, smem);
 }
 
-// persistent plain products (on by default), nf_gemm256_set_persist: the DP runner turns it off
-// for multi-rank backwards (RCCL kernels take CUs while a grid of exactly one block per CU runs,
-// and a persistent block that cannot start delays its whole tile list)
+// persistent plain products, nf_gemm256_set_persist: 1 (default) fixed tile lists, 2 tiles
+// claimed at run time (the DP runner's multi-rank backward: RCCL kernels take CUs while a grid of
+// one block per CU runs, and a fixed-list block that cannot start delays its whole list),
+// 0 one block per tile
 static int g_persist = 1;
+
+// mode 2's claim counters: QSLOTS slots of 16 ints (8 per-XCD counters + the finished-block
+// count), one slot per launch in rotation. Allocated and zeroed by the first
+// nf_gemm256_set_persist(2) (outside any graph capture); each launch's last block re-zeroes its
+// slot. Launches of one stream never overlap, and 256 slots keep even concurrent streams apart.
+constexpr int QSLOTS = 256;
+static int* g_qctr = nullptr;
+static int g_qctr_dev = -1;
+static unsigned g_qslot = 0;
 
 // CUs the persistent grid leaves free (nf_gemm256_set_reserve): a multi-rank backward runs
 // RCCL kernels beside the GEMMs, and a persistent block queued behind one would hold back its
@@ -1064,10 +1156,24 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
     int cus = (device_cus_256() - g_reserve) & ~7;   // whole XCD rounds: xcd_remap's b & 7
     cus = cus > 8 ? cus : 8;
     const int G = ntiles < cus ? ntiles : cus;
-    hipLaunchKernelGGL((gemm256_persistent_kernel<AK, BK_, EPI>), dim3(G), dim3(NTHR), 0, stream,
-                       a);
-    NF_HIP_CHECK(hipGetLastError());
-    return;
+    // (mode 2 excludes the coupling forward: its epilogue reads other waves' staging regions,
+    // where the claimed id is published; the engines run their forwards in mode 1)
+    if constexpr (EPI != EPI_CPL_FWD) {
+      int dev = -1;
+      if (g_persist == 2 && g_qctr && hipGetDevice(&dev) == hipSuccess && dev == g_qctr_dev) {
+        a.qctr = g_qctr + 16 * (g_qslot++ % QSLOTS);
+        hipLaunchKernelGGL((gemm256_persistent_kernel<AK, BK_, EPI, true>), dim3(G), dim3(NTHR),
+                           0, stream, a);
+        NF_HIP_CHECK(hipGetLastError());
+        return;
+      }
+    }
+    if (g_persist == 1) {
+      hipLaunchKernelGGL((gemm256_persistent_kernel<AK, BK_, EPI>), dim3(G), dim3(NTHR), 0,
+                         stream, a);
+      NF_HIP_CHECK(hipGetLastError());
+      return;
+    }
   }
   }
   dim3 grid(a.pair_tiles ? ntm * (ntn / 2) : ntm * ntn, splits), block(NTHR);
@@ -1100,7 +1206,22 @@ int nf_gemm256_set_pair(int mode) {   // mode < 0: query; returns the previous s
   if (mode >= 0) g256::g_pair = mode > 2 ? 2 : mode;
   return prev;
 }
-void nf_gemm256_set_persist(int on) { g256::g_persist = on ? 1 : 0; }
+void nf_gemm256_set_persist(int mode) {
+  using namespace g256;
+  g_persist = mode == 2 ? 2 : mode ? 1 : 0;
+  int dev = -1;
+  if (g_persist == 2 && !g_qctr && hipGetDevice(&dev) == hipSuccess) {
+    void* p = nullptr;
+    if (hipMalloc(&p, QSLOTS * 16 * sizeof(int)) == hipSuccess &&
+        hipMemset(p, 0, QSLOTS * 16 * sizeof(int)) == hipSuccess &&
+        hipDeviceSynchronize() == hipSuccess) {
+      g_qctr = (int*)p;
+      g_qctr_dev = dev;
+    } else {
+      fprintf(stderr, "vinf: persist mode 2 counters unavailable, using one block per tile\n");
+    }
+  }
+}
 int nf_gemm256_set_reserve(int cus) {
   const int prev = g256::g_reserve;
   if (cus >= 0) g256::g_reserve = cus;

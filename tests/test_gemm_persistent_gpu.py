@@ -173,10 +173,12 @@ def test_persistent_grid_reserve_bitwise(gpu, reserve):
     assert torch.equal(y0, y1) and torch.equal(m0, m1)
 
 
-def test_engine_persistent_forward_only_bitwise(gpu):
-    """DP policy (parallel/runner.py): persistent grid in the forward only, one block per tile in
-    the backward. Same K order per tile -> loss and every gradient bitwise equal to the
-    all-persistent step, and the global switch is left off for the backward's collectives."""
+@pytest.mark.parametrize("bwd_mode", [0, 2], ids=["one_tile_per_block", "claimed_tiles"])
+def test_engine_persistent_forward_only_bitwise(gpu, bwd_mode):
+    """DP policies (parallel/runner.py): persistent grid in the forward, and in the backward one
+    block per tile ("fwd") or persistent blocks claiming tiles at run time ("dyn", mode 2). Same
+    K order per tile -> loss and every gradient bitwise equal to the all-persistent step, and the
+    global switch is left at the backward's mode for the collectives."""
     from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI
 
     cfg = RealNVPConfig(dim=784, n_layers=2, hidden=1024, anneal="none")
@@ -187,7 +189,7 @@ def test_engine_persistent_forward_only_bitwise(gpu):
     prev = torch.ops.vinf.gemm_persist(1)
     try:
         for fwd_only in (False, True):
-            torch.ops.vinf.gemm_persist(0 if fwd_only else 1)
+            torch.ops.vinf.gemm_persist(bwd_mode if fwd_only else 1)
             eng = RealNVPVI(cfg, batch=B, device=gpu, seed=4, lr=1e-3)
             eng.persist_forward_only = fwd_only
             eng.eps_override = eps
@@ -196,11 +198,93 @@ def test_engine_persistent_forward_only_bitwise(gpu):
             torch.cuda.synchronize()
             out.append((eng.loss.clone(), eng.params.grad.clone(), eng.params.master.clone()))
             if fwd_only:
-                assert torch.ops.vinf.gemm_persist(-1) == 0
+                assert torch.ops.vinf.gemm_persist(-1) == bwd_mode
     finally:
         torch.ops.vinf.gemm_persist(prev)
     (l0, g0, p0), (l1, g1, p1) = out
     assert torch.equal(l0, l1) and torch.equal(g0, g1) and torch.equal(p0, p1)
+
+
+def _claimed_vs_fixed(gpu, fn, reserve=0):
+    """Outputs of fn() under persist mode 1 (fixed tile lists) and mode 2 (claimed tiles), the
+    latter run 4 times in a row (each launch's last block re-zeroes its counter slot)."""
+    prev = torch.ops.vinf.gemm_persist(1)
+    prev_r = torch.ops.vinf.gemm_grid_reserve(0)
+    try:
+        ref = fn()
+        torch.ops.vinf.gemm_grid_reserve(reserve)
+        torch.ops.vinf.gemm_persist(2)
+        assert torch.ops.vinf.gemm_persist(-1) == 2
+        runs = [fn() for _ in range(4)]
+    finally:
+        torch.ops.vinf.gemm_persist(prev)
+        torch.ops.vinf.gemm_grid_reserve(prev_r)
+    torch.cuda.synchronize()
+    return ref, runs
+
+
+@pytest.mark.parametrize("M,reserve", [(70000, 0), (65536, 0), (66000, 40), (700, 0)])
+def test_persistent_claimed_tiles_bitwise(gpu, M, reserve):
+    """Persist mode 2 (blocks claim tiles from per-XCD counters, ids published through LDS):
+    every tile keeps its K order, so the bias + ReLU + bitmask forward, the bitmask input
+    gradient and the fp32-accumulate NN product are bitwise those of the fixed tile lists - for
+    uneven tile counts, a reserved (smaller) grid and a grid smaller than the chip."""
+    from vi_normflows_amd.ops import gemm
+
+    torch.manual_seed(M)
+    K, N = 1024, 1024
+    x, W, b = _bf(M, K, device=gpu), _bf(N, K, device=gpu, scale=0.05), _bf(N, device=gpu)
+    act = _bf(M, N, device=gpu)
+    bits = _pack_bits(act > 0)
+    Wd = _bf(N, N, device=gpu, scale=0.05)
+    Wdt = Wd.t().contiguous()
+    base = torch.randn(M, 416, device=gpu)
+    Wn = _bf(K, 416, device=gpu, scale=0.05)
+
+    def run():
+        y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        m = torch.empty(M, N // 8, device=gpu, dtype=torch.uint8)
+        torch.ops.vinf.gemm_nt(x, W, b, y, 1, m)
+        d = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        gemm.linear_dgrad(x, Wd, d, relu_of=act, relu_bits=bits, Wt=Wdt)
+        f = base.clone()
+        torch.ops.vinf.gemm_nn(x, Wn, None, f, True)
+        return y, m, d, f
+
+    ref, runs = _claimed_vs_fixed(gpu, run, reserve)
+    _check(ref[0], (x.float() @ W.float().t() + b.float()).clamp_min(0), 1e-2)
+    for r in runs:
+        for u, v in zip(r, ref):
+            assert torch.equal(u, v)
+
+
+def test_persistent_claimed_tiles_graph_replay(gpu):
+    """Mode 2 inside a captured graph: the counter slot baked into each launch is re-zeroed by
+    the launch's last block, so every replay claims every tile again."""
+    torch.manual_seed(12)
+    M, N, K = 70000, 1024, 416
+    x, W, b = _bf(M, K, device=gpu), _bf(N, K, device=gpu, scale=0.05), _bf(N, device=gpu)
+    y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    prev = torch.ops.vinf.gemm_persist(1)
+    try:
+        ref = torch.empty_like(y)
+        torch.ops.vinf.gemm_nt(x, W, b, ref, 1, None)
+        torch.ops.vinf.gemm_persist(2)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            torch.ops.vinf.gemm_nt(x, W, b, y, 1, None)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            torch.ops.vinf.gemm_nt(x, W, b, y, 1, None)
+        for _ in range(3):
+            y.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(y, ref)
+    finally:
+        torch.ops.vinf.gemm_persist(prev)
 
 
 def test_wgrad_xcd_packing_bitwise(gpu):

@@ -51,7 +51,7 @@ def main() -> None:
     dev = torch.device("cuda:0")
     eng = RealNVPVI(RealNVPConfig(n_layers=a.layers, anneal="none", banana_pairing="split"),
                     batch=a.batch, device=dev, seed=1, lr=1e-3, lr_warmup=100.0)
-    # the DP runner's default policy ("fwd"): persistent grid in the forward only
+    # the DP runner's earlier policy ("fwd"): persistent grid in the forward only
     nat.gemm_persist(0)
     eng.persist_forward_only = True
     ranges = eng.layout.unit_ranges

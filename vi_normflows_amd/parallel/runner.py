@@ -48,13 +48,15 @@ def _init_single_rank_group(info: DistInfo) -> None:
 _POLICY = {"refs": 0, "saved": None}
 
 
-def _policy_acquire() -> None:
+def _policy_acquire(mode: int = 0) -> None:
+    """mode: the library's persistent-grid setting outside the forward (0 one block per tile,
+    2 persistent with run-time tile claims)."""
     from ..ops._ext import native
 
     if _POLICY["refs"] == 0:
         _POLICY["saved"] = int(native().gemm_persist(-1))
     _POLICY["refs"] += 1
-    native().gemm_persist(0)
+    native().gemm_persist(mode)
 
 
 def _policy_release() -> None:
@@ -71,21 +73,24 @@ class DataParallelRunner:
     exists: a 1-rank RCCL communicator then runs the exact collective / stream-ordering /
     graph-capture path of the multi-GPU job on one GPU.
 
-    ``persist``: the multi-rank GEMM grid policy - ``"fwd"`` (default): persistent grids (one
-    block per CU) in the forward only, one block per tile in the backward, where RCCL kernels
-    take CUs; ``"all"``: persistent everywhere (measured 38.64 vs 39.05 ms on the 1-rank RCCL
-    path, but a collective holding CUs stalls whole tile lists on a real node);
-    ``"none"``: one block per tile everywhere. (A grid that left 16 / 8 CUs to RCCL measured
-    41.0-41.3 ms: profiles/r3/dp_backward_policy_ab.jsonl.)
+    ``persist``: the multi-rank GEMM grid policy. ``"dyn"`` (default): persistent grids (one
+    block per CU) with fixed tile lists in the forward, and in the backward, where RCCL kernels
+    take CUs, persistent grids whose blocks claim tiles at run time (library persist mode 2), so
+    a block held back by an RCCL kernel takes fewer tiles instead of delaying a fixed list. On
+    the 1-rank RCCL path: 34.41-34.51 ms against 34.96-35.04 for ``"fwd"``
+    (profiles/r5/dyn_claims_ab.jsonl). ``"fwd"``: as ``"dyn"`` but one block per tile in the
+    backward; ``"all"``: fixed-list persistent grids everywhere (a collective holding CUs stalls
+    whole tile lists on a real node); ``"none"``: one block per tile everywhere. (A grid that
+    left 16 / 8 CUs to RCCL measured 41.0-41.3 ms: profiles/r3/dp_backward_policy_ab.jsonl.)
     ``graph_collectives``: capture the step WITH its collectives into the hipGraph at world > 1
     (default off: eager replay costs ~0.1 ms of a ~37 ms step,
     profiles/r2_graph_vs_eager_rccl_ab.jsonl); a 1-rank communicator is captured by default."""
 
     def __init__(self, engine, info: DistInfo, bucket_cap_mb: float = 32.0,
-                 compress_bf16: bool = False, force_reduce: bool = False, persist: str = "fwd",
+                 compress_bf16: bool = False, force_reduce: bool = False, persist: str = "dyn",
                  graph_collectives: bool | None = None):
-        if persist not in ("fwd", "all", "none"):
-            raise ValueError(f"persist must be fwd | all | none, got {persist!r}")
+        if persist not in ("fwd", "dyn", "all", "none"):
+            raise ValueError(f"persist must be fwd | dyn | all | none, got {persist!r}")
         self.graph_collectives = graph_collectives
         self.engine = engine
         self.info = info
@@ -102,9 +107,9 @@ class DataParallelRunner:
             # all-reduce holds, so the backward's products launch one block per tile. The
             # forward has no collective in flight: engines that support it run the full
             # persistent grid there (``persist_forward_only``).
-            _policy_acquire()
+            _policy_acquire(2 if persist == "dyn" else 0)
             self._policy_held = True
-            if persist == "fwd" and hasattr(engine, "persist_forward_only"):
+            if persist in ("fwd", "dyn") and hasattr(engine, "persist_forward_only"):
                 engine.persist_forward_only = True
         if info.world > 1 or (force and dist.is_initialized()):
             P = engine.params
