@@ -121,10 +121,11 @@ struct GemmArgs {
   // ldj share is -sum s; C (s_hat) may be null
   int cf_inverse;
   // persistent launches with dynamic tile claims (gemm256.hip, persist mode 2): this launch's
-  // counter slot, 8 per-XCD claim counters + 1 finished-block counter, zero at launch start and
-  // zeroed again by the launch's last block
+  // counter slot, 8 per-XCD claim counters + 1 finished-block counter (one 128-B line each,
+  // QCTR_LINE ints apart), zero at launch start and zeroed again by the launch's last block
   int* qctr;
 };
+constexpr int QCTR_LINE = 32, QCTR_SLOT = 9 * QCTR_LINE;
 
 // The alignment the LDS-staged epilogue's 16-B row accesses need (host side); shapes that miss
 // it take the fragment-layout stores.

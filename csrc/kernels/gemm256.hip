@@ -703,7 +703,7 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
 // tile's first stream K-tile), which nothing touches between the epilogue-ending barrier and
 // the next tile's phase-2 DMA into that slot; every wave reads it at the loop top, before its
 // first barrier of the tile (read + readfirstlane: complete before any wave can issue that DMA).
-// Only the block's first claim is exposed. Every block increments a.qctr[8] once, as it
+// Only the block's first claim is exposed. Every block increments the done counter once, as it
 // finishes; the last one zeroes the slot for the next launch that uses it. No block ever waits
 // on another (no spin), so the grid always drains.
 template <bool A_KMAJOR, bool B_KMAJOR, int EPI, bool DYN = false>
@@ -728,7 +728,7 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
   auto claim_add = [&](int x) {
     int z;
     asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-    return atomicAdd(a.qctr + x + z, 1);
+    return atomicAdd(a.qctr + x * QCTR_LINE + z, 1);
   };
   const int xcd = b & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
   auto xcount = [&](int x) { return x < r8 ? q8 + 1 : q8; };
@@ -739,7 +739,7 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
   auto finished = [&](int old) {   // old: this block's pre-increment value of the done counter
     if (old == G - 1)
 #pragma unroll
-      for (int x = 0; x < 9; ++x) atomicExch(a.qctr + x, 0);
+      for (int x = 0; x < 9; ++x) atomicExch(a.qctr + x * QCTR_LINE, 0);
   };
   const int nkt = (a.K + BK - 1) / BK;              // K-tiles per tile
   // Column rotation: with every block holding the same number of tiles and each XCD's step-s
@@ -1094,8 +1094,9 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
 // 0 one block per tile
 static int g_persist = 1;
 
-// mode 2's claim counters: QSLOTS slots of 16 ints (8 per-XCD counters + the finished-block
-// count), one slot per launch in rotation. Allocated and zeroed by the first
+// mode 2's claim counters: QSLOTS slots of QCTR_SLOT ints (8 per-XCD counters + the
+// finished-block count, each on its own 128-B line so the 32 blocks of one XCD do not queue
+// behind the other XCDs' claims on one line), one slot per launch in rotation. Allocated and zeroed by the first
 // nf_gemm256_set_persist(2) (outside any graph capture); each launch's last block re-zeroes its
 // slot. Launches of one stream never overlap, and 256 slots keep even concurrent streams apart.
 constexpr int QSLOTS = 256;
@@ -1161,7 +1162,7 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
     if constexpr (EPI != EPI_CPL_FWD) {
       int dev = -1;
       if (g_persist == 2 && g_qctr && hipGetDevice(&dev) == hipSuccess && dev == g_qctr_dev) {
-        a.qctr = g_qctr + 16 * (g_qslot++ % QSLOTS);
+        a.qctr = g_qctr + QCTR_SLOT * (g_qslot++ % QSLOTS);
         hipLaunchKernelGGL((gemm256_persistent_kernel<AK, BK_, EPI, true>), dim3(G), dim3(NTHR),
                            0, stream, a);
         NF_HIP_CHECK(hipGetLastError());
@@ -1212,8 +1213,8 @@ void nf_gemm256_set_persist(int mode) {
   int dev = -1;
   if (g_persist == 2 && !g_qctr && hipGetDevice(&dev) == hipSuccess) {
     void* p = nullptr;
-    if (hipMalloc(&p, QSLOTS * 16 * sizeof(int)) == hipSuccess &&
-        hipMemset(p, 0, QSLOTS * 16 * sizeof(int)) == hipSuccess &&
+    if (hipMalloc(&p, QSLOTS * QCTR_SLOT * sizeof(int)) == hipSuccess &&
+        hipMemset(p, 0, QSLOTS * QCTR_SLOT * sizeof(int)) == hipSuccess &&
         hipDeviceSynchronize() == hipSuccess) {
       g_qctr = (int*)p;
       g_qctr_dev = dev;
