@@ -239,3 +239,22 @@ def test_trainer_dp_mixed_dtypes_averages_gradients(tmp_path):
             TrainConfig(iters=3, lr=0.05, optimizer="sgd")).fit(3)
     for a, b in zip(r[0]["params"], list(model.parameters()) + [scale]):
         assert torch.allclose(a, b.detach().to(a.dtype), atol=1e-6, rtol=1e-5)
+
+
+def test_runner_persist_policy_names():
+    """The multi-rank GEMM grid policies DataParallelRunner accepts ("dyn" is the default:
+    claimed-tile persistent grids in the backward); anything else is rejected up front. On the
+    CPU no policy touches the GEMM library."""
+    import inspect
+
+    from vi_normflows_amd.parallel.dist import DistInfo
+    from vi_normflows_amd.parallel.runner import DataParallelRunner
+
+    assert inspect.signature(DataParallelRunner).parameters["persist"].default == "dyn"
+    eng = RealNVPVI(RealNVPConfig(dim=8, n_layers=2, hidden=16), batch=4, device="cpu", seed=0)
+    info = DistInfo(device=torch.device("cpu"))
+    for p in ("fwd", "dyn", "all", "none"):
+        with DataParallelRunner(eng, info, persist=p) as run:
+            assert run.reducer is None and not run._policy_held
+    with pytest.raises(ValueError):
+        DataParallelRunner(eng, info, persist="static")
