@@ -1094,15 +1094,39 @@ __global__ void __launch_bounds__(NTHR, 1) gemm256_multi_kernel(TnMulti t) {
 // 0 one block per tile
 static int g_persist = 1;
 
-// mode 2's claim counters: QSLOTS slots of QCTR_SLOT ints (8 per-XCD counters + the
-// finished-block count, each on its own 128-B line so the 32 blocks of one XCD do not queue
-// behind the other XCDs' claims on one line), one slot per launch in rotation. Allocated and zeroed by the first
-// nf_gemm256_set_persist(2) (outside any graph capture); each launch's last block re-zeroes its
-// slot. Launches of one stream never overlap, and 256 slots keep even concurrent streams apart.
-constexpr int QSLOTS = 256;
+// mode 2's claim counters: slots of QCTR_SLOT ints (8 per-XCD counters + the finished-block
+// count, each on its own 128-B line so the 32 blocks of one XCD do not queue behind the other
+// XCDs' claims on one line). Allocated and zeroed by the first nf_gemm256_set_persist(2)
+// (outside any graph capture); each launch's last block re-zeroes its slot. Two pools:
+//  - eager launches rotate over the QSLOTS_EAGER first slots (launches of one stream never
+//    overlap; concurrent streams would need QSLOTS_EAGER launches in flight to meet);
+//  - a launch recorded into a hipGraph keeps its slot for every replay, so it takes a slot of
+//    its own from the capture pool, which no eager launch and no other captured launch ever
+//    gets. A graph exec never runs concurrently with itself, so its replays may share. When the
+//    capture pool is used up (QSLOTS_CAPT captured claim launches in one process) further
+//    captures fall back to the fixed-list persistent kernel, with a one-time notice.
+constexpr int QSLOTS_EAGER = 256, QSLOTS_CAPT = 7936, QSLOTS = QSLOTS_EAGER + QSLOTS_CAPT;
 static int* g_qctr = nullptr;
 static int g_qctr_dev = -1;
 static unsigned g_qslot = 0;
+static int g_qslot_capt = 0;
+
+// counter slot for one claimed-tile launch on `stream`, or null (use the fixed lists)
+inline int* claim_slot(hipStream_t stream) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) != hipSuccess) return nullptr;
+  if (cs == hipStreamCaptureStatusNone) return g_qctr + QCTR_SLOT * (g_qslot++ % QSLOTS_EAGER);
+  if (g_qslot_capt >= QSLOTS_CAPT) {
+    static bool told = false;
+    if (!told) {
+      fprintf(stderr, "vinf: claim-counter capture pool used up, captured launches use fixed "
+                      "tile lists from now on\n");
+      told = true;
+    }
+    return nullptr;
+  }
+  return g_qctr + QCTR_SLOT * (QSLOTS_EAGER + g_qslot_capt++);
+}
 
 // CUs the persistent grid leaves free (nf_gemm256_set_reserve): a multi-rank backward runs
 // RCCL kernels beside the GEMMs, and a persistent block queued behind one would hold back its
@@ -1162,9 +1186,13 @@ void launch(GemmArgs a, int splits, hipStream_t stream) {
     if constexpr (EPI != EPI_CPL_FWD) {
       int dev = -1;
       if (g_persist == 2 && g_qctr && hipGetDevice(&dev) == hipSuccess && dev == g_qctr_dev) {
-        a.qctr = g_qctr + QCTR_SLOT * (g_qslot++ % QSLOTS);
-        hipLaunchKernelGGL((gemm256_persistent_kernel<AK, BK_, EPI, true>), dim3(G), dim3(NTHR),
-                           0, stream, a);
+        a.qctr = claim_slot(stream);
+        if (a.qctr)
+          hipLaunchKernelGGL((gemm256_persistent_kernel<AK, BK_, EPI, true>), dim3(G),
+                             dim3(NTHR), 0, stream, a);
+        else   // capture pool used up: fixed tile lists
+          hipLaunchKernelGGL((gemm256_persistent_kernel<AK, BK_, EPI>), dim3(G), dim3(NTHR), 0,
+                             stream, a);
         NF_HIP_CHECK(hipGetLastError());
         return;
       }

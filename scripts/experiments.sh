@@ -7,12 +7,61 @@ name=$1; shift
 O=gpurun_out/exp_$name; mkdir -p $O
 
 case $name in
+  lib_ab)         # this tree's library vs a variant build (csrc/build.py --variant V -D ...):
+                  # args V [pytest files]: GPU tests of the default library, the 4096^2 x 65536
+                  # weight-gradient probe and the real 13-layer launch on both, then three
+                  # interleaved whole steps
+    v=$1; shift; P=vi_normflows_amd/_native/libvinf_hip_$v.so
+    if [ $# -gt 0 ]; then
+      timeout -k 10 400 python -u -m pytest "$@" -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 || { echo PYTEST_FAIL; tail -30 $O/pytest.txt; exit 1; }
+      tail -1 $O/pytest.txt
+    fi
+    for r in 1 2; do
+      for lib in default $v; do
+        if [ $lib = default ]; then L=""; else L=$P; fi
+        VINF_NATIVE_LIB=$L timeout -k 10 200 python -m vi_normflows_amd.bench.wgrad_bench --tag $lib --probe --cases tn4w_real,tn4w_cached --iters 5 >> $O/probe.jsonl || exit 1
+        VINF_NATIVE_LIB=$L timeout -k 10 200 python -m vi_normflows_amd.bench.wgrad_bench --tag $lib --layout-probe --layers 13 --iters 3 --layouts 3 >> $O/wg.jsonl || exit 1
+      done
+    done
+    cat $O/probe.jsonl $O/wg.jsonl
+    for r in 1 2 3; do
+      for lib in default $v; do
+        if [ $lib = default ]; then L=""; else L=$P; fi
+        VINF_NATIVE_LIB=$L timeout -k 10 240 python bench.py --steps 20 --warmup 5 > $O/b.json 2> $O/b.err || { echo BENCH_FAIL; tail -20 $O/b.err; exit 1; }
+        python -c "import json;d=json.load(open('$O/b.json'));print(json.dumps({'lib':'$lib','ms':d['ms_per_step'],'F':d['notes']['final_free_energy']}))" | tee -a $O/bench.jsonl
+      done
+    done ;;
   mem_issue)      # per-CU / per-XCD global load & store issue rates (tools/mem_issue_bench.hip)
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/mem_issue_bench.hip -o $O/mem_issue_bench &&
     timeout -k 10 120 $O/mem_issue_bench full > $O/mem.jsonl ;;
   dma)            # LDS-DMA operand stream: segment size x footprint x DMA depth per wave
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/mem_issue_bench.hip -o $O/mem_issue_bench &&
     timeout -k 10 120 $O/mem_issue_bench dma > $O/dma.jsonl ;;
+  probe_libs)     # the 4096^2 x 65536 weight-gradient probe on this tree's library and on
+                  # variant builds (args: variant names; timing-only probe builds allowed)
+    for r in 1 2; do
+      for lib in default "$@"; do
+        if [ $lib = default ]; then L=""; else L=vi_normflows_amd/_native/libvinf_hip_$lib.so; fi
+        VINF_NATIVE_LIB=$L timeout -k 10 200 python -m vi_normflows_amd.bench.wgrad_bench --tag $lib --probe --cases tn4w_real,tn4w_cached --iters 5 >> $O/probe.jsonl || exit 1
+      done
+    done
+    cat $O/probe.jsonl ;;
+  probe_pmc)      # counter passes of the 4-wave weight-gradient probe (tn4w_real) on this
+                  # tree's library and variant builds (args: variant names); pass 1: issue /
+                  # FIFO stalls at the SQ, pass 2: TA / TD / TCP stalls
+    export TMPDIR=/tmp
+    P1="GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_VMEM SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL"
+    P2="GRBM_GUI_ACTIVE SQ_WAVE_CYCLES TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_UTCL1_SERIALIZATION_STALL_sum"
+    P3="GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_SCA"
+    for lib in default "$@"; do
+      if [ $lib = default ]; then L=""; else L=vi_normflows_amd/_native/libvinf_hip_$lib.so; fi
+      for pp in 1 2 3; do
+        eval "C=\$P$pp"
+        VINF_NATIVE_LIB=$L timeout -s KILL 120 rocprofv3 --pmc $C -d $O/${lib}_p$pp -o pmc --output-format csv -- python3 -m vi_normflows_amd.bench.wgrad_bench --probe --cases tn4w_real --iters 3 > $O/${lib}_p$pp.log 2>&1 || { echo P${pp}_FAIL $lib; tail -20 $O/${lib}_p$pp.log; exit 1; }
+      done
+      python3 -m vi_normflows_amd.bench.pmc_summary $O/${lib}_p1 $O/${lib}_p2 $O/${lib}_p3 > $O/${lib}_summary.txt 2>&1
+      echo "== $lib"; grep -A3 tn4w $O/${lib}_summary.txt
+    done ;;
   wgrad_probe)    # TN weight-gradient loop: real vs cache-resident operands vs the NT kernel
     timeout -k 10 300 python -m vi_normflows_amd.bench.wgrad_bench --tag ${1:-cur} --probe --iters 5 > $O/probe.jsonl &&
     true ;;

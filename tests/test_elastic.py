@@ -20,24 +20,33 @@ def _port():
     return p
 
 
-def _run(out, fault_env=None):
+_JOBS = {
+    "realnvp": ["--config", "config2_realnvp8", "device=cpu", "dim=8", "hidden=16", "K=2",
+                "batch=16"],
+    # the config-5 MAF engine (CPU: fp32 products) under the DP runner
+    "maf": ["--config", "config5_maf64", "device=cpu", "dim=16", "hidden=32", "K=3",
+            "batch=32"],
+}
+
+
+def _run(out, fault_env=None, job="realnvp"):
     env = dict(os.environ, OMP_NUM_THREADS="1")
     env.pop("VINF_FAULT", None)
     if fault_env:
         env.update(fault_env)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--max-restarts=1", "--rdzv-backend=c10d", f"--rdzv-endpoint=127.0.0.1:{_port()}",
-           "-m", "vi_normflows_amd.train", "--config", "config2_realnvp8", "device=cpu", "dim=8",
-           "hidden=16", "K=2", "batch=16", "iters=12", "ckpt_every=4", "log_every=4",
-           f"out_dir={out}", "name=job"]
+           "-m", "vi_normflows_amd.train", *_JOBS[job], "iters=12", "ckpt_every=4",
+           "log_every=4", f"out_dir={out}", "name=job"]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     return p, safe_load(out / "job" / "ckpt.pt")
 
 
-def test_rank_loss_restart_resumes_bitwise(tmp_path):
-    _, clean = _run(tmp_path / "clean")
-    p, faulted = _run(tmp_path / "faulted", {"VINF_FAULT": "exit:6:1"})
+@pytest.mark.parametrize("job", ["realnvp", "maf"])
+def test_rank_loss_restart_resumes_bitwise(tmp_path, job):
+    _, clean = _run(tmp_path / "clean", job=job)
+    p, faulted = _run(tmp_path / "faulted", {"VINF_FAULT": "exit:6:1"}, job=job)
     log = p.stdout + p.stderr
     assert "resumed from" in log                       # the restarted attempt loaded step 4
     assert int(clean["engine"]["step"]) == int(faulted["engine"]["step"]) == 12

@@ -278,3 +278,41 @@ def test_gemm_tn4w_matches_tn_multi(gpu, B):
         if outs[3][1][p] is not None:
             _check(outs[3][1][p], dys[p].float().sum(0), 1e-4)
             assert torch.equal(outs[3][1][p], outs[4][1][p]), p
+
+
+def _check_elem(out, ref, rtol, atol):
+    """Per-element bound |out - ref| <= rtol |ref| + atol (ref in fp64): a wrong small-magnitude
+    output cannot hide behind the largest one, unlike the max-normalised _check."""
+    err = (out.double() - ref).abs()
+    bound = rtol * ref.abs() + atol
+    bad = err > bound
+    assert not bad.any(), (int(bad.sum()), err.max().item(), (err - bound).max().item())
+
+
+def test_gemm_tn4w_headline_k65536(gpu):
+    """The bench's weight-gradient shape: K = batch = 65536 through the 4-wave kernel, i.e. 2048
+    32-deep K-tiles through the 4-stage LDS ring with counted vmcnt (the long-K steady state
+    that the B <= 4096 cases above never reach), on the RealNVP conditioner's three problem
+    shapes (392-1024-1024-784, padded 416 / 800) in one launch, against fp64 per element.
+    fp32 accumulation of 65536 exact bf16 products: the reordering error is ~1e-5 of the row
+    scale, a lost or duplicated K-tile would be ~sqrt(32) / sqrt(65536) = 2 % of it.
+    Reference layer math: /root/reference/normflows/normflows/nn_models.py:41-84."""
+    from vi_normflows_amd.ops._ext import native
+
+    torch.manual_seed(11)
+    B = 65536
+    shapes = [(800, 1024), (1024, 1024), (1024, 416)]
+    dys = [_bf(B, M, device=gpu) for M, _ in shapes]
+    xs = [_bf(B, N, device=gpu) for _, N in shapes]
+    total = sum(((M + 255) // 256) * ((N + 255) // 256) for M, N in shapes)
+    dWs = [torch.full((M, N), 3.0, device=gpu) for M, N in shapes]
+    dbs = [torch.full((M,), 3.0, device=gpu) for M, _ in shapes]
+    native().gemm_tn_multi_layout(dys, xs, dWs, dbs, 0, total, 3)
+    torch.cuda.synchronize()
+    for p in range(len(shapes)):
+        ref = dys[p].double().t() @ xs[p].double()
+        scale = ref.pow(2).mean().sqrt().item()          # ~ sqrt(B) for unit-variance operands
+        _check_elem(dWs[p], ref, 1e-4, 2e-4 * scale)
+        rb = dys[p].double().sum(0)
+        _check_elem(dbs[p], rb, 1e-4, 2e-4 * rb.pow(2).mean().sqrt().item())
+        del ref

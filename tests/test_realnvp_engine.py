@@ -297,17 +297,21 @@ def test_gemm_nt_cpl_matches_torch(gpu):
         assert err <= 2e-2 * v.abs().max().item() + 1e-3, err
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("M,K,init", [(700, 1024, True), (65, 512, False), (4096, 256, True)])
-def test_cpl_edge_kernel_matches_fused_edge_tile(gpu, M, K, init):
-    """The last Dh % 128 = 8 features through cpl_edge_fwd_kernel (gemm_cpl_edge(1), default)
-    vs the fused edge column tile (gemm_cpl_edge(0)): the same MFMA k-sequence, so s_hat, y and
-    its bf16 copy are bitwise equal; the pad columns are zeroed; the log-det partial row only
-    differs in summation order (also under ldj accumulate)."""
+def test_cpl_fused_edge_tile_matches_torch(gpu, M, K, init):
+    """The last Dh % 128 = 8 coupling features (Dh = 392 = 3 x 128 + 8) come out of the fused
+    product's fourth, edge column tile. Checked per element against an fp64 torch reference on
+    those 8 features, with and without log-det accumulation. The kernel rounds s_hat and t to
+    bf16 before the coupling (as the stored s_hat the backward reads), so the bounds are one
+    bf16 rounding of each propagated through y = x e^s + t, s = scale tanh(s_hat). The pad
+    columns of the bf16 copy must be zero. (The separate edge kernel this test used to compare
+    against was removed in round 5.) Reference transform:
+    /root/reference/normflows/normflows/flows.py:8-34."""
     from vi_normflows_amd.ops import gemm
-    from vi_normflows_amd.ops._ext import native
 
     torch.manual_seed(11)
-    Dh = 392
+    Dh, scale, e0 = 392, 0.5, 384
     h = torch.randn(M, K, device=gpu).to(torch.bfloat16)
     W = torch.zeros(800, K, device=gpu)
     W[:2 * Dh] = torch.randn(2 * Dh, K, device=gpu) * 0.03
@@ -315,26 +319,28 @@ def test_cpl_edge_kernel_matches_fused_edge_tile(gpu, M, K, init):
     b = (torch.randn(800, device=gpu) * 0.1).to(torch.bfloat16)
     x = torch.randn(M, Dh, device=gpu)
     ldj0 = torch.randn(4, M, device=gpu)
-    outs = []
-    prev = native().gemm_cpl_edge(1)
-    try:
-        for on in (1, 0):
-            native().gemm_cpl_edge(on)
-            st = torch.full((M, 800), 5.0, device=gpu).to(torch.bfloat16)
-            y = torch.full((M, Dh), 7.0, device=gpu)
-            yb = torch.full((M, 416), 3.0, device=gpu).to(torch.bfloat16)
-            ldjp = ldj0.clone()
-            gemm.linear_fwd_coupling(h, W, b, st, x, y, yb, ldjp, init, 0.5)
-            outs.append((st[:, :Dh].clone(), y, yb, ldjp))
-    finally:
-        native().gemm_cpl_edge(prev)
+    st = torch.full((M, 800), 5.0, device=gpu).to(torch.bfloat16)
+    y = torch.full((M, Dh), 7.0, device=gpu)
+    yb = torch.full((M, 416), 3.0, device=gpu).to(torch.bfloat16)
+    ldjp = ldj0.clone()
+    gemm.linear_fwd_coupling(h, W, b, st, x, y, yb, ldjp, init, scale)
     torch.cuda.synchronize()
-    (s1, y1, b1, l1), (s2, y2, b2, l2) = outs
-    assert torch.equal(s1, s2)
-    assert torch.equal(y1, y2)
-    assert torch.equal(b1, b2)
-    assert (b1[:, Dh:] == 0).all()
-    assert torch.allclose(l1, l2, rtol=1e-5, atol=1e-5)
+    o = h.double() @ W.double().t() + b.double()
+    sh, t = o[:, :Dh], o[:, Dh:2 * Dh]
+    s = scale * torch.tanh(sh)
+    yr = x.double() * torch.exp(s) + t
+    u = 2.0 ** -8                                  # bf16 rounding, relative
+    E = slice(e0, Dh)
+    assert (yb[:, Dh:] == 0).all()
+    assert ((st[:, E].double() - sh[:, E]).abs() <= 1.01 * u * sh[:, E].abs() + 1e-5).all()
+    dy_bound = 1.01 * u * ((x.double() * torch.exp(s)).abs() * scale * sh.abs() + t.abs())
+    err = (y[:, E].double() - yr[:, E]).abs()
+    assert (err <= dy_bound[:, E] + 1e-5 * yr[:, E].abs() + 1e-5).all(), err.max().item()
+    errb = (yb[:, E].double() - yr[:, E]).abs()
+    assert (errb <= dy_bound[:, E] + 1.01 * u * yr[:, E].abs() + 1e-5).all()
+    lr = s.sum(1) + (0 if init else ldj0.double().sum(0))
+    lb = 1.01 * u * (scale * sh.abs()).sum(1) + 1e-4 * (1 + lr.abs())
+    assert ((ldjp.double().sum(0) - lr).abs() <= lb).all()
 
 
 @pytest.mark.gpu

@@ -72,6 +72,8 @@ def probe(B: int, iters: int, tag: str, dev, only: str = ""):
         "tn_b_cached": lambda: gemm.WgradPlan([(dy, x0, dW, db)]).run(0, 256),
         "nt_real": lambda: gemm.linear_fwd(dyt, xt, None, out),
         "nn_real": lambda: gemm.linear_dgrad(dyt, x, out),
+        # hipBLASLt's own TN kernel on the same operands (bf16 out): the library reference
+        "blas_tn": lambda: torch.mm(dy.t(), x, out=out),
     }
     flops = 2.0 * B * n * n
     if only:   # e.g. "tn4w_real,tn4w_cached" (counter passes: one kernel family per run)

@@ -31,9 +31,11 @@ def main(argv=None):
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--composite-target", action="store_true",
                     help="evaluate the target with the torch composite instead of the HIP kernel")
-    if len([a for a in argv if not a.startswith("-")]) < 3:
+    def _usage_error(message):   # reference-style usage text, then argparse's own message
         print(__doc__)
-        raise SystemExit(2)
+        ap.exit(2, f"{ap.prog}: error: {message}\n")
+
+    ap.error = _usage_error
     a = ap.parse_args(argv)
     from .distributions.energies import get_target
     from .ops import fused

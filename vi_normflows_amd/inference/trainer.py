@@ -209,13 +209,15 @@ class Trainer:
         iters = iters if iters is not None else self.cfg.iters
         t0 = time.perf_counter()
         end = self.t + iters
+        # the counters are process-wide: log only this fit's calls, not those of earlier models
+        dense0 = precision_counts()
         while self.t < end:
             res, ok = self.step()
             t = self.t - 1
             if t % self.cfg.log_every == 0 or self.t == end:
                 rec = {"step": t, "F": res.item(), "skipped": self.n_skipped,
                        "elapsed_s": time.perf_counter() - t0, **res.stats}
-                dense = precision_counts()
+                dense = {k: v - dense0.get(k, 0) for k, v in precision_counts().items()}
                 if any(dense.values()):   # which dense-layer precision path(s) the model took
                     rec["dense_precision"] = ",".join(k for k, v in dense.items() if v)
                 self.history.append(rec)

@@ -708,3 +708,29 @@ class MAFEngine:
         self.rng_offset.copy_(sd["rng_offset"])
         if self.fp8:
             self._wq_fresh = False
+
+    def rank_state_dict(self) -> dict:
+        """State that differs between data-parallel ranks and is not in :meth:`state_dict`:
+        the delayed e4m3 scales. Each rank quantises its own activations and gradients, so its
+        amax history, the scales of the next step, the saturation counters and the bootstrap
+        flags are rank-local (tests/test_distributed_engines.py). Without them a resumed fp8
+        run re-bootstraps every scale (its first backward runs bf16) and leaves the trajectory
+        of the uninterrupted run. Saved per rank by ``utils.checkpoint.save_engine``."""
+        if not self.fp8:
+            return {}
+        st = self.sx + self.sh + self.sdo + self.sdh
+        return {"amax_pool": self.amax_pool.detach().cpu(),
+                "f8_scale_pool": self.f8_scale_pool.detach().cpu(),
+                "f8_saturated": self.f8_saturated.detach().cpu(),
+                "gscale_ready": bool(self._gscale_ready),
+                "scale_ready": torch.tensor([bool(d.ready) for d in st])}
+
+    def load_rank_state_dict(self, sd: dict) -> None:
+        if not self.fp8 or not sd:
+            return
+        self.amax_pool.copy_(sd["amax_pool"])
+        self.f8_scale_pool.copy_(sd["f8_scale_pool"])
+        self.f8_saturated.copy_(sd["f8_saturated"])
+        self._gscale_ready = bool(sd["gscale_ready"])
+        for d, r in zip(self.sx + self.sh + self.sdo + self.sdh, sd["scale_ready"].tolist()):
+            d.ready = bool(r)

@@ -127,6 +127,24 @@ class PlanarVAEEngine:
     def set_batch(self, x: torch.Tensor) -> None:
         self.x.copy_(x)
 
+    # ------------------------------------------------------------------ checkpoint
+    def state_dict(self) -> dict:
+        """Parameters + Adam moments, step and the RNG counter (utils.checkpoint.save_engine);
+        beta is a function of the step. The batch is the caller's (set_batch), so a resumed run
+        replays the same batches by iterating its data from the restored step."""
+        return {"params": self.params.state_dict(), "step": self.step_t.detach().cpu(),
+                "rng_offset": self.rng_offset.detach().cpu(),
+                "cfg": {k: v for k, v in self.cfg.__dict__.items()
+                        if isinstance(v, (int, float, str, bool))}}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.params.load_state_dict(sd["params"])
+        self.step_t.copy_(sd["step"])
+        self.rng_offset.copy_(sd["rng_offset"])
+        if self.anneal == "reference":
+            cool = min(self.anneal_iters / 4.0, 1e4)
+            torch.clamp((self.step_t - 1.0) * (1.0 / cool) + 0.001, max=1.0, out=self.beta)
+
     # ------------------------------------------------------------------ step
     def _update_schedule(self):
         self.step_t.add_(1.0)

@@ -156,7 +156,11 @@ class Energy2DLogp(torch.autograd.Function):
         return lp
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, go):
+        # the saved gradient is a constant to autograd: a second derivative through it would
+        # silently be zero, so double backward raises instead (use the torch composite,
+        # Target(fused=False), for Hessians)
         (g,) = ctx.saved_tensors
         return g * go.unsqueeze(1), None
 

@@ -311,25 +311,40 @@ def run_maf(cfg, out, info, logger):
     if cfg.extra.get("impl", "engine") == "engine":
         from .models.maf_engine import MAFEngine, MAFEngineConfig
         from .parallel.runner import DataParallelRunner
-        from .utils.checkpoint import save_engine
+        from .utils.checkpoint import load_engine, save_engine
 
         mc = MAFEngineConfig(dim=cfg.dim, n_layers=cfg.K, hidden=cfg.hidden,
                              precision=cfg.extra.get("precision", "fp8"))
         eng = MAFEngine(mc, batch=cfg.batch, device=dev, seed=cfg.seed, rank=info.rank, lr=cfg.lr,
                         optimizer=cfg.optimizer)
+        ckpt = out / "ckpt.pt"
+        # elastic-lite as in run_realnvp; every rank also restores its own delayed e4m3 scales
+        # (MAFEngine.rank_state_dict) from its per-rank file
+        if cfg.extra.get("resume"):
+            load_engine(eng, cfg.extra["resume"], info.rank)
+        elif cfg.extra.get("auto_resume", True) and ckpt.exists():
+            load_engine(eng, ckpt, info.rank)
+            if info.is_main:
+                print(f"[train] resumed from {ckpt} at step {int(eng.step_t.item())}", flush=True)
         run = _runner(eng, info)
-        if dev.type == "cuda" and cfg.extra.get("graph", True):
+        fault = bool(os.environ.get("VINF_FAULT"))
+        if dev.type == "cuda" and cfg.extra.get("graph", True) and not fault:
             run.capture(warmup=1)
         t0 = time.perf_counter()
-        for t in range(cfg.iters):
+        start = int(eng.step_t.item())
+        for t in range(start, cfg.iters):
+            maybe_inject(t, info.rank)
             run.step()
-            if t % cfg.log_every == 0 or t == cfg.iters - 1:
+            if t == start or t % cfg.log_every == 0 or t == cfg.iters - 1:
                 el = time.perf_counter() - t0
                 logger.log({"step": t, "nll": float(eng.loss.item()),
                             "grad_norm": math.sqrt(max(float(eng.gnorm2.item()), 0.0)),
-                            "samples_per_s": (t + 1) * cfg.batch * info.world / el,
+                            "samples_per_s": (t - start + 1) * cfg.batch * info.world / el,
                             **eng.fp8_saturation()})
-        save_engine(eng, out / "ckpt.pt", info.rank)
+            if cfg.ckpt_every and (t + 1) % cfg.ckpt_every == 0:
+                save_engine(eng, ckpt, info.rank)
+                vdist.barrier()
+        save_engine(eng, ckpt, info.rank)
         vdist.barrier()
         return {"nll": float(eng.loss.item()), "nll_floor_entropy": mc.entropy(),
                 "precision": mc.precision if dev.type == "cuda" else "fp32"}

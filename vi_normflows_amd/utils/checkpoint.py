@@ -3,8 +3,9 @@
 Native checkpoints are plain ``torch.save`` dicts of tensors/ints written atomically
 (tmp file + rename) and read back with ``torch.load(weights_only=True)``: parameters,
 optimizer moments, step, per-rank RNG state and the config. In data-parallel runs rank 0
-writes the shared state and every rank writes its own RNG stream
-(``<path>.rank<r>.rng``) so a resumed job continues with identical noise streams.
+writes the shared state and every rank writes its own file (``<path>.rank<r>.rng``): the
+RNG stream, plus the engine's rank-local state (``engine.rank_state_dict()``, e.g. the MAF
+engine's delayed e4m3 scales), so a resumed job continues bitwise where it stopped.
 The reference's flat ``.npy`` format is handled by :mod:`vi_normflows_amd.utils.npy_io`.
 """
 from __future__ import annotations
@@ -37,8 +38,10 @@ def save_engine(engine, path, rank: int = 0, extra: dict | None = None) -> None:
         if extra:
             payload["extra"] = extra
         atomic_save(payload, path)
+    local = engine.rank_state_dict() if hasattr(engine, "rank_state_dict") else {}
     atomic_save({"rng_offset": sd["rng_offset"], "rank": rank, "step": sd.get("step"),
-                 "torch_rng": torch.get_rng_state()}, f"{path}.rank{rank}.rng")
+                 "torch_rng": torch.get_rng_state(), "rank_state": local},
+                f"{path}.rank{rank}.rng")
 
 
 def load_engine(engine, path, rank: int = 0) -> dict:
@@ -55,6 +58,8 @@ def load_engine(engine, path, rank: int = 0) -> dict:
                                                               torch.as_tensor(st).cpu()):
             engine.rng_offset.copy_(r["rng_offset"])
             torch.set_rng_state(r["torch_rng"])
+            if r.get("rank_state") and hasattr(engine, "load_rank_state_dict"):
+                engine.load_rank_state_dict(r["rank_state"])
     return payload.get("extra", {})
 
 
