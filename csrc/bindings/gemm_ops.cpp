@@ -1046,6 +1046,9 @@ void gemm_fp8_nt(const at::Tensor& xq, const at::Tensor& sx, const at::Tensor& w
 
 int64_t gemm_set_mode(int64_t mode) { return nf_gemm_set_mode((int)mode); }   // < 0: query
 int64_t gemm_pair(int64_t mode) { return nf_gemm256_set_pair((int)mode); }   // < 0: query
+int nf_gemm_cpl4w(int on);
+// RealNVP coupling-forward product on the 4-fat-wave kernel (1) or the 8-wave one (0)
+int64_t gemm_cpl4w(int64_t on) { return nf_gemm_cpl4w((int)on); }   // < 0: query
 int nf_gemm256_xcd_pack(int on);
 int64_t gemm_wgrad_xcd_pack(int64_t on) { return nf_gemm256_xcd_pack((int)on); }
 int64_t gemm_persist(int64_t on) {   // on < 0: query only; returns the previous setting
@@ -1067,6 +1070,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
 #endif
   m.def("gemm_set_mode(int mode) -> int", &gemm_set_mode);
   m.def("gemm_pair(int mode) -> int", &gemm_pair);
+  m.def("gemm_cpl4w(int on) -> int", &gemm_cpl4w);
   m.def("gemm_persist(int on) -> int", &gemm_persist);
   m.def("gemm_grid_reserve(int cus) -> int", &gemm_grid_reserve);
   m.def("gemm_wgrad_xcd_pack(int on) -> int", &gemm_wgrad_xcd_pack);

@@ -79,9 +79,13 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
 // v_exp_f32 + one v_rcp_f32 (libm tanhf is a ~25-instruction branchy sequence, and the fused
 // coupling epilogues evaluate it for every element of a 256-row tile while no MFMA runs).
 // Absolute error ~1e-7 (the s_hat it reads is bf16); e^{2|x|} = inf gives exactly +-1.
+// The reciprocal is v_rcp_f32 itself (1 ulp): HIP's __fdividef is an IEEE division here, a
+// ~10-instruction v_div_scale / v_div_fmas / v_div_fixup sequence plus its hazard nops, and it
+// made up most of the VALU work of every coupling / MAF epilogue (12.7k v_div_scale_f32 in
+// gemm256.hip alone before this).
 __device__ __forceinline__ float fast_tanhf(float x) {
   const float e = __expf(2.f * fabsf(x));
-  return copysignf(1.f - __fdividef(2.f, 1.f + e), x);
+  return copysignf(1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e), x);
 }
 
 // Numerically stable softplus and log(1+x) helpers used by flow kernels.

@@ -30,6 +30,7 @@
 #include "gemm_tile.h"
 #include "wgrad_pack.h"
 #include "tn_multi.h"
+#include "cpl4w.h"
 
 // Diagnostic build only (csrc/build.py --variant stamps -D NF_G256_STAMPS): every block records
 // s_memrealtime (100 MHz, chip-global) at body entry, after the prologue wait, after the main
@@ -1133,6 +1134,15 @@ inline int* claim_slot(hipStream_t stream) {
 // whole tile list; grid = min(tiles, CUs - reserve) keeps every block startable
 static int g_reserve = 0;
 
+// the RealNVP coupling-forward product on gemm_cpl4w.hip (nf_gemm_cpl4w): opt-in, measured
+// slower at the headline shape (docs/PERF_NOTES.md round 6: its one-wave-per-SIMD epilogue
+// runs at half the VALU issue rate of this kernel's two waves per SIMD); NF_CPL4W_ON build: on
+#ifdef NF_CPL4W_ON
+static int g_cpl4w = 1;
+#else
+static int g_cpl4w = 0;
+#endif
+
 // weight-gradient tile -> block packing by XCD (nf_gemm256_xcd_pack, on by default)
 static int g_xcd_pack = 1;
 
@@ -1363,7 +1373,24 @@ void nf_launch_gemm256_nt_cpl(const void* h, long ldh, const void* W, long ldw, 
                     "2 Dh weight rows\n");
     abort();
   }
+  if (g256::g_cpl4w) {   // the 4-fat-wave 136-feature tiles (gemm_cpl4w.hip): no edge tile
+    cpl4w::Args c{};
+    c.A = (const nf::bf16_t*)h; c.lda = ldh;
+    c.W = (const nf::bf16_t*)W; c.ldw = ldw; c.w_rows = w_rows;
+    c.bias = (const nf::bf16_t*)bias;
+    c.st = (nf::bf16_t*)st; c.ld_st = ld_st;
+    c.x = x; c.ld_x = ld_x; c.y = y; c.ld_y = ld_y;
+    c.yb = (nf::bf16_t*)yb; c.ld_yb = ld_yb; c.yb_width = yb_width;
+    c.ldjp = ldjp; c.ld_ldjp = ld_ldjp; c.ldj_rows = ntn; c.ldj_init = ldj_init;
+    c.M = M; c.K = K; c.Dh = Dh; c.scale = scale; c.inverse = inverse;
+    if (launch_cpl4w(c, stream)) return;
+  }
   g256::launch<true, true, EPI_CPL_FWD>(a, 1, stream);
+}
+int nf_gemm_cpl4w(int on) {   // on < 0: query; returns the previous setting
+  const int prev = g256::g_cpl4w;
+  if (on >= 0) g256::g_cpl4w = on ? 1 : 0;
+  return prev;
 }
 
 // Second MADE product of MAF layer l with the layer's transform fused (EPI_CPL_FWD, cf_mode 1):

@@ -26,9 +26,10 @@ namespace nf {
 namespace gemm {
 namespace tn4w {
 
+// BK: the launch granule (launch_tn4w_multi needs K % (2 BK) == 0, i.e. a whole number of
+// 4-K-tile loop iterations); the body itself runs 32-deep K-tiles in 4 stages of 32 KiB
+// (tile_body4: BK4, HALF4)
 constexpr int BM = 256, BN = 256, BK = 64, NTHR = 256;
-constexpr int HALF = 128 * 64 * 2;     // 16 KiB half-image
-constexpr int STAGE = 4 * HALF;        // 64 KiB per K-tile
 
 // stage half-image `h` of the K-tile at k0 (wave-uniform h == wave): 16 pieces of 4 k-rows.
 // Address = uniform row base (SGPRs: k-row k0 + 4 piece) + a per-lane 32-bit byte offset that
@@ -45,10 +46,16 @@ __device__ __forceinline__ void stage(const bf16_t* __restrict__ base, long ld, 
     int gm = col0 + lc * 8;
     gm = gm < cols_total ? gm : cols_total - 8;
     voff[v] = (unsigned)(((lane >> 4) * ld + gm) * 2);
+#ifdef NF_PROBE_DMA_SAMEADDR   // timing probe: every lane of a piece reads the same 16 B
+    voff[v] = 0;
+#endif
   }
   const char* b = (const char*)base + (long)k0 * ld * 2;
 #pragma unroll
   for (int piece = 0; piece < NPIECE; ++piece) {
+#ifdef NF_PROBE_DMA_HALF       // timing probe: half the pieces
+    if (piece & 1) continue;
+#endif
     const char* row = b + (long)(piece * 4) * ld * 2;
     const unsigned lds = (unsigned)(unsigned long)(LDS_AS char*)(dst + piece * 1024);
     // saddr + voffset form in asm: the builtin hoisted 16 64-bit per-lane addresses out of the
@@ -247,186 +254,6 @@ __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, ch
   }
 }
 
-// One LDS-DMA piece (4 k-rows x 256 B of a half-image) of the K-tile at k0: the per-lane
-// offsets voff[2] are loop-invariant (stage_offsets), the row base is scalar.
-__device__ __forceinline__ void stage_offsets(long ld, int col0, int cols_total, int lane,
-                                              unsigned (&voff)[2]) {
-#pragma unroll
-  for (int v = 0; v < 2; ++v) {
-    const int kr = v * 8 + (lane >> 4);
-    const int lc = (lane & 15) ^ mn_swz(kr);
-    int gm = col0 + lc * 8;
-    gm = gm < cols_total ? gm : cols_total - 8;
-    voff[v] = (unsigned)(((lane >> 4) * ld + gm) * 2);
-  }
-}
-__device__ __forceinline__ void stage_piece(const bf16_t* __restrict__ base, long ld, int k0,
-                                            int piece, char* dst, const unsigned (&voff)[2]) {
-  const char* row = (const char*)base + (long)(k0 + piece * 4) * ld * 2;
-  const unsigned lds = (unsigned)(unsigned long)(LDS_AS char*)(dst + piece * 1024);
-  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1"
-               :: "v"(voff[(piece >> 1) & 1]), "s"(row), "s"(lds) : "memory", "m0");
-}
-
-// The same product as tile_body4 with the K-tile's memory work spread over its 64 MFMAs.
-// tile_body4 issued, right after the first 8 MFMAs of a K-tile, all 8 LDS-DMA pieces and the 16
-// B-fragment reads of the next K-tile in one burst: one wave per SIMD issues in order, every
-// wave of the block reaches that burst at the same time (they leave the same barrier), and the
-// CU's address path then serialises 32 pieces while no MFMA issues (MFMA busy 0.56,
-// profiles/r5/tn4w_probe_pmc.txt). Here A and B fragments are both double-buffered (the reads of
-// K-tile t + 1 go to the other register set, so they can sit anywhere in K-tile t), and every
-// 8-MFMA group j of K-tile t carries one DMA piece (piece j of K-tile t + 3), B fragment j and
-// A fragment j of K-tile t + 1: 5 memory instructions per 8 MFMAs, each in its own MFMA gap
-// (sched_barrier fences keep the compiler from re-bunching them). Same k order and the same
-// accumulation chains as tile_body4, so the results are bitwise equal.
-template <bool DODB>
-__device__ __forceinline__ void tile_body_sp(const GemmArgs& a, int m0, int n0, char* q0, char* q1,
-                                             char* q2, char* q3) {
-  constexpr int BK4 = 32, HALF4 = 128 * BK4 * 2;   // 8 KiB half-image
-  constexpr int PD = 3;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int nkt = a.K / BK4;   // a multiple of 4 (launch_tn4w_multi: K % 128 == 0)
-  const bf16_t* sbase = wave < 2 ? a.A : a.B;
-  const long sld = wave < 2 ? a.lda : a.ldb;
-  const int scol0 = wave < 2 ? m0 + wave * 128 : n0 + (wave - 2) * 128;
-  const int stot = wave < 2 ? a.M : a.N;
-  unsigned voff[2];
-  stage_offsets(sld, scol0, stot, lane, voff);
-  auto stp = [&](auto q_c) -> char* {
-    constexpr int Q = decltype(q_c)::value;
-    return Q == 0 ? q0 : Q == 1 ? q1 : Q == 2 ? q2 : q3;
-  };
-  v4f acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
-  float dbs[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) dbs[j] = 0.f;
-  v8s fa0[8], fa1[8], fb0[8], fb1[8];
-  auto rd_a = [&](auto q_c, int j) { return read_frag<false>(stp(q_c) + wr * HALF4, j * 16, 0, lane); };
-  auto rd_b = [&](auto q_c, int i) {
-    return read_frag<false>(stp(q_c) + (2 + wc) * HALF4, i * 16, 0, lane);
-  };
-  using Q0 = std::integral_constant<int, 0>;
-  // prologue: K-tiles 0..2 in flight, K-tile 0's fragments in set 0
-#pragma unroll
-  for (int p = 0; p < 8; ++p) stage_piece(sbase, sld, 0, p, q0 + wave * HALF4, voff);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) stage_piece(sbase, sld, BK4, p, q1 + wave * HALF4, voff);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) stage_piece(sbase, sld, 2 * BK4, p, q2 + wave * HALF4, voff);
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-#pragma unroll
-  for (int j = 0; j < 8; ++j) fa0[j] = rd_a(Q0{}, j);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) fb0[i] = rd_b(Q0{}, i);
-  // K-tile t in stage Q, fragments in (fac, fbc); the next K-tile's go to (fan, fbn). Every
-  // K-tile runs the same code: past the end the DMA re-loads the last K-tile into the stage
-  // nobody reads any more (so vmcnt(8) always means "K-tile t + 1 has landed") and the reads
-  // fill the unused register set. With a separate tail the register allocator had renamed the
-  // accumulators at the loop exit, copying AGPRs the last asm MFMAs had not written yet.
-  const int klast = (nkt - 1) * BK4;
-  auto ktile = [&](int t, auto q_c, const v8s (&fac)[8], const v8s (&fbc)[8], v8s (&fan)[8],
-                   v8s (&fbn)[8]) {
-    constexpr int Q = decltype(q_c)::value;
-    using QN = std::integral_constant<int, (Q + 1) & 3>;
-    using QI = std::integral_constant<int, (Q + PD) & 3>;
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(8)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    char* qi = stp(QI{}) + wave * HALF4;
-    int knext = (t + PD) * BK4;
-    knext = knext < klast ? knext : klast;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        mfma_acc(acc[i][j], fbc[i], fac[j]);
-        __builtin_amdgcn_sched_barrier(0);
-        if (i == 0) {
-          stage_piece(sbase, sld, knext, j, qi, voff);
-        } else if (i == 1) {
-          fbn[j] = rd_b(QN{}, j);
-        } else if (i == 3) {
-          fan[j] = rd_a(QN{}, j);
-        } else if (DODB && i >= 4) {
-          typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
-          const v2bf one = {(__bf16)1.0f, (__bf16)1.0f};
-          const int e = i - 4;
-          const unsigned w = (unsigned)(unsigned short)fac[j][2 * e] |
-                             ((unsigned)(unsigned short)fac[j][2 * e + 1] << 16);
-          dbs[j] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf, w), one, dbs[j], false);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  };
-  using Q1 = std::integral_constant<int, 1>;
-  using Q2 = std::integral_constant<int, 2>;
-  using Q3 = std::integral_constant<int, 3>;
-  for (int t = 0; t < nkt; t += 4) {
-    ktile(t, Q0{}, fa0, fb0, fa1, fb1);
-    ktile(t + 1, Q1{}, fa1, fb1, fa0, fb0);
-    ktile(t + 2, Q2{}, fa0, fb0, fa1, fb1);
-    ktile(t + 3, Q3{}, fa1, fb1, fa0, fb0);
-    // the MFMAs are asm the compiler cannot see, and at the loop exit it copies accumulators
-    // (v_accvgpr_read for the epilogue): an MFMA's result needs its wait states before any
-    // reader but the next MFMA of its chain, so the last iteration pads before leaving
-    if (t + 4 >= nkt) {
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  // the re-loads past the end write the stages the epilogue stages through
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-
-  const int g = lane >> 4, c = lane & 15;
-  if (DODB && wc == 0) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = dbs[j];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      const int m = m0 + wr * 128 + j * 16 + c;
-      if (g == 0 && m < a.M) a.dbias[m] = v;
-    }
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  __syncthreads();
-  char* region = (wave == 0 ? q0 : wave == 1 ? q1 : wave == 2 ? q2 : q3);   // 32 KiB per wave
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    v4f sub[4][8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sub[i][j] = acc[4 * h + i][j];
-    if (a.staged)
-      epi_tile_staged<EPI_F32, 8>(a, sub, m0 + wr * 128, n0 + wc * 128 + h * 64, 0,
-                                  region + h * 16384, lane);
-    else
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int m = m0 + wr * 128 + j * 16 + c;
-        if (m >= a.M) continue;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int n = n0 + wc * 128 + h * 64 + i * 16 + g * 4;
-          if (n < a.N) epi_store<EPI_F32>(a, sub[i][j], m, n, 0);
-        }
-      }
-  }
-}
-
 template <int PD>
 __global__ void __launch_bounds__(NTHR, 1) gemm_tn4w4_kernel(g256::TnMulti t) {
   __shared__ __attribute__((aligned(16))) char q0[32768];
@@ -450,13 +277,8 @@ __global__ void __launch_bounds__(NTHR, 1) gemm_tn4w4_kernel(g256::TnMulti t) {
   const int local = d.tiles ? (int)d.tiles[id - d.start] : id - d.start;
   const int ntn = (a.N + BN - 1) / BN;
   const int tm = local / ntn, tn = local % ntn;
-#ifndef NF_TN4W_SPREAD
   if (a.dbias != nullptr && tn == 0) tile_body4<true, PD>(a, tm * BM, tn * BN, q0, q1, q2, q3);
   else tile_body4<false, PD>(a, tm * BM, tn * BN, q0, q1, q2, q3);
-#else
-  if (a.dbias != nullptr && tn == 0) tile_body_sp<true>(a, tm * BM, tn * BN, q0, q1, q2, q3);
-  else tile_body_sp<false>(a, tm * BM, tn * BN, q0, q1, q2, q3);
-#endif
 }
 
 }  // namespace tn4w

@@ -190,7 +190,7 @@ PY
                 "--config 5 --precision bf16 --batch 32768" "--config 5 --precision fp8 --batch 32768"; do
       timeout -k 10 240 python -m vi_normflows_amd.bench.configs $args >> $O/configs.jsonl 2>> $O/configs.err || { echo "FAIL $args"; tail -20 $O/configs.err; exit 1; }
     done ;;
-  lib_ab)         # default library vs a variant build (arg: variant name): GEMM tests on the
+  lib_ab_cfg5)    # default library vs a variant build (arg: variant name): GEMM tests on the
                   # default, then per-product, headline and config-5 timings, alternating
     v=$1; L=vi_normflows_amd/_native/libvinf_hip_$v.so
     timeout -k 10 600 python -u -m pytest tests/test_gemm_gpu.py tests/test_gemm_persistent_gpu.py tests/test_realnvp_engine.py tests/test_maf_engine.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
@@ -208,5 +208,90 @@ PY
       done
     done
     unset VINF_NATIVE_LIB ;;
+  step_libs)      # whole headline step, this tree's library vs variant builds, interleaved
+                  # (args: [rounds] variants...)
+    n=$1; shift
+    for r in $(seq $n); do
+      for lib in default "$@"; do
+        if [ $lib = default ]; then L=""; else L=vi_normflows_amd/_native/libvinf_hip_$lib.so; fi
+        VINF_NATIVE_LIB=$L timeout -k 10 240 python bench.py --steps 20 --warmup 5 > $O/b.json 2> $O/b.err || { echo BENCH_FAIL; tail -20 $O/b.err; exit 1; }
+        python -c "import json;d=json.load(open('$O/b.json'));print(json.dumps({'lib':'$lib','ms':d['ms_per_step'],'F':d['notes']['final_free_energy']}))" | tee -a $O/bench.jsonl
+      done
+    done ;;
+  cfg5_libs)      # config 5 (MAF-64, B = 32768) fp8 and bf16, this tree's library vs variants
+                  # (args: [rounds] variants...)
+    n=$1; shift
+    for r in $(seq $n); do
+      for lib in default "$@"; do
+        if [ $lib = default ]; then L=""; else L=vi_normflows_amd/_native/libvinf_hip_$lib.so; fi
+        for pr in fp8 bf16; do
+          VINF_NATIVE_LIB=$L timeout -k 10 240 python -m vi_normflows_amd.bench.configs --config 5 --precision $pr --batch 32768 > $O/c.json 2>> $O/c.err || { tail -20 $O/c.err; exit 1; }
+          python -c "import json;d=json.load(open('$O/c.json'));print(json.dumps({'lib':'$lib','prec':'$pr','ms':d['ms_per_step'],'sps':d['samples_per_s']}))" | tee -a $O/cfg5.jsonl
+        done
+      done
+    done ;;
+  sg_ab)          # per-product step-GEMM timings, default library vs variant builds
+                  # (args: "<products>" variants...; e.g. "fwd_l2,cpl_fwd,dgrad_l2" spread2)
+    ONLY=$1; shift
+    for r in 1 2; do
+      for v in default "$@"; do
+        if [ $v = default ]; then L=""; else L=vi_normflows_amd/_native/libvinf_hip_$v.so; fi
+        VINF_NATIVE_LIB=$L timeout -k 10 180 python -m vi_normflows_amd.bench.step_gemms --tag $v --iters 20 --only $ONLY >> $O/sg.jsonl 2> $O/sg_$v.err || { tail -20 $O/sg_$v.err; exit 1; }
+      done
+    done
+    grep -v '"sum"' $O/sg.jsonl ;;
+  quick)          # selected GPU tests, per-product timings, headline bench
+                  # (args: "<pytest paths>" ["<step_gemms --only list>"])
+    TESTS=$1; ONLY=${2:-fwd_l1,fwd_l2,fwd_l2_nomask,cpl_fwd,dgrad_l3,dgrad_l2,cpl_bwd}
+    if [ -n "$TESTS" ]; then
+      timeout -k 10 600 python -u -m pytest $TESTS -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 || { echo PYTEST_FAIL; tail -40 $O/pytest.txt; exit 1; }
+      tail -2 $O/pytest.txt
+    fi
+    timeout -k 10 180 python -m vi_normflows_amd.bench.step_gemms --iters 20 --only $ONLY > $O/sg.jsonl 2> $O/sg.err || { echo SG_FAIL; tail -20 $O/sg.err; exit 1; }
+    cat $O/sg.jsonl
+    timeout -k 10 240 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
+    python -c "import json;d=json.load(open('$O/bench.json'));print('BENCH', d['ms_per_step'], d['value'], d['notes']['final_free_energy'])" ;;
+  cfg_trace)      # kernel trace of one north-star config (graph off): args CONFIG BATCH [configs.py args]
+    export TMPDIR=/tmp
+    c=$1; b=$2; shift 2
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/t_$c -o run --output-format csv -- \
+      python3 -m vi_normflows_amd.bench.configs --config $c --batch $b --graph off --steps 5 --warmup 3 "$@" > $O/r_$c.json 2> $O/r_$c.err || { tail -20 $O/r_$c.err; exit 1; }
+    python3 -m vi_normflows_amd.bench.prof_summary $O/t_$c > $O/summary_$c.txt 2>&1; head -20 $O/summary_$c.txt; cat $O/r_$c.json ;;
+  configs_final)  # every north-star config once, engine and module paths (one process each)
+    for args in "--config 0 --batch 128" "--config 0 --batch 1024" "--config 0 --impl module --batch 1024" \
+                "--config 2 --batch 32768" "--config 3 --batch 16384" \
+                "--config 4 --batch 8192" "--config 4 --impl module --batch 8192" \
+                "--config 5 --precision bf16 --batch 32768" "--config 5 --precision fp8 --batch 32768"; do
+      timeout -k 10 300 python -m vi_normflows_amd.bench.configs $args >> $O/configs.jsonl 2>> $O/configs.err || { echo "FAIL $args"; tail -20 $O/configs.err; exit 1; }
+      tail -1 $O/configs.jsonl | cut -c1-300
+    done ;;
+  f8_ab)          # config-5 fp8 vs bf16, interleaved (args: [batch] [rounds]) after the fp8 tests
+    b=${1:-32768}; n=${2:-2}
+    timeout -k 10 400 python -u -m pytest tests/test_fp8_wgrad_gpu.py tests/test_maf_engine.py -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 || { tail -40 $O/pytest.txt; exit 1; }
+    tail -1 $O/pytest.txt
+    for r in $(seq $n); do
+      for pr in fp8 bf16; do
+        timeout -k 10 240 python -m vi_normflows_amd.bench.configs --config 5 --precision $pr --batch $b >> $O/cfg5.jsonl 2>> $O/cfg5.err || { tail -20 $O/cfg5.err; exit 1; }
+      done
+    done
+    python -c "
+import json
+for l in open('$O/cfg5.jsonl'):
+    d=json.loads(l); print(d.get('precision'), d.get('ms_per_step'), d.get('samples_per_s'))" ;;
+  rccl_trace)     # kernel traces of the headline step, plain graph path vs the 1-rank RCCL path
+                  # (bench.py --force-reduce [args]) on one box
+    export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/plain -o step --output-format csv -- python3 bench.py --steps 10 --warmup 3 > $O/plain.log 2>&1 || { echo PLAIN_FAIL; tail -20 $O/plain.log; exit 1; }
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rccl -o step --output-format csv -- python3 bench.py --steps 10 --warmup 3 --force-reduce "$@" > $O/rccl.log 2>&1 || { echo RCCL_FAIL; tail -20 $O/rccl.log; exit 1; }
+    for t in plain rccl; do
+      python3 -m vi_normflows_amd.bench.prof_summary $O/$t > $O/${t}_summary.txt 2>&1
+      python3 -m vi_normflows_amd.bench.gap_summary $O/$t > $O/${t}_gaps.txt 2>&1 || true
+    done
+    head -14 $O/plain_summary.txt; head -24 $O/rccl_summary.txt ;;
+  getdata_trace)  # kernel trace of the 2-D potential CLI on the GPU (fused target kernel)
+    export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 -m vi_normflows_amd.get_data 8 100 0.02 p1 --device cuda --samples 1048576 --quiet > $O/out.txt 2>&1 || { echo PROF_FAIL; tail -20 $O/out.txt; exit 1; }
+    tail -3 $O/out.txt
+    python3 -m vi_normflows_amd.bench.prof_summary $O/prof > $O/summary.txt 2>&1 && head -25 $O/summary.txt ;;
   *) echo "unknown experiment $name"; exit 2 ;;
 esac

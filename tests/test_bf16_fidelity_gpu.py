@@ -5,7 +5,7 @@ gradients, both coupling fusions in the GEMM epilogues, NT input gradients again
 copy) is compared with a plain fp32 autograd re-implementation of the same model
 (``test_realnvp_engine.autograd_free_energy``) on the same GPU, with the same parameters and the
 same base noise (``eps_override``), for RealNVP-8 and RealNVP-32 at D = 784, H = 1024,
-B = 1024. The parameters are first trained for 150 steps by the bf16 engine itself (split
+B = 1024, and RealNVP-32 at B = 16384. The parameters are first trained for 150 steps by the bf16 engine itself (split
 twisted-Gaussian target, lr 1e-3), so the coupling layers are far from the identity.
 
 Tolerances (bf16 unit roundoff u = 2^-8 = 3.9e-3, round-to-nearest error <= u/2):
@@ -38,13 +38,16 @@ def _rel(a, b):
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("layers,tol_layer", [(8, 4e-2), (32, 6e-2)])
-def test_bf16_engine_matches_fp32_oracle_at_headline_shape(gpu, layers, tol_layer):
+@pytest.mark.parametrize("layers,tol_layer,B", [(8, 4e-2, 1024), (32, 6e-2, 1024),
+                                                 (32, 6e-2, 16384)])
+def test_bf16_engine_matches_fp32_oracle_at_headline_shape(gpu, layers, tol_layer, B):
+    """B = 16384: a quarter of the bench's per-GPU batch, so every product runs the long-K
+    weight-gradient loop (512 K-tiles per tile) and the persistent forward / input-gradient
+    grids hold several tiles per CU, as at the headline shape, under the same bounds."""
     from vi_normflows_amd.models.realnvp import RealNVPConfig, RealNVPVI
 
     cfg = RealNVPConfig(dim=784, n_layers=layers, hidden=1024, anneal="none",
                         banana_pairing="split")
-    B = 1024
     eng = RealNVPVI(cfg, batch=B, device=gpu, seed=11, lr=1e-3, lr_warmup=20)
     assert eng.cdt == torch.bfloat16 and eng.wgrad_defer and eng.cpl_fuse and eng.cf_fuse
     for _ in range(150):

@@ -15,10 +15,24 @@ def _bf(*shape, device, scale=1.0):
     return (torch.randn(*shape, device=device) * scale).to(torch.bfloat16)
 
 
-def _check(out, ref, tol):
-    err = (out.float() - ref).abs().max().item()
-    mag = ref.abs().max().item() + 1e-6
-    assert err <= tol * mag, (err, mag)
+U_BF16 = 2.0 ** -8     # bf16 unit roundoff (rounding to nearest: |err| <= U_BF16 / 2 relative)
+
+
+def _mag(a, b_t):
+    """sum_k |a_ik| |b_kj|: the scale of every fp32 rounding inside one dot product."""
+    return a.float().abs() @ b_t.float().abs()
+
+
+def _check(out, ref, mag, rtol=U_BF16, acc=2.0 ** -14):
+    """Per element: |out - ref| <= rtol |ref| + acc * mag, ref in fp64. rtol covers the
+    output's own rounding (one bf16 ulp by default: twice the round-to-nearest bound); acc * mag
+    covers fp32 accumulation in any order over K <= 1024 products (K eps_f32 = 2^-14 at
+    K = 1024, the worst case). Unlike a max-normalised check, a wrong small-magnitude output
+    fails here."""
+    err = (out.double() - ref.double()).abs()
+    bound = rtol * ref.double().abs() + acc * mag.double()
+    bad = err > bound
+    assert not bad.any(), (int(bad.sum()), err.max().item(), float((err - bound).max()))
 
 
 def _pack_bits(pos: torch.Tensor) -> torch.Tensor:
@@ -35,7 +49,8 @@ def test_persistent_nt_bias_relu_mask(gpu, M, N, K):
     y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
     mask = torch.full((M, N // 8), 0xAA, device=gpu, dtype=torch.uint8)
     torch.ops.vinf.gemm_nt(x, W, b, y, 1, mask)
-    _check(y, (x.float() @ W.float().t() + b.float()).clamp_min(0), 1e-2)
+    ref = (x.double() @ W.double().t() + b.double()).clamp_min(0)
+    _check(y, ref, _mag(x, W.t()) + b.float().abs())
     assert torch.equal(mask, _pack_bits(y > 0))
 
 
@@ -49,7 +64,7 @@ def test_persistent_dgrad_bits_nt(gpu, M, N, K):
     bits = _pack_bits(act > 0)
     out = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
     gemm.linear_dgrad(dy, W, out, relu_of=act, relu_bits=bits, Wt=W.t().contiguous())
-    _check(out, (dy.float() @ W.float()) * (act.float() > 0), 1e-2)
+    _check(out, (dy.double() @ W.double()) * (act > 0), _mag(dy, W))
 
 
 def test_persistent_f32_accumulate(gpu):
@@ -59,7 +74,9 @@ def test_persistent_f32_accumulate(gpu):
     base = torch.randn(M, N, device=gpu)
     out = base.clone()
     torch.ops.vinf.gemm_nn(dy, W, None, out, True)
-    _check(out, dy.float() @ W.float() + base, 2e-2)
+    # fp32 output: its own rounding is 2^-24 relative; the accumulation term dominates
+    _check(out, dy.double() @ W.double() + base.double(), _mag(dy, W) + base.abs(),
+           rtol=2.0 ** -23)
 
 
 # M = 65536: 256 row tiles, every block holds the same tile count -> the column rotation is on
@@ -77,20 +94,29 @@ def test_persistent_fused_coupling_fwd_bwd(gpu, M):
     W = W.to(torch.bfloat16)
     b = (torch.randn(800, device=gpu) * 0.1).to(torch.bfloat16)
     x = torch.randn(M, Dh, device=gpu)
-    outs = []
-    for backend in ("mfma", "oracle"):
-        with (gemm.oracle() if backend == "oracle" else contextlib.nullcontext()):
-            st = torch.zeros(M, 800, device=gpu, dtype=torch.bfloat16)
-            y = torch.empty(M, Dh, device=gpu)
-            yb = torch.full((M, 416), 3.0, device=gpu).to(torch.bfloat16)
-            ldjp = torch.full((4, M), 9.0, device=gpu)
-            gemm.linear_fwd_coupling(h, W, b, st, x, y, yb, ldjp, True, 1.0)
-            outs.append((st[:, :Dh].float(), y, yb.float(), ldjp.sum(0)))
-    (s1, y1, b1, l1), (s2, y2, b2, l2) = outs
-    assert (b1[:, Dh:] == 0).all()
-    for u, v in ((s1, s2), (y1, y2), (b1, b2), (l1, l2)):
-        err = (u - v).abs().max().item()
-        assert err <= 2e-2 * v.abs().max().item() + 1e-3, err
+    st = torch.zeros(M, 800, device=gpu, dtype=torch.bfloat16)
+    y = torch.empty(M, Dh, device=gpu)
+    yb = torch.full((M, 416), 3.0, device=gpu).to(torch.bfloat16)
+    ldjp = torch.full((4, M), 9.0, device=gpu)
+    gemm.linear_fwd_coupling(h, W, b, st, x, y, yb, ldjp, True, 1.0)
+    # fp64 reference per element. The kernel rounds s_hat and t to bf16 before the coupling
+    # (the stored s_hat is what the backward reads), so y carries one bf16 rounding of each,
+    # propagated through y = x e^s + t, s = tanh(s_hat) (scale 1)
+    o = h.double() @ W.double().t() + b.double()
+    mo = _mag(h, W.t()) + b.float().abs()
+    sh, t, msh, mt = o[:, :Dh], o[:, Dh:2 * Dh], mo[:, :Dh], mo[:, Dh:2 * Dh]
+    s = torch.tanh(sh)
+    yr = x.double() * torch.exp(s) + t
+    assert (yb[:, Dh:] == 0).all()
+    _check(st[:, :Dh], sh, msh)
+    dsh = U_BF16 * sh.abs() + 2.0 ** -14 * msh.double()
+    dt = U_BF16 * t.abs() + 2.0 ** -14 * mt.double()
+    dyb = (x.double() * torch.exp(s)).abs() * dsh + dt
+    err = (y.double() - yr).abs()
+    assert (err <= dyb + 2.0 ** -20 * yr.abs()).all(), float((err - dyb).max())
+    assert ((yb[:, :Dh].double() - yr).abs() <= dyb + U_BF16 * yr.abs()).all()
+    lr = s.sum(1)
+    assert ((ldjp.sum(0).double() - lr).abs() <= dsh.sum(1) + 1e-5 * (1 + lr.abs())).all()
 
     N = 416
     dy = _bf(M, K, device=gpu)
@@ -98,18 +124,25 @@ def test_persistent_fused_coupling_fwd_bwd(gpu, M):
     G = torch.randn(M, N, device=gpu)
     G[:, Dh:] = 0
     s_hat = _bf(M, 800, device=gpu)
-    res = []
-    for backend in ("mfma", "oracle"):
-        with (gemm.oracle() if backend == "oracle" else contextlib.nullcontext()):
-            o = [torch.full((M, 800), 5.0, device=gpu).to(torch.bfloat16),
-                 torch.full((M, Dh), 5.0, device=gpu)]
-            gemm.linear_dgrad_coupling(dy, Wd, G, s_hat[:, :Dh], x, o[0], o[1], 1.0, -1e-3,
-                                       Wt=Wd.t().contiguous() if backend == "mfma" else None)
-            res.append(o)
-    assert (res[0][0][:, 2 * Dh:] == 0).all()
-    for o, r in zip(res[0], res[1]):
-        err = (o.float() - r.float()).abs().max().item()
-        assert err <= 2e-2 * r.float().abs().max().item(), err
+    dst = torch.full((M, 800), 5.0, device=gpu).to(torch.bfloat16)
+    gx = torch.full((M, Dh), 5.0, device=gpu)
+    c = -1e-3
+    gemm.linear_dgrad_coupling(dy, Wd, G, s_hat[:, :Dh], x, dst, gx, 1.0, c,
+                               Wt=Wd.t().contiguous())
+    assert (dst[:, 2 * Dh:] == 0).all()
+    # fp64 reference: gy = G + dy Wd (fp32 in the kernel: accumulation term only), then the
+    # coupling backward on the exact bf16 s_hat; dS and gy are stored in bf16, gx in fp32
+    gy = G.double() + dy.double() @ Wd.double()
+    dgy = 2.0 ** -14 * (_mag(dy, Wd) + G.abs()).double()[:, :Dh]
+    gy = gy[:, :Dh]
+    sv = torch.tanh(s_hat[:, :Dh].double())
+    es = torch.exp(sv)
+    fac = 1.0 - sv * sv
+    dS = (gy * x.double() * es + c) * fac
+    ddS = (x.double() * es * fac).abs() * dgy + 2.0 ** -20 * dS.abs()
+    assert ((dst[:, :Dh].double() - dS).abs() <= U_BF16 * dS.abs() + ddS).all()
+    assert ((dst[:, Dh:2 * Dh].double() - gy).abs() <= U_BF16 * gy.abs() + dgy).all()
+    assert ((gx.double() - gy * es).abs() <= es * dgy + 2.0 ** -20 * (gy * es).abs()).all()
 
 
 def test_persistent_repeatable(gpu):
@@ -252,7 +285,8 @@ def test_persistent_claimed_tiles_bitwise(gpu, M, reserve):
         return y, m, d, f
 
     ref, runs = _claimed_vs_fixed(gpu, run, reserve)
-    _check(ref[0], (x.float() @ W.float().t() + b.float()).clamp_min(0), 1e-2)
+    _check(ref[0], (x.double() @ W.double().t() + b.double()).clamp_min(0),
+           _mag(x, W.t()) + b.float().abs())
     for r in runs:
         for u, v in zip(r, ref):
             assert torch.equal(u, v)

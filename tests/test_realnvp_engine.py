@@ -484,3 +484,68 @@ def test_affine_coupling_inverse_kernel_gpu(gpu):
     assert torch.allclose(xb.double(), xb2, atol=1e-5) and torch.allclose(l.double(), l2, atol=1e-4)
     assert torch.allclose(st.grad.double(), st2.grad, rtol=1e-4, atol=1e-4)
     assert torch.allclose(yb.grad.double(), yb2.grad, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,K,init,inverse", [(65536, 1024, True, False), (4096, 256, False, False),
+                                              (4096, 1024, True, True), (1040, 128, False, False)])
+def test_cpl4w_matches_8wave_coupling_product(gpu, M, K, init, inverse):
+    """The 4-fat-wave coupling-forward product (gemm_cpl4w.hip: 136-feature tiles, no edge tile)
+    against the 8-wave EPI_CPL_FWD product (gemm_cpl4w(0)): the same k order per output and the
+    same epilogue arithmetic, so s_hat, y and its bf16 copy are bitwise equal; the log-det
+    partials come in 3 instead of 4 column tiles, so only their row sums are compared (fp32
+    reordering). M = 1040: a partial last row tile."""
+    from vi_normflows_amd.ops import gemm
+    from vi_normflows_amd.ops._ext import native
+
+    torch.manual_seed(M + K)
+    Dh = 392
+    h = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = torch.zeros(800, K, device=gpu)
+    W[:2 * Dh] = torch.randn(2 * Dh, K, device=gpu) * (0.5 / K ** 0.5)
+    W = W.to(torch.bfloat16)
+    b = (torch.randn(800, device=gpu) * 0.1).to(torch.bfloat16)
+    x = torch.randn(M, Dh, device=gpu)
+    ldj0 = torch.randn(4, M, device=gpu)
+    outs = []
+    prev = native().gemm_cpl4w(1)
+    try:
+        for on in (0, 1):
+            native().gemm_cpl4w(on)
+            st = torch.full((M, 800), 5.0, device=gpu).to(torch.bfloat16)
+            y = torch.full((M, Dh), 7.0, device=gpu)
+            yb = torch.full((M, 416), 3.0, device=gpu).to(torch.bfloat16)
+            ldjp = ldj0.clone()
+            gemm.linear_fwd_coupling(h, W, b, None if inverse else st, x, y, yb, ldjp, init, 0.5,
+                                     inverse=inverse)
+            outs.append((st[:, :Dh].clone(), y, yb, ldjp.sum(0)))
+    finally:
+        native().gemm_cpl4w(prev)
+    torch.cuda.synchronize()
+    (s0, y0, b0, l0), (s1, y1, b1, l1) = outs
+    assert torch.equal(s0, s1)
+    assert torch.equal(y0, y1)
+    assert torch.equal(b0, b1)
+    assert (b1[:, Dh:] == 0).all()
+    assert torch.allclose(l0, l1, rtol=1e-5, atol=1e-4)
+
+
+def test_cpl4w_lds_layout_conflict_free():
+    """Host model of gemm_cpl4w.hip's LDS image (64-B rows, chunk c of row r at position
+    c ^ (((r >> 2) & 1) << 1)): the DMA (lane l of a 16-row piece writes row l >> 2, position
+    l & 3, from source chunk (l & 3) ^ ((l >> 4) & 1) * 2) lands every chunk where the fragment
+    read looks for it, and every ds_read_b128 lane group (MI355X_MICROARCH.md §LDS: 4 groups of
+    16 lanes) hits 16 distinct 16-B bank slots, i.e. no bank conflict."""
+    pos = lambda r, c: c ^ (((r >> 2) & 1) << 1)
+    for r0 in range(0, 64, 16):            # DMA: source chunk of the slot each lane writes
+        for l in range(64):
+            r, p = r0 + (l >> 2), l & 3
+            csrc = (l & 3) ^ (((l >> 4) & 1) << 1)
+            assert pos(r, csrc) == p
+    groups = [[0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27],
+              [4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31]]
+    groups += [[g + 32 for g in G] for G in groups]
+    for r0 in range(0, 272, 16):
+        for G in groups:
+            slots = {((r0 + (l & 15)) * 64 + pos(r0 + (l & 15), l >> 4) * 16) // 16 % 16 for l in G}
+            assert len(slots) == 16
