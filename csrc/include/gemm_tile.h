@@ -575,7 +575,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
                 const float4 xv = xp[it];
                 xs[0] = xv.x; xs[1] = xv.y; xs[2] = xv.z; xs[3] = xv.w;
               }
-              const float inv = 1.0f / a.cpl_scale;
+              const float inv = __builtin_amdgcn_rcpf(a.cpl_scale);   // v_rcp (1 ulp): an IEEE division per element group here
               float gx[4], dsh[4], d1v[4];
               if (a.cpl_mode) {   // MAF: dst = [dmu | ds_raw], x = u of layer l-1
 #pragma unroll

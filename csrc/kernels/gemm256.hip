@@ -321,7 +321,7 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
           const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
           float y[8];
           if (maf) {   // shv = s_raw, tv = mu
-            const float ib = 1.f / a.cf_scale;
+            const float ib = __builtin_amdgcn_rcpf(a.cf_scale);   // v_rcp, not an IEEE division per row
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const unsigned us = sh[e >> 1], ut = tt[e >> 1];
