@@ -80,7 +80,15 @@ __device__ __forceinline__ void mfma_acc(v4f& acc, const v8s& a, const v8s& b) {
 // barrier per 64 MFMAs. (A 2-stage body of 64-deep K-tiles, 64 KiB in flight, took 2193-2316 us
 // per real multi-layer launch against 1959-2075 for this one: profiles/r4/tn4w4_layout_probe.jsonl;
 // prefetch distance 2 2217-2234 us: profiles/r4/tn4w4_pd_layout.jsonl.)
-template <bool DODB, int PD>
+// DBM: bit j set = this wave sums the bias gradient of its A row block j (rows 16 j of its
+// 128-row half) with v_dot2 on the A fragments it already holds. Every row block of a row tile is
+// owned by exactly one (column tile, wave) pair (gemm_tn4w4_kernel: db_mask), so the dot
+// products are spread over the waves of the first two column tiles instead of all four waves of
+// the first column tile each summing all eight blocks (half of it redundant: the two column
+// waves hold the same A rows). Compile-time masks: a runtime mask test inside the unrolled
+// K-step split the MFMA / ds_read / DMA schedule into basic blocks and cost more than it saved
+// (docs/PERF_NOTES.md round 5, "dbhalf").
+template <int DBM, int PD>
 __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, char* q0, char* q1,
                                            char* q2, char* q3) {
   constexpr int BK4 = 32, HALF4 = 128 * BK4 * 2;   // 8 KiB half-image
@@ -120,7 +128,7 @@ __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, ch
     constexpr int j = decltype(j_c)::value;
 #pragma unroll
     for (int i = 0; i < 8; ++i) mfma_acc(acc[i][j], fb[i], fa[j]);
-    if constexpr (DODB) {
+    if constexpr ((DBM >> j) & 1) {
       typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
       const v2bf one = {(__bf16)1.0f, (__bf16)1.0f};
 #pragma unroll
@@ -213,9 +221,10 @@ __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, ch
   ktile(t + 3, Q3{}, fb1, fb0, F{}, F{}, F{});
 
   const int g = lane >> 4, c = lane & 15;
-  if (DODB && wc == 0) {
+  if constexpr (DBM != 0) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
+      if (!((DBM >> j) & 1)) continue;
       float v = dbs[j];
       v += __shfl_xor(v, 16);
       v += __shfl_xor(v, 32);
@@ -277,8 +286,28 @@ __global__ void __launch_bounds__(NTHR, 1) gemm_tn4w4_kernel(g256::TnMulti t) {
   const int local = d.tiles ? (int)d.tiles[id - d.start] : id - d.start;
   const int ntn = (a.N + BN - 1) / BN;
   const int tm = local / ntn, tn = local % ntn;
-  if (a.dbias != nullptr && tn == 0) tile_body4<true, PD>(a, tm * BM, tn * BN, q0, q1, q2, q3);
-  else tile_body4<false, PD>(a, tm * BM, tn * BN, q0, q1, q2, q3);
+  // bias-gradient ownership: with >= 2 column tiles, column tile 0 sums row blocks 0-3 and
+  // column tile 1 row blocks 4-7, each split between its two column waves (2 blocks per wave);
+  // a single column tile gives each of its column waves 4 blocks
+  const int wc = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & 1;
+  const int m0 = tm * BM, n0 = tn * BN;
+  // (a masked problem launches only its active tiles: there the first column tile alone owns
+  // the row tile's bias gradient, split between its two column waves, as before)
+  const bool spread = d.tiles == nullptr && ntn >= 2;
+  if (a.dbias != nullptr && (spread ? tn < 2 : tn == 0)) {
+    if (!spread) {
+      if (wc == 0) tile_body4<0x0F, PD>(a, m0, n0, q0, q1, q2, q3);
+      else tile_body4<0xF0, PD>(a, m0, n0, q0, q1, q2, q3);
+    } else if (tn == 0) {
+      if (wc == 0) tile_body4<0x03, PD>(a, m0, n0, q0, q1, q2, q3);
+      else tile_body4<0x0C, PD>(a, m0, n0, q0, q1, q2, q3);
+    } else {
+      if (wc == 0) tile_body4<0x30, PD>(a, m0, n0, q0, q1, q2, q3);
+      else tile_body4<0xC0, PD>(a, m0, n0, q0, q1, q2, q3);
+    }
+  } else {
+    tile_body4<0, PD>(a, m0, n0, q0, q1, q2, q3);
+  }
 }
 
 }  // namespace tn4w

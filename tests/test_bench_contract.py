@@ -82,6 +82,19 @@ def test_bench_self_launch_two_ranks_cpu():
     assert recs[0]["notes"]["replicas_identical"] is True
 
 
+def test_bench_self_launch_eight_ranks_cpu():
+    """The driver's largest scaling point (N = 8) rehearsed on gloo: eight ranks, one bucketed
+    all-reduce per step, rank 0's single JSON line with dp8 and bitwise-identical replicas."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", *SMALL],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    _check(recs[0], 8)
+    assert recs[0]["config"]["parallelism"] == "dp8"
+    assert recs[0]["notes"]["replicas_identical"] is True
+
+
 def test_bench_gpus_world_mismatch_is_an_error():
     env = dict(_env(), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *SMALL],
