@@ -124,6 +124,10 @@ __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, ch
   };
   // MFMAs of A fragment j (+ its bias-gradient dot products), then A fragment j of the next
   // K-tile into the freed registers
+  // the next K-tile's B fragments: fragment 0 behind the DMA burst, fragment j behind the MFMAs
+  // of A fragment j (one burst of all 16 reads after the first 8 MFMAs held the MFMA pipe:
+  // real 13-layer launch 2210-2273 vs 2259-2313 us median, profiles/r6/tn4w_bspread_ab.jsonl)
+  v8s* fbn_p = nullptr;
   auto mfma_j = [&](const v8s (&fb)[8], auto qn_c, auto rd_c, auto j_c) {
     constexpr int j = decltype(j_c)::value;
 #pragma unroll
@@ -139,6 +143,8 @@ __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, ch
       }
     }
     if constexpr (decltype(rd_c)::value) fa[j] = rd_a(qn_c, j);
+    if constexpr (decltype(rd_c)::value && j > 0)
+      fbn_p[j] = read_frag<false>(stp(qn_c) + (2 + wc) * HALF4, j * 16, 0, lane);
   };
   // A fragments 1..7 of a K-tile (fragment 0 is issued first, see ktile)
   auto kstep_from1 = [&](const v8s (&fb)[8], auto qn_c, auto rd_c) {
@@ -192,9 +198,9 @@ __device__ __forceinline__ void tile_body4(const GemmArgs& a, int m0, int n0, ch
 #ifndef NF_PROBE_NODMA   // timing probes only (wrong results): no operand DMA in the K loop
     if constexpr (decltype(issue_c)::value) issue(t + PD, QI{});
 #endif
-#ifndef NF_PROBE_NOBREAD   // timing probe: B fragments never re-read
-    if constexpr (decltype(next_c)::value) rd_b(QN{}, fbn);
-#endif
+    if constexpr (decltype(next_c)::value)
+      fbn[0] = read_frag<false>(stp(QN{}) + (2 + wc) * HALF4, 0, 0, lane);
+    fbn_p = fbn;
     __builtin_amdgcn_sched_barrier(0);
     kstep_from1(fbc, QN{}, next_c);
   };
