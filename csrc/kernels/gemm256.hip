@@ -704,7 +704,9 @@ __device__ __forceinline__ void gemm256_body(const GemmArgs& a, int wg, int spli
 // tile's first stream K-tile), which nothing touches between the epilogue-ending barrier and
 // the next tile's phase-2 DMA into that slot; every wave reads it at the loop top, before its
 // first barrier of the tile (read + readfirstlane: complete before any wave can issue that DMA).
-// Only the block's first claim is exposed. Every block increments the done counter once, as it
+// A block's first tile is not claimed: XCD x's first nbx tiles belong to its nbx blocks in block
+// order and the counter hands out the rest, so no claim round trip is ever exposed (a block that
+// starts late delays one tile, not a list). Every block increments the done counter once, as it
 // finishes; the last one zeroes the slot for the next launch that uses it. No block ever waits
 // on another (no spin), so the grid always drains.
 template <bool A_KMAJOR, bool B_KMAJOR, int EPI, bool DYN = false>
@@ -734,9 +736,14 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
   const int xcd = b & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
   auto xcount = [&](int x) { return x < r8 ? q8 + 1 : q8; };
   auto xbase = [&](int x) { return x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8; };
+  // DYN: the XCD's first nbx tiles are the first tiles of its nbx blocks (block b = xcd + 8 i
+  // takes tile i unclaimed); the counter hands out the rest
+  const int nbx = (G >> 3) + (xcd < (G & 7) ? 1 : 0);
   // tile id for the own-XCD claim `raw`; -1: the XCD's tiles are all taken (no stealing across
   // XCDs: RCCL's blocks spread over every XCD, and the claim code must stay register-cheap)
-  auto resolve = [&](int raw) -> int { return raw < xcount(xcd) ? xbase(xcd) + raw : -1; };
+  auto resolve = [&](int raw) -> int {
+    return raw + nbx < xcount(xcd) ? xbase(xcd) + raw + nbx : -1;
+  };
   auto finished = [&](int old) {   // old: this block's pre-increment value of the done counter
     if (old == G - 1)
 #pragma unroll
@@ -878,16 +885,15 @@ __device__ __forceinline__ void gemm256_persistent_body(const GemmArgs& a, char*
   int m0, n0;
   int raw = 0;   // DYN, lane QL: the claim in flight (own-XCD counter value or done count)
   if constexpr (DYN) {
-    volatile LDS_AS int* q0 = (volatile LDS_AS int*)(LDS_AS char*)(smem + 7 * HALF_BYTES);
-    if (threadIdx.x == QL) {   // (slot 7 is free in the prologue)
-      const int id0 = resolve(claim_add(xcd));
-      *q0 = id0;
-      if (id0 < 0) finished(claim_add(8));
-      else raw = claim_add(xcd);   // tile 1, resolved after the prologue's DMA wait
+    // the first tile is static (see nbx): its DMA is issued at once, with tile 1's claim in
+    // flight beside it, so no claim round trip precedes the block's first operand
+    const int bi = b >> 3;
+    const int id0 = bi < xcount(xcd) ? xbase(xcd) + bi : -1;
+    if (id0 < 0) {   // (G <= ntiles: not taken; the done count must still reach G)
+      if (threadIdx.x == QL) finished(claim_add(8));
+      return;
     }
-    __syncthreads();
-    const int id0 = __builtin_amdgcn_readfirstlane(*q0);
-    if (id0 < 0) return;
+    if (threadIdx.x == QL) raw = claim_add(xcd);   // tile 1, resolved after the prologue's DMA wait
     tile_at(id0, m0, n0);
   } else {
     tile_org(0, m0, n0);

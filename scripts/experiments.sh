@@ -288,6 +288,21 @@ for l in open('$O/cfg5.jsonl'):
       python3 -m vi_normflows_amd.bench.gap_summary $O/$t > $O/${t}_gaps.txt 2>&1 || true
     done
     head -14 $O/plain_summary.txt; head -24 $O/rccl_summary.txt ;;
+  rccl_ab)        # the 1-rank RCCL path (bench.py --force-reduce) of this tree's library vs a
+                  # variant build, with the plain step alongside: args V [rounds]; the persistent
+                  # GEMM GPU tests first
+    v=$1; r=${2:-3}; P=vi_normflows_amd/_native/libvinf_hip_$v.so
+    timeout -k 10 400 python -u -m pytest tests/test_gemm_persistent_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 || { echo PYTEST_FAIL; tail -30 $O/pytest.txt; exit 1; }
+    tail -1 $O/pytest.txt
+    for i in $(seq $r); do
+      for arm in plain rccl rccl_$v; do
+        L=""; X=""
+        [ $arm != plain ] && X=--force-reduce
+        [ $arm = rccl_$v ] && L=$P
+        VINF_NATIVE_LIB=$L timeout -k 10 240 python bench.py --steps 20 --warmup 5 $X > $O/b.json 2> $O/b.err || { echo BENCH_FAIL; tail -20 $O/b.err; exit 1; }
+        python -c "import json;d=json.load(open('$O/b.json'));print(json.dumps({'arm':'$arm','ms':d['ms_per_step'],'identical':d['notes']['replicas_identical']}))" | tee -a $O/ab.jsonl
+      done
+    done ;;
   getdata_trace)  # kernel trace of the 2-D potential CLI on the GPU (fused target kernel)
     export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 -m vi_normflows_amd.get_data 8 100 0.02 p1 --device cuda --samples 1048576 --quiet > $O/out.txt 2>&1 || { echo PROF_FAIL; tail -20 $O/out.txt; exit 1; }
