@@ -288,6 +288,17 @@ for l in open('$O/cfg5.jsonl'):
       python3 -m vi_normflows_amd.bench.gap_summary $O/$t > $O/${t}_gaps.txt 2>&1 || true
     done
     head -14 $O/plain_summary.txt; head -24 $O/rccl_summary.txt ;;
+  cfg_trace_libs) # kernel traces of one north-star config on this tree's library and on variant
+                  # builds (probe builds included: timings only): args CONFIG BATCH PREC variants...
+    export TMPDIR=/tmp
+    c=$1; b=$2; pr=$3; shift 3
+    for lib in default "$@"; do
+      if [ $lib = default ]; then L=""; else L=vi_normflows_amd/_native/libvinf_hip_$lib.so; fi
+      VINF_NATIVE_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/t_${lib}_$pr -o run --output-format csv -- \
+        python3 -m vi_normflows_amd.bench.configs --config $c --batch $b --precision $pr --graph off --steps 5 --warmup 3 > $O/r_${lib}_$pr.json 2> $O/r_${lib}_$pr.err || { tail -20 $O/r_${lib}_$pr.err; exit 1; }
+      python3 -m vi_normflows_amd.bench.prof_summary $O/t_${lib}_$pr > $O/summary_${lib}_$pr.txt 2>&1
+      echo "== $lib $pr"; head -8 $O/summary_${lib}_$pr.txt
+    done ;;
   rccl_ab)        # the 1-rank RCCL path (bench.py --force-reduce) of this tree's library vs a
                   # variant build, with the plain step alongside: args V [rounds]; the persistent
                   # GEMM GPU tests first
