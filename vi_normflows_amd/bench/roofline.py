@@ -41,12 +41,12 @@ FAMILIES = [
     (r"gemm_tn4w4?_kernel", "wgrad TN bf16 4-wave (multi-layer, K = batch)", 16384),
     (r"gemm256_multi_kernel<4, true", "wgrad TN e4m3 (multi-layer)", 65536),
     (r"gemm256_multi_kernel<", "wgrad TN bf16 (multi-layer, K = batch)", 16384),
-    (r"gemm256_persistent_kernel<true, true, 0>", "fwd NT EPI0 (bias+ReLU+bitmask)", 16384),
-    (r"gemm256_persistent_kernel<true, true, 2>", "dgrad NT EPI2 (ReLU bitmask)", 16384),
-    (r"gemm256_persistent_kernel<true, true, 5>", "coupling fwd NT EPI5 (fused)", 16384),
-    (r"gemm256_persistent_kernel<true, true, 4>", "coupling bwd NT EPI4 (fused)", 16384),
-    (r"gemm256_persistent_kernel<true, true, 6>", "coupling bwd NT EPI6 (fused, bf16 x)", 16384),
-    (r"gemm256_persistent_kernel<true, false, 3>", "layer-0 dgrad NN EPI3 (fp32 acc)", 16384),
+    (r"gemm256_persistent_kernel<true, true, 0(, (true|false))?>", "fwd NT EPI0 (bias+ReLU+bitmask)", 16384),
+    (r"gemm256_persistent_kernel<true, true, 2(, (true|false))?>", "dgrad NT EPI2 (ReLU bitmask)", 16384),
+    (r"gemm256_persistent_kernel<true, true, 5(, (true|false))?>", "coupling fwd NT EPI5 (fused)", 16384),
+    (r"gemm256_persistent_kernel<true, true, 4(, (true|false))?>", "coupling bwd NT EPI4 (fused)", 16384),
+    (r"gemm256_persistent_kernel<true, true, 6(, (true|false))?>", "coupling bwd NT EPI6 (fused, bf16 x)", 16384),
+    (r"gemm256_persistent_kernel<true, false, 3(, (true|false))?>", "layer-0 dgrad NN EPI3 (fp32 acc)", 16384),
     (r"gemm256_kernel<true, true, 5, 4, false, true>", "MAF fwd e4m3 EPI5 (fused)", 65536),
     (r"gemm256_kernel<true, true, 4, 4, false, true>", "MAF bwd e4m3 EPI4 (fused)", 65536),
     (r"gemm256_kernel<true, true, 2, 4, false, true>", "dgrad e4m3 EPI2", 65536),
