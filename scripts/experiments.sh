@@ -299,6 +299,34 @@ for l in open('$O/cfg5.jsonl'):
       python3 -m vi_normflows_amd.bench.prof_summary $O/t_${lib}_$pr > $O/summary_${lib}_$pr.txt 2>&1
       echo "== $lib $pr"; head -8 $O/summary_${lib}_$pr.txt
     done ;;
+  f8_lib_ab)      # e4m3 path of a variant build (arg: V): the fp8 / MAF GPU tests on V, the
+                  # e4m3 256x256 products alternating default / V, config-5 fp8 kernel traces and
+                  # two interleaved config-5 rounds (fp8 and bf16)
+    v=$1; P=vi_normflows_amd/_native/libvinf_hip_$v.so
+    VINF_NATIVE_LIB=$P timeout -k 10 600 python -u -m pytest tests/test_fp8_gpu.py tests/test_fp8_wgrad_gpu.py tests/test_maf_engine.py -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 || { echo PYTEST_FAIL; tail -30 $O/pytest.txt; exit 1; }
+    tail -1 $O/pytest.txt
+    for lib in default $v default $v; do
+      if [ $lib = default ]; then L=""; else L=$P; fi
+      VINF_NATIVE_LIB=$L timeout -k 10 200 python -m vi_normflows_amd.bench.gemm_bench --batch 32768 --only fwd_l2_fp8,sq4096_fp8 > $O/g.txt 2>&1 || { tail -20 $O/g.txt; exit 1; }
+      grep shape $O/g.txt | sed "s/^/$lib /" | tee -a $O/gemm.txt
+    done
+    bash scripts/experiments.sh cfg_trace_libs 5 32768 fp8 $v && bash scripts/experiments.sh cfg5_libs 2 $v ;;
+  f8_pmc)         # wave-state counters of the 256x256 kernel on the 4096^3 product, bf16 vs e4m3
+                  # (args: [variant libs]): where an e4m3 K-tile spends its extra time
+    export TMPDIR=/tmp
+    P1="GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA"
+    P2="GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC"
+    for lib in default "$@"; do
+      if [ $lib = default ]; then L=""; else L=vi_normflows_amd/_native/libvinf_hip_$lib.so; fi
+      for s in sq4096 sq4096_fp8; do
+        for pp in 1 2; do
+          eval "C=\$P$pp"
+          VINF_NATIVE_LIB=$L timeout -s KILL 120 rocprofv3 --pmc $C -d $O/${lib}_${s}_p$pp -o pmc --output-format csv -- python3 -m vi_normflows_amd.bench.gemm_bench --only $s > $O/${lib}_${s}_p$pp.log 2>&1 || { echo P${pp}_FAIL $lib $s; tail -20 $O/${lib}_${s}_p$pp.log; exit 1; }
+        done
+        python3 -m vi_normflows_amd.bench.pmc_summary $O/${lib}_${s}_p1 $O/${lib}_${s}_p2 > $O/${lib}_${s}_summary.txt 2>&1
+        echo "== $lib $s"; cat $O/${lib}_${s}_summary.txt
+      done
+    done ;;
   rccl_ab)        # the 1-rank RCCL path (bench.py --force-reduce) of this tree's library vs a
                   # variant build, with the plain step alongside: args V [rounds]; the persistent
                   # GEMM GPU tests first
