@@ -120,9 +120,26 @@ def _check_maf(tmp_path, precision, gpu):
     rel = float((dp - ref).norm() / ref.norm())
     # fp32 (CPU): summation order only; bf16 GEMMs: the same per-row products, only the
     # batch reduction splits; fp8: per-tensor activation scales depend on each rank's batch
-    tol = {"fp32": 1e-5, "bf16": 1e-3, "fp8": 5e-2}["fp32" if not gpu else precision]
+    # (measured on MI355X: bf16 8.6e-8, fp8 9.5e-3)
+    tol = {"fp32": 1e-5, "bf16": 1e-5, "fp8": 2.5e-2}["fp32" if not gpu else precision]
     assert rel < tol, rel
     if precision == "fp8" and gpu:
+        # the DP deviation is e4m3 quantisation noise, not a reduction error: it stays within
+        # the same order as the single-process fp8 gradient's own distance from bf16 on the
+        # same batch and weights
+        bf = MAFEngine(_maf_cfg("bf16", gpu), batch=world * B, device=dev, seed=5)
+        bf.params.master.copy_(r0["master0"].to(dev))
+        bf.params.sync_compute()
+        bf.data_override = data_all.to(dev)
+        bf._update_schedule()
+        bf.forward()
+        bf.backward()
+        ref_bf = bf.params.grad.cpu()
+        e_f8 = float((ref - ref_bf).norm() / ref_bf.norm())
+        e_dp = float((dp - ref_bf).norm() / ref_bf.norm())
+        print(f"[dp maf fp8] |dp - single fp8| {rel:.3e}, |single fp8 - bf16| {e_f8:.3e}, "
+              f"|dp - bf16| {e_dp:.3e}")
+        assert rel < 2.0 * e_f8 and e_dp < 2.0 * e_f8, (rel, e_f8, e_dp)
         assert r0["f8_wgrad"]
         # rank-local delayed scales: the ranks saw different data, so their amax histories
         # differ - and the replicas above are still bitwise identical
