@@ -503,7 +503,8 @@ void gemm_nn_cpl(const at::Tensor& dy, const at::Tensor& W, const at::Tensor& G,
 void maf_gemm_fwd(const at::Tensor& h, const c10::optional<at::Tensor>& hs, const at::Tensor& W,
                   const c10::optional<at::Tensor>& ws, const c10::optional<at::Tensor>& b,
                   const at::Tensor& krange, const at::Tensor& s_out, const at::Tensor& x,
-                  const at::Tensor& u, const c10::optional<at::Tensor>& ubf, const at::Tensor& ldjp,
+                  const c10::optional<at::Tensor>& u, const c10::optional<at::Tensor>& ubf,
+                  const at::Tensor& ldjp,
                   bool ldj_init, double bound, const c10::optional<at::Tensor>& uq,
                   const c10::optional<at::Tensor>& q_amax_prev,
                   const c10::optional<at::Tensor>& q_scale,
@@ -521,11 +522,16 @@ void maf_gemm_fwd(const at::Tensor& h, const c10::optional<at::Tensor>& hs, cons
     chk_mat(W, "W", at::kBFloat16);
   }
   chk_mat(s_out, "s_out", at::kBFloat16);
-  chk_mat(x, "x", at::kFloat);
-  chk_mat(u, "u", at::kFloat);
+  // x: fp32 or bf16 (a bf16 flow state); u may be None when ubf is given (bf16 state out)
+  const bool x_bf16 = x.scalar_type() == at::kBFloat16;
+  chk_mat(x, "x", x_bf16 ? at::kBFloat16 : at::kFloat);
+  const bool has_u = u && u->defined();
+  if (has_u) chk_mat(*u, "u", at::kFloat);
+  TORCH_CHECK(has_u || (ubf && ubf->defined()),
+              "maf_gemm_fwd: u may be omitted only with a ubf output (a bf16 state)");
   const int M = h.size(0), K = h.size(1), D = x.size(1);
   TORCH_CHECK(W.size(0) == 2 * D && W.size(1) == K, "W must be [2D, K]");
-  TORCH_CHECK(D % 128 == 0 && x.size(0) == M && u.size(0) == M && u.size(1) == D &&
+  TORCH_CHECK(D % 128 == 0 && x.size(0) == M && (!has_u || (u->size(0) == M && u->size(1) == D)) &&
                   s_out.size(0) == M && s_out.size(1) == D, "maf_gemm_fwd shapes (D % 128 == 0)");
   chk_ranges(krange, D / 128, "krange");
   TORCH_CHECK(ldjp.is_cuda() && ldjp.scalar_type() == at::kFloat && ldjp.dim() == 2 &&
@@ -565,9 +571,10 @@ void maf_gemm_fwd(const at::Tensor& h, const c10::optional<at::Tensor>& hs, cons
   nf_launch_gemm256_maf_fwd(h.data_ptr(), ld2(h), f8 ? 1 : 0, f8 ? hs->data_ptr<float>() : nullptr,
                             W.data_ptr(), ld2(W), f8 ? ws->data_ptr<float>() : nullptr, bp,
                             krange.data_ptr<int>(), s_out.data_ptr(), ld2(s_out), M, K, D,
-                            x.data_ptr<float>(), ld2(x), u.data_ptr<float>(), ld2(u), ubp, ldub,
+                            (const float*)x.data_ptr(), ld2(x),
+                            has_u ? u->data_ptr<float>() : nullptr, has_u ? ld2(*u) : 0, ubp, ldub,
                             ldjp.data_ptr<float>(), ldjp.stride(0), ldj_init, (float)bound, qp, ldq,
-                            qap, qs, qac, cur_stream());
+                            qap, qs, qac, cur_stream(), x_bf16 ? 1 : 0);
 }
 
 // MAF layer l's first MADE product input gradient (gy = G + dy (W1*M1), NT against Wt = (W1*M1)^T,
@@ -674,7 +681,8 @@ void maf_gemm_bwd(const at::Tensor& dy, const at::Tensor& Wt, const at::Tensor& 
   TORCH_CHECK(has_dst || (f8 && dstq && dstq->defined()), "maf_gemm_bwd: dst and / or dstq");
   if (has_dst) chk_mat(*dst_opt, "dst", at::kBFloat16);
   chk_mat(G, "G", at::kFloat);
-  chk_mat(u, "u", at::kFloat);
+  const bool u_bf16 = u.scalar_type() == at::kBFloat16;   // a bf16 MAF state (bf16_state)
+  chk_mat(u, "u", u_bf16 ? at::kBFloat16 : at::kFloat);
   chk_mat(gx, "gx", at::kFloat);
   const int M = dy.size(0), K = dy.size(1), D = Wt.size(0);
   TORCH_CHECK(Wt.size(1) == K && K % 32 == 0 && D % 8 == 0, "Wt must be [D, K], K % 32 == 0");
@@ -694,11 +702,12 @@ void maf_gemm_bwd(const at::Tensor& dy, const at::Tensor& Wt, const at::Tensor& 
     fo.q_amax_prev = o.ap; fo.q_scale_out = o.qs; fo.q_amax_cur = o.ac;
   }
   nf_launch_gemm256_nn_cpl(dy.data_ptr(), ld2(dy), Wt.data_ptr(), ld2(Wt), G.data_ptr<float>(),
-                           ld2(G), M, D, K, s_raw.data_ptr(), ld2(s_raw), u.data_ptr<float>(),
-                           ld2(u), has_dst ? dst_opt->data_ptr() : nullptr,
+                           ld2(G), M, D, K, s_raw.data_ptr(), ld2(s_raw),
+                           (const float*)u.data_ptr(), ld2(u),
+                           has_dst ? dst_opt->data_ptr() : nullptr,
                            has_dst ? ld2(*dst_opt) : 2 * D, 2 * D, gx.data_ptr<float>(), ld2(gx),
                            D, (float)bound, (float)c, cur_stream(), 1, krange256.data_ptr<int>(),
-                           segs, 1, f8 ? &fo : nullptr);
+                           segs, 1, f8 ? &fo : nullptr, u_bf16 ? 1 : 0);
 }
 
 // all `layers` weights of one kind (rows_per x C each, layer_stride elements apart in the flat
@@ -1093,7 +1102,7 @@ TORCH_LIBRARY_FRAGMENT(vinf, m) {
   m.def("gemm_tn_multi_f8(Tensor[] dy, Tensor[] x, Tensor(a!)[] dW, Tensor(b!)?[] db, int tile0, int ntiles, Tensor?[] tiles, Tensor?[] cmask, Tensor scales, int[] sa_idx, int[] sb_idx) -> ()");
   m.def("gemm_nt_cpl(Tensor h, Tensor W, Tensor? b, Tensor(a!)? st, Tensor x, Tensor(b!) y, Tensor(c!)? yb, Tensor(d!) ldjp, bool ldj_init, float scale, bool inverse=False) -> ()");
   m.def("gemm_nn_cpl(Tensor dy, Tensor W, Tensor G, Tensor s_hat, Tensor x, Tensor(a!) dst, Tensor(b!) gx, float scale, float c, Tensor? Wt=None) -> ()");
-  m.def("maf_gemm_fwd(Tensor h, Tensor? hs, Tensor W, Tensor? ws, Tensor? b, Tensor krange, Tensor(a!) s_out, Tensor x, Tensor(b!) u, Tensor(c!)? ubf, Tensor(d!) ldjp, bool ldj_init, float bound, Tensor(e!)? uq=None, Tensor? q_amax_prev=None, Tensor(f!)? q_scale=None, Tensor(g!)? q_amax_cur=None) -> ()");
+  m.def("maf_gemm_fwd(Tensor h, Tensor? hs, Tensor W, Tensor? ws, Tensor? b, Tensor krange, Tensor(a!) s_out, Tensor x, Tensor(b!)? u, Tensor(c!)? ubf, Tensor(d!) ldjp, bool ldj_init, float bound, Tensor(e!)? uq=None, Tensor? q_amax_prev=None, Tensor(f!)? q_scale=None, Tensor(g!)? q_amax_cur=None) -> ()");
   m.def("maf_gemm_bwd(Tensor dy, Tensor Wt, Tensor krange256, Tensor G, Tensor s_raw, Tensor u, Tensor(a!)? dst, Tensor(b!) gx, float bound, float c, Tensor? sa=None, Tensor? sb=None, Tensor(c!)? dstq=None, Tensor? q_amax_prev=None, Tensor(d!)? q_scale=None, Tensor(e!)? q_amax_cur=None) -> ()");
   m.def("fp8_dgrad(Tensor dyq, Tensor sa, Tensor Wtq, Tensor sb, Tensor h, Tensor(a!)? dx, Tensor krange256, Tensor(b!)? dxq=None, Tensor? q_amax_prev=None, Tensor(c!)? q_scale=None, Tensor(d!)? q_amax_cur=None) -> ()");
   m.def("fp8_quant_rows_strided(Tensor x, int layer_stride, int rows_per, int layers, int C, Tensor(a!) q, Tensor(b!) scale) -> ()");

@@ -120,6 +120,9 @@ struct GemmArgs {
   // cf_mode 0 inverse: x = (y - t) e^-s from the layer's output y (cf_x) into cf_y / cf_yb, the
   // ldj share is -sum s; C (s_hat) may be null
   int cf_inverse;
+  // cf_x_bf16: cf_x holds bf16 (a bf16 flow state: the MAF engine's bf16_state option). cf_y may
+  // be null (a bf16 state out: only cf_yb is written)
+  int cf_x_bf16;
   // persistent launches with dynamic tile claims (gemm256.hip, persist mode 2): this launch's
   // counter slot, 8 per-XCD claim counters + 1 finished-block counter (one 128-B line each,
   // QCTR_LINE ints apart), zero at launch start and zeroed again by the launch's last block
@@ -481,11 +484,11 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
     // registers for the pass's preloaded operands, 264 B/lane of scratch at 2)
     constexpr bool CPLB = EPI == EPI_CPL_BWD || EPI == EPI_CPL_BWD_XB;
     constexpr bool XB = EPI == EPI_CPL_BWD_XB;   // x operand in bf16
-    constexpr int PJ = (F8 && EPI == EPI_CPL_BWD) ? 1 : 2;
+    constexpr int PJ = (F8 && CPLB) ? 1 : 2;
     constexpr int PIT = PJ * 4;       // readback iterations (4 rows each) per pass
     // e4m3 operands (EPI_CPL_BWD): acc * f8_sa[0] * f8_sb[n], and with f8_cq the e4m3 copy of
     // dst = [dS | dT] (the next fp8 input-gradient product's operand) under a delayed scale
-    constexpr bool f8c = F8 && EPI == EPI_CPL_BWD;
+    constexpr bool f8c = F8 && CPLB;
     // e4m3 weight gradients (EPI_F32): dW = acc * sa * sb, both per-tensor scales
     float w8 = 1.f;
     if constexpr (F8 && EPI == EPI_F32) w8 = a.f8_sa[0] * a.f8_sb[0];

@@ -161,7 +161,7 @@ void nf_launch_gemm256_maf_fwd(const void* h, long ldh, int f8, const float* hs,
                                long ld_x, float* u, long ld_u, void* ubf, long ld_ub, float* ldjp,
                                long ld_ldjp, int ldj_init, float bound, void* uq, long lduq,
                                const float* q_amax_prev, float* q_scale_out, float* q_amax_cur,
-                               hipStream_t stream);
+                               hipStream_t stream, int x_bf16 = 0);
 int nf_launch_gemm256_tn_partials(const void* dy, long lddy, const void* x, long ldx, float* C,
                                   long ldc, long slab_stride, float* dbias, int M, int N, int K,
                                   int splits, hipStream_t stream);

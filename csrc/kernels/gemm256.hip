@@ -298,9 +298,14 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
       xv[it][0] = xv[it][1] = make_float4(0.f, 0.f, 0.f, 0.f);
       lold[it] = 0.f;
       if (m < a.M && fok && xl_on) {
-        const float* xr = a.cf_x + (long)m * a.ld_cf_x + jf;
-        xv[it][0] = *reinterpret_cast<const float4*>(xr);
-        xv[it][1] = *reinterpret_cast<const float4*>(xr + 4);
+        if (a.cf_x_bf16) {   // 8 bf16 in xv[it][0]'s bits, expanded at the use
+          const bf16_t* xr = reinterpret_cast<const bf16_t*>(a.cf_x) + (long)m * a.ld_cf_x + jf;
+          xv[it][0] = __builtin_bit_cast(float4, *reinterpret_cast<const uint4*>(xr));
+        } else {
+          const float* xr = a.cf_x + (long)m * a.ld_cf_x + jf;
+          xv[it][0] = *reinterpret_cast<const float4*>(xr);
+          xv[it][1] = *reinterpret_cast<const float4*>(xr + 4);
+        }
       }
       if (!a.cf_ldj_init && f8 == 0 && m < a.M) lold[it] = a.cf_ldj[(long)tn * a.ld_cf_ldj + m];
     }
@@ -342,7 +347,16 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
           const v4u sh = bf_stage_fix(*(const LDS_AS v4u*)(region_of(wrr * 4 + ws) + off), swp);
           const v4u tt = bf_stage_fix(*(const LDS_AS v4u*)(region_of(wrr * 4 + 2 + ws) + off), swp);
           const float4 x0 = xv[it][0], x1 = xv[it][1];
-          const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          if (a.cf_x_bf16) {
+            const uint4 xb = __builtin_bit_cast(uint4, x0);
+            const unsigned w4[4] = {xb.x, xb.y, xb.z, xb.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              xs[2 * e] = __uint_as_float(w4[e] << 16);
+              xs[2 * e + 1] = __uint_as_float(w4[e] & 0xffff0000u);
+            }
+          }
           float y[8];
           if (maf) {   // shv = s_raw, tv = mu
             const float ib = __builtin_amdgcn_rcpf(a.cf_scale);   // v_rcp, not an IEEE division per row
@@ -392,7 +406,7 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
                 make_uint2((unsigned)q0, (unsigned)q1);
           }
           float* yr = a.cf_y + (long)m * a.ld_cf_y + jf;
-          if (st_on) {
+          if (st_on && a.cf_y) {
             *reinterpret_cast<float4*>(yr) = make_float4(y[0], y[1], y[2], y[3]);
             *reinterpret_cast<float4*>(yr + 4) = make_float4(y[4], y[5], y[6], y[7]);
           }
@@ -1438,7 +1452,7 @@ void nf_launch_gemm256_maf_fwd(const void* h, long ldh, int f8, const float* hs,
                                long ld_x, float* u, long ld_u, void* ubf, long ld_ub, float* ldjp,
                                long ld_ldjp, int ldj_init, float bound, void* uq, long lduq,
                                const float* q_amax_prev, float* q_scale_out, float* q_amax_cur,
-                               hipStream_t stream) {
+                               hipStream_t stream, int x_bf16) {
   if (M <= 0) return;
   const int EB = f8 ? 1 : 2;
   GemmArgs a{};
@@ -1449,7 +1463,7 @@ void nf_launch_gemm256_maf_fwd(const void* h, long ldh, int f8, const float* hs,
   const int ntn = D / 128;
   a.M = M; a.N = ntn * 256; a.K = K; a.k_per_split = f8 ? K : ((K + 63) / 64) * 64;
   a.krange = krange; a.krange_segs = 1;
-  a.cf_x = x; a.ld_cf_x = ld_x;
+  a.cf_x = x; a.ld_cf_x = ld_x; a.cf_x_bf16 = x_bf16;   // x_bf16: x points at bf16 (u may be null)
   a.cf_y = u; a.ld_cf_y = ld_u;
   a.cf_yb = (nf::bf16_t*)ubf; a.ld_cf_yb = ld_ub; a.cf_yb_width = D;
   a.cf_ldj = ldjp; a.ld_cf_ldj = ld_ldjp; a.cf_ldj_init = ldj_init;
@@ -1458,8 +1472,9 @@ void nf_launch_gemm256_maf_fwd(const void* h, long ldh, int f8, const float* hs,
   a.f8_cq = (unsigned char*)uq; a.ld_f8_cq = lduq;
   a.f8_q_amax_prev = q_amax_prev; a.f8_q_scale_out = q_scale_out; a.f8_q_amax_cur = q_amax_cur;
   auto al16 = [](const void* p) { return ((unsigned long)p & 15) == 0; };
-  if (D % 128 || ld_x % 4 || ld_u % 4 || ld_s % 8 || (ubf && (ld_ub % 8 || !al16(ubf))) ||
-      !al16(x) || !al16(u) || !al16(s_out) || !krange || (f8 && (K % 128 || !hs || !ws)) ||
+  if (D % 128 || ld_x % (x_bf16 ? 8 : 4) || (u && ld_u % 4) || ld_s % 8 ||
+      (ubf && (ld_ub % 8 || !al16(ubf))) || (!u && !ubf) ||
+      !al16(x) || (u && !al16(u)) || !al16(s_out) || !krange || (f8 && (K % 128 || !hs || !ws)) ||
       (uq && (!f8 || lduq % 8 || !q_amax_prev || !q_scale_out || !q_amax_cur)) ||
       (!f8 && K % 32)) {
     fprintf(stderr, "vinf: fused MAF-forward GEMM needs D %% 128 == 0, 16-B aligned rows, K "
@@ -1536,10 +1551,12 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
     fprintf(stderr, "vinf: bf16 G chain in the fused backward needs the bf16-x form\n");
     abort();
   }
-  // x_bf16: x is the bf16 copy of h_{l-1} (EPI_CPL_BWD_XB; bf16 coupling form only)
+  // x_bf16 (EPI_CPL_BWD_XB): x is the bf16 copy of h_{l-1} (coupling) or the bf16 MAF state u
   const int epi = x_bf16 ? EPI_CPL_BWD_XB : EPI_CPL_BWD;
-  if (x_bf16 && (f8 || mode || !w_kmajor)) {
-    fprintf(stderr, "vinf: bf16 x in the fused backward needs the bf16 coupling form with Wt\n");
+  // (the MAF engine's bf16_state option runs the MAF mode, e4m3 included, on bf16 u)
+  if (x_bf16 && (!w_kmajor || ((g_in_bf16 || gx_bf16) && (f8 || mode)))) {
+    fprintf(stderr, "vinf: bf16 x in the fused backward needs Wt (and the bf16 G chain the bf16 "
+                    "coupling form)\n");
     abort();
   }
   if (Dh > N || dst_pad < 2 * Dh || dst_pad > Dh + N || !staged_ok(a, epi)) {
@@ -1553,7 +1570,8 @@ void nf_launch_gemm256_nn_cpl(const void* dy, long lddy, const void* W, long ldw
       abort();
     }
     a.k_per_split = K;
-    g256::launch_f8<EPI_CPL_BWD>(a, stream);
+    if (x_bf16) g256::launch_f8<EPI_CPL_BWD_XB>(a, stream);
+    else g256::launch_f8<EPI_CPL_BWD>(a, stream);
     return;
   }
   if (x_bf16) {

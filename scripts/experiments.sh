@@ -311,6 +311,23 @@ for l in open('$O/cfg5.jsonl'):
       grep shape $O/g.txt | sed "s/^/$lib /" | tee -a $O/gemm.txt
     done
     bash scripts/experiments.sh cfg_trace_libs 5 32768 fp8 $v && bash scripts/experiments.sh cfg5_libs 2 $v ;;
+  cfg5_state_ab)  # config 5 with the bf16 MAF state (KernelPaths.maf_bf16_state) vs the fp32
+                  # state: the MAF engine GPU tests, then interleaved fp8 / bf16 runs [rounds] and
+                  # an fp8 kernel trace with the option
+    export TMPDIR=/tmp
+    timeout -k 10 600 python -u -m pytest tests/test_maf_engine.py -m gpu -x -q -s --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.txt 2>&1 || { echo PYTEST_FAIL; tail -40 $O/pytest.txt; exit 1; }
+    grep "bf16 state\|passed" $O/pytest.txt
+    for r in $(seq ${1:-2}); do
+      for st in 0 1; do
+        for pr in fp8 bf16; do
+          VINF_KERNEL_PATHS=maf_bf16_state=$st timeout -k 10 240 python -m vi_normflows_amd.bench.configs --config 5 --precision $pr --batch 32768 > $O/c.json 2>> $O/c.err || { tail -20 $O/c.err; exit 1; }
+          python -c "import json;d=json.load(open('$O/c.json'));print(json.dumps({'bf16_state':$st,'prec':'$pr','ms':d['ms_per_step'],'sps':d['samples_per_s']}))" | tee -a $O/cfg5.jsonl
+        done
+      done
+    done
+    VINF_KERNEL_PATHS=maf_bf16_state=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/t_state -o run --output-format csv -- \
+      python3 -m vi_normflows_amd.bench.configs --config 5 --batch 32768 --precision fp8 --graph off --steps 5 --warmup 3 > $O/r_state.json 2> $O/r_state.err || { tail -20 $O/r_state.err; exit 1; }
+    python3 -m vi_normflows_amd.bench.prof_summary $O/t_state > $O/summary_state.txt 2>&1; head -10 $O/summary_state.txt ;;
   f8_pmc)         # wave-state counters of the 256x256 kernel on the 4096^3 product, bf16 vs e4m3
                   # (args: [variant libs]): where an e4m3 K-tile spends its extra time
     export TMPDIR=/tmp

@@ -178,9 +178,17 @@ class MAFEngine:
         self.wt_dgrad = self.wgrad_defer and kp.dgrad_nt
         # (the fused backward is an NT product against (W*M)^T)
         self.fuse = dev.type == "cuda" and D % 128 == 0 and fuse_env and self.wt_dgrad
+        # bf16 flow state (paths.maf_bf16_state, fused GPU engine only): the layers pass
+        # u_1 .. u_{L-1} in bf16 (Xbf, which the next MADE product and the weight gradients read
+        # anyway) instead of fp32 plus a bf16 copy; the data x_0 and u_L (the NLL) stay fp32.
+        # The fused MAF epilogues then read half the state bytes and the forward writes a third
+        # of them (docs/PERF_NOTES.md round 6, "MAF forward epilogue"). It changes the density's
+        # numerics (every intermediate u rounded to bf16), so it is opt-in.
+        self.bf16_state = False
         if self.fuse:
             self.S = torch.empty(L, B, D, dtype=self.cdt, device=dev)      # s_raw per layer
             self.ldjp = torch.empty(D // 128, B, dtype=f32, device=dev)    # per-tile ldj shares
+            self.bf16_state = kp.maf_bf16_state and self.cdt == torch.bfloat16
         else:
             self.O = torch.empty(L, B, 2 * D, dtype=self.cdt, device=dev)  # [mu | s_raw]
         self.WT = None
@@ -256,6 +264,12 @@ class MAFEngine:
         else:
             self.fp8_bwd = False
             self.f8_wgrad = False
+
+    def _state(self, l: int) -> torch.Tensor:
+        """u_l as the fused kernels read it: bf16 for 0 < l < L under bf16_state, else fp32."""
+        if self.bf16_state and 0 < l < self.cfg.n_layers:
+            return self.Xbf[l]
+        return self.X[l]
 
     def _lean8(self) -> bool:
         """Steady fp8 steps with e4m3 weight gradients: the bf16 copies of x, dO and dH have no
@@ -432,21 +446,31 @@ class MAFEngine:
                 nxt = None if last else self.sx[l + 1]
                 qargs = ((self._xq(l + 1), nxt.amax[0:1], nxt.scale, nxt.cur)
                          if nxt is not None else ())
-                ubf = None if self._lean8() else self.Xbf[l + 1]
+                u, ubf = self._fwd_outputs(l)
                 native().maf_gemm_fwd(self._hq(l), sh, self.W2q[l * 2 * D:(l + 1) * 2 * D],
                                       self.s2[l * 2 * D:(l + 1) * 2 * D], b2, mk["P2pair"],
-                                      self.S[l], self.X[l], self.X[l + 1], ubf,
+                                      self.S[l], self._state(l), u, ubf,
                                       self.ldjp, l == 0, float(cfg.alpha_bound), *qargs)
                 if nxt is not None:
                     sxs = nxt.scale
             else:
                 native().masked_gemm_nt(self.Xbf[l], P.c(f"l{l}.W1"), b1, self.Hbf[l], 1,
                                         mk["P1"].fwd, mk["P1"].fwd256)
+                u, ubf = self._fwd_outputs(l)
                 native().maf_gemm_fwd(self.Hbf[l], None, P.c(f"l{l}.W2"), None, b2, mk["P2pair"],
-                                      self.S[l], self.X[l], self.X[l + 1], self.Xbf[l + 1],
+                                      self.S[l], self._state(l), u, ubf,
                                       self.ldjp, l == 0, float(cfg.alpha_bound))
         torch.sum(self.ldjp, 0, out=self.ldj)
         self._nll()
+
+    def _fwd_outputs(self, l: int):
+        """(fp32 u, bf16 u) written by layer l's fused forward: under bf16_state only the bf16
+        state below the top layer; else fp32 u plus its bf16 copy (skipped by steady fp8 steps
+        with e4m3 weight gradients, whose next product reads the e4m3 copy)."""
+        top = l + 1 == self.cfg.n_layers
+        if self.bf16_state and not top:
+            return None, self.Xbf[l + 1]
+        return self.X[l + 1], (None if self._lean8() else self.Xbf[l + 1])
 
     def s_raw(self, l: int) -> torch.Tensor:
         """s_raw of layer l (the fused engine keeps only this half of [mu | s_raw])."""
@@ -570,7 +594,7 @@ class MAFEngine:
             if l > 0:
                 # gy_{l-1} = gx (direct path of layer l) + dH_l (W1 M1): layer l-1's backward
                 native().maf_gemm_bwd(self.dHL[l], WT[l][0], mk["P1"].bwd256, gx, self.S[l - 1],
-                                      self.X[l], self.dOL[l - 1], gu, float(cfg.alpha_bound),
+                                      self._state(l), self.dOL[l - 1], gu, float(cfg.alpha_bound),
                                       1.0 / self.B)
                 gu, gx = gx, gu
             sched.ready(plan.unit_ends[k][1], final=(l == 0))
@@ -627,7 +651,7 @@ class MAFEngine:
             if l > 0:
                 nx = self.sdo[l - 1]
                 native().maf_gemm_bwd(self._dhq(l), self.W1Tq[l * D:(l + 1) * D], mk["P1"].bwd256,
-                                      gx, self.S[l - 1], self.X[l],
+                                      gx, self.S[l - 1], self._state(l),
                                       None if lean else self.dOL[l - 1], gu, bound, c,
                                       sdh.scale, self.sW1T[l * D:(l + 1) * D], self._doq(l - 1),
                                       nx.amax[0:1], nx.scale, nx.cur)

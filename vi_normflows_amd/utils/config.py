@@ -180,6 +180,7 @@ class KernelPaths:
     maf_fuse: bool = True        # MAF transform fused into the MADE GEMM epilogues
     fp8_dgrad: bool = True       # MAF fp8: e4m3 input gradients
     fp8_wgrad: bool = True       # MAF fp8: e4m3 weight gradients
+    maf_bf16_state: bool = False  # MAF fused engine: u_1 .. u_{L-1} kept in bf16 only (opt-in)
     made_fused: bool = True      # module path: fused MADE autograd function (ops.made_fused)
 
     @classmethod
