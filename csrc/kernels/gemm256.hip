@@ -246,33 +246,42 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
     return;
   }
 #endif
-  // bias (and e4m3 dequantisation scale) of the 4 columns of fragment i. AT_USE: read where
-  // they are used (cached; 32 more live registers across the parking loop spilled the e4m3 and
+  // bias (and e4m3 dequantisation scale) of the 4 columns of fragment i. AT_USE: read per pass,
+  // ahead of the pass's x loads (held across the whole epilogue they spilled the e4m3 and
   // one-pass builds); otherwise (the persistent bf16 form) read once up front.
   constexpr bool AT_USE = F8 || NP == 1;
-  auto col_params = [&](int i, float (&bv)[4], float (&sv)[4]) {
+  // raw per fragment i: bias bits (4 bf16 in 2 dwords) and, e4m3, the 4 weight-row scales
+  // (times f8_sa[0] at the use); kept packed so the per-pass preload stays small
+  unsigned bq[4][2];
+  float4 sq[4];
+  auto col_params = [&](int i) {
+    bq[i][0] = bq[i][1] = 0u;
+    sq[i] = make_float4(1.f, 1.f, 1.f, 1.f);
+#ifdef NF_PROBE_CF_NOCOLP   // timing probe: no bias / scale loads in the parking loop
+    return;
+#endif
     const int tc = wc * 64 + i * 16 + g * 4;                     // tile column (4 consecutive)
     const int f = j0 + (tc & 127);                               // feature
     const int row = tc < 128 ? f : a.cf_pair + f;                // weight / bias row
-    bv[0] = bv[1] = bv[2] = bv[3] = 0.f;
     if (a.bias && f < a.cf_dh) {
-      const ushort4 bb = *reinterpret_cast<const ushort4*>(a.bias + row);
-      bv[0] = bf2f(bb.x); bv[1] = bf2f(bb.y); bv[2] = bf2f(bb.z); bv[3] = bf2f(bb.w);
+      const uint2 bb = *reinterpret_cast<const uint2*>(a.bias + row);
+      bq[i][0] = bb.x; bq[i][1] = bb.y;
     }
-    sv[0] = sv[1] = sv[2] = sv[3] = 1.f;
     if constexpr (F8) {
-      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (f < a.cf_dh) t = *reinterpret_cast<const float4*>(a.f8_sb + row);
-      const float sa = a.f8_sa[0];
-      sv[0] = sa * t.x; sv[1] = sa * t.y; sv[2] = sa * t.z; sv[3] = sa * t.w;
+      sq[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (f < a.cf_dh) sq[i] = *reinterpret_cast<const float4*>(a.f8_sb + row);
     }
   };
-  float bpre[4][4];
+  float bpre[4][4];   // !AT_USE (persistent bf16): the bias as floats, converted once
   if constexpr (!AT_USE) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float sv[4];
-      col_params(i, bpre[i], sv);
+      col_params(i);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        bpre[i][2 * e] = __uint_as_float(bq[i][e] << 16);
+        bpre[i][2 * e + 1] = __uint_as_float(bq[i][e] & 0xffff0000u);
+      }
     }
   }
   float qinv = 1.f, qamax = 0.f;
@@ -286,6 +295,15 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     if (p) barrier();   // every wave's readback of the previous pass is done (its values were used)
+    // AT_USE: the pass's bias / scale loads go out BEFORE its x loads. vmcnt retires in issue
+    // order, so loaded at their use (inside the parking loop, behind the x loads) their first
+    // wait also waited out every x row: the x round trip sat in front of the parking instead
+    // of under it (e4m3 MAF forward 163 -> 139 us per call without those loads,
+    // profiles/r6/maf_fwd_colparams_probe.txt)
+    if constexpr (AT_USE) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) col_params(i);
+    }
     // this pass's x rows / previous log-det partials fetched up front: all in flight while the
     // accumulators are parked (the epilogue runs on every CU at once, so a load round trip per
     // row pair would sit exposed after the main loop)
@@ -315,15 +333,19 @@ __device__ __forceinline__ void epi_coupling_fwd(const GemmArgs& a, const v4f (&
       const int row = jj * 16 + c;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float bv[4], sv[4];
+        float bv[4];
         if constexpr (AT_USE) {
-          col_params(i, bv, sv);
+          bv[0] = __uint_as_float(bq[i][0] << 16);
+          bv[1] = __uint_as_float(bq[i][0] & 0xffff0000u);
+          bv[2] = __uint_as_float(bq[i][1] << 16);
+          bv[3] = __uint_as_float(bq[i][1] & 0xffff0000u);
         } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            bv[r] = bpre[i][r];
-            sv[r] = 1.f;
-          }
+          bv[0] = bpre[i][0]; bv[1] = bpre[i][1]; bv[2] = bpre[i][2]; bv[3] = bpre[i][3];
+        }
+        float sv[4] = {1.f, 1.f, 1.f, 1.f};
+        if constexpr (F8) {
+          const float sa = a.f8_sa[0];
+          sv[0] = sa * sq[i].x; sv[1] = sa * sq[i].y; sv[2] = sa * sq[i].z; sv[3] = sa * sq[i].w;
         }
         const unsigned lo = (unsigned)f2bf(fmaf(acc[i][j][0], sv[0], bv[0])) |
                             ((unsigned)f2bf(fmaf(acc[i][j][1], sv[1], bv[1])) << 16);
