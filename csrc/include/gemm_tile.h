@@ -484,6 +484,26 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
     // registers for the pass's preloaded operands, 264 B/lane of scratch at 2)
     constexpr bool CPLB = EPI == EPI_CPL_BWD || EPI == EPI_CPL_BWD_XB;
     constexpr bool XB = EPI == EPI_CPL_BWD_XB;   // x operand in bf16
+    // timing probes of the fused backward epilogue (docs/PERF_NOTES.md round 6; wrong results):
+    // NF_PROBE_CB_NOEPI no epilogue, NF_PROBE_CB_NOLOAD no C / s_hat / x reads,
+    // NF_PROBE_CB_NOSTORE no gx / dst / e4m3 stores
+#ifdef NF_PROBE_CB_NOEPI
+    if constexpr (CPLB) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          s += acc[i][J0 + j][0] + acc[i][J0 + j][1] + acc[i][J0 + j][2] + acc[i][J0 + j][3];
+      if (s == 1.2345e-30f) a.cpl_gx[lane] = s;
+      return;
+    }
+#endif
+#ifdef NF_PROBE_CB_NOSTORE
+    const bool cb_st = a.cpl_scale == 1.2345e-30f;
+#else
+    constexpr bool cb_st = true;
+#endif
     constexpr int PJ = (F8 && CPLB) ? 1 : 2;
     constexpr int PIT = PJ * 4;       // readback iterations (4 rows each) per pass
     // e4m3 operands (EPI_CPL_BWD): acc * f8_sa[0] * f8_sb[n], and with f8_cq the e4m3 copy of
@@ -514,7 +534,16 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
       float4 cv[PIT];
       float4 xp[PIT];
       ushort4 sp[PIT], xh[PIT];
+#ifdef NF_PROBE_CB_NOLOAD
+#pragma unroll
+      for (int it = 0; it < PIT; ++it) {
+        cv[it] = xp[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+        sp[it] = xh[it] = make_ushort4(0, 0, 0, 0);
+      }
+      if constexpr (EPI == EPI_F32_ACC || (CPLB && false)) {
+#else
       if constexpr (EPI == EPI_F32_ACC || CPLB) {
+#endif
 #pragma unroll
         for (int it = 0; it < PIT; ++it) {
           int m = m0 + hj * 16 * PJ + it * 4 + (lane >> 4), n = n0 + q * 4;
@@ -562,7 +591,7 @@ __device__ __forceinline__ void epi_tile_staged(const GemmArgs& a, const v4f (&a
           v[0] *= w8; v[1] *= w8; v[2] *= w8; v[3] *= w8;
         }
         const int m = m0 + hj * 16 * PJ + row, n = n0 + q * 4;
-        if (m < a.M && n < a.N) {
+        if (m < a.M && n < a.N && cb_st) {
           if constexpr (CPLB) {
             const float4 o = cv[it];
             const float gy[4] = {o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]};
