@@ -394,3 +394,19 @@ def test_engine_bf16_state_matches_fp32_state(gpu, precision):
         mk = b._mask(l)
         assert (b.params.g(f"l{l}.W1")[mk["M1"] == 0] == 0).all()
         assert (b.params.g(f"l{l}.W2")[mk["M2"] == 0] == 0).all()
+
+
+def test_bf16_state_option_is_gpu_only_cpu():
+    """KernelPaths.maf_bf16_state is a fused-GPU-engine option: on CPU (fp32 engine, no fused
+    kernels) it is ignored and the engine steps as before (same loss as without it)."""
+    from vi_normflows_amd.utils.config import KernelPaths
+
+    cfg = MAFEngineConfig(dim=16, hidden=32, n_layers=2, precision="fp32", init_out_std=0.3)
+    a = MAFEngine(cfg, batch=32, device="cpu", seed=3)
+    b = MAFEngine(dataclasses.replace(cfg, paths=KernelPaths(maf_bf16_state=True)), batch=32,
+                  device="cpu", seed=3)
+    assert not a.bf16_state and not b.bf16_state
+    for e in (a, b):
+        e.train_step()
+    assert torch.equal(a.loss, b.loss)
+    assert torch.equal(a.params.master, b.params.master)
